@@ -1,0 +1,102 @@
+"""In-tree build of the native library ``_pz_C.so`` (gfx950 HIP kernels + host C++ runtime).
+
+Usage: ``python -m penr_oz_neural_network_torch_amd._build [--force] [-j N]``
+
+* ``*.hip`` → ``hipcc --offload-arch=gfx950 -O3`` (device code, no torch headers: fast compiles)
+* ``*.cpp`` → ``g++ -O3`` with the torch / ROCm include paths (operator bindings, JSON formatter)
+* link  → ``hipcc -shared`` against libtorch / libc10_hip
+
+Objects are rebuilt only when their source or any header is newer; the ``.so`` lands next to
+this file so it travels with the repository snapshot (``gpurun``) and is the one the GPU tests
+load. No hipify, no ``torch.utils.cpp_extension`` JIT cache.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import glob
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+BUILD = os.path.join(PKG, "build")
+OUT = os.path.join(PKG, "_pz_C.so")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+
+def _torch_paths():
+    import torch
+    root = os.path.dirname(torch.__file__)
+    inc = [os.path.join(root, "include"), os.path.join(root, "include", "torch", "csrc", "api", "include")]
+    return inc, os.path.join(root, "lib"), int(torch._C._GLIBCXX_USE_CXX11_ABI)
+
+
+def _hipcc() -> str:
+    return shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+
+
+def _newest_header() -> float:
+    return max(os.path.getmtime(h) for h in glob.glob(os.path.join(CSRC, "*.h")))
+
+
+def _compile(src: str, force: bool) -> str:
+    obj = os.path.join(BUILD, os.path.basename(src) + ".o")
+    if not force and os.path.exists(obj):
+        if os.path.getmtime(obj) >= max(os.path.getmtime(src), _newest_header()):
+            return obj
+    if src.endswith(".hip"):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
+               "-I", CSRC, "-ffp-contract=fast", "-Wno-unused-result"]
+    else:
+        inc, _, abi = _torch_paths()
+        cmd = ["g++", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj, "-I", CSRC,
+               "-I", os.path.join(ROCM, "include"), "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
+               f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DTORCH_EXTENSION_NAME=_pz_C", "-Wno-deprecated-declarations"]
+        for i in inc:
+            cmd += ["-isystem", i]
+        cmd += ["-isystem", sysconfig.get_paths()["include"]]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    return obj
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    sources = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+    jobs = jobs or min(len(sources), int(os.environ.get("MAX_JOBS", os.cpu_count() or 4)), 16)
+    with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(lambda s: _compile(s, force), sources))
+    if not force and os.path.exists(OUT) and os.path.getmtime(OUT) >= max(os.path.getmtime(o) for o in objs):
+        if verbose:
+            print(f"[pz build] up to date: {OUT}")
+        return OUT
+    _, libdir, _ = _torch_paths()
+    tmp = OUT + ".tmp"
+    cmd = [_hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp, "-L", libdir,
+           "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip", f"-Wl,-rpath,{libdir}"]
+    res = subprocess.run(cmd, capture_output=True, text=True)
+    if res.returncode != 0:
+        raise RuntimeError(f"link failed: {' '.join(cmd)}\n{res.stdout}\n{res.stderr}")
+    os.replace(tmp, OUT)
+    if verbose:
+        print(f"[pz build] built {OUT}")
+    return OUT
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    args = ap.parse_args(argv)
+    build(force=args.force, jobs=args.jobs)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,531 @@
+// torch.ops.pz — registers every native kernel of the framework as a PyTorch operator.
+//
+// Device ops are registered for the CUDA dispatch key (which is the HIP device on ROCm builds of
+// PyTorch) and launch on PyTorch's current HIP stream, so they order correctly with the caching
+// allocator, RCCL collectives issued through torch.distributed, and hipGraph capture.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPStream.h>
+#include <torch/library.h>
+
+#include <cstring>
+#include <vector>
+
+#include "json_format.h"
+#include "pz_kernels.h"
+
+namespace {
+
+using at::Tensor;
+using c10::optional;
+
+#define PZ_HIP_CHECK(expr)                                                                   \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    TORCH_CHECK(_e == hipSuccess, "pz: HIP error ", hipGetErrorString(_e), " in " #expr);    \
+  } while (0)
+
+hipStream_t cur_stream(const Tensor& t) { return c10::hip::getCurrentHIPStream(t.device().index()).stream(); }
+
+int dt_of(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kBFloat16: return pz::DT_BF16;
+    case at::kFloat: return pz::DT_F32;
+    case at::kDouble: return pz::DT_F64;
+    case at::kFloat8_e4m3fn: return pz::DT_FP8;
+    default: TORCH_CHECK(false, "pz: unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), "pz: ", name, " must be a GPU tensor");
+}
+
+template <typename T = void>
+T* ptr_or_null(const optional<Tensor>& t) {
+  return t.has_value() && t->defined() ? static_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
+  pz::EpiSpec e{};
+  e.act = pz::ACT_NONE;
+  e.drop_pre = -1;
+  e.drop_post = -1;
+  e.scale = 1.f;
+  e.inv_scale = 1.f;
+  if (ei.size() >= 7) {
+    e.act = static_cast<int>(ei[0]);
+    e.drop_pre = static_cast<int>(ei[1]);
+    e.drop_post = static_cast<int>(ei[2]);
+    e.seed_lo = static_cast<uint32_t>(ei[3]);
+    e.seed_hi = static_cast<uint32_t>(ei[4]);
+    e.thresh16 = static_cast<uint32_t>(ei[5]);
+    e.drop_all = static_cast<int>(ei[6]);
+  }
+  if (ef.size() >= 2) {
+    e.scale = static_cast<float>(ef[0]);
+    e.inv_scale = static_cast<float>(ef[1]);
+  }
+  return e;
+}
+
+// ------------------------------------------------------------------------------------ GEMM
+pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C,
+                       const optional<Tensor>& bias, const optional<Tensor>& aux, const optional<Tensor>& colsum,
+                       int64_t epi_mode, at::IntArrayRef epi_i, at::ArrayRef<double> epi_f, double alpha,
+                       bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld, bool force_generic) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "pz::gemm: 2-D operands expected");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "pz::gemm: unit inner stride expected");
+  TORCH_CHECK(A.scalar_type() == B.scalar_type(), "pz::gemm: A/B dtype mismatch");
+  TORCH_CHECK(a_kc ? (A.size(0) >= M && A.size(1) >= K) : (A.size(0) >= K && A.size(1) >= M), "pz::gemm: A shape");
+  TORCH_CHECK(b_kc ? (B.size(0) >= N && B.size(1) >= K) : (B.size(0) >= K && B.size(1) >= N), "pz::gemm: B shape");
+  TORCH_CHECK(C.size(0) >= M && C.size(1) >= N, "pz::gemm: C shape");
+  pz::GemmArgs p{};
+  p.A = A.data_ptr();
+  p.B = B.data_ptr();
+  p.C = C.data_ptr();
+  p.M = static_cast<int>(M);
+  p.N = static_cast<int>(N);
+  p.K = static_cast<int>(K);
+  p.lda = A.stride(0);
+  p.ldb = B.stride(0);
+  p.ldc = C.stride(0);
+  p.a_kc = a_kc;
+  p.b_kc = b_kc;
+  p.in_dtype = dt_of(A);
+  p.out_dtype = dt_of(C);
+  p.alpha = static_cast<float>(alpha);
+  p.accumulate = accumulate;
+  if (bias.has_value() && bias->defined()) {
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() >= N, "pz::gemm: bias");
+    p.bias = bias->data_ptr<float>();
+  }
+  if (aux.has_value() && aux->defined()) {
+    TORCH_CHECK(aux->dim() == 2 && aux->stride(1) == 1 && aux->size(0) >= M && aux->size(1) >= N, "pz::gemm: aux");
+    p.aux = aux->data_ptr();
+    p.ldaux = aux->stride(0);
+    p.aux_dtype = dt_of(*aux);
+  }
+  if (colsum.has_value() && colsum->defined()) {
+    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->numel() >= N, "pz::gemm: colsum must be fp32 [N]");
+    p.colsum = colsum->data_ptr<float>();
+  }
+  p.epi_mode = static_cast<int>(epi_mode);
+  p.epi = make_epi(epi_i, epi_f);
+  p.idx_ld = idx_ld > 0 ? idx_ld : N;
+  p.force_generic = force_generic;
+  return p;
+}
+
+void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, const optional<Tensor>& bias,
+             const optional<Tensor>& aux, const optional<Tensor>& colsum, int64_t epi_mode, at::IntArrayRef epi_i,
+             at::ArrayRef<double> epi_f, double alpha, bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld,
+             bool force_generic) {
+  check_dev(A, "A");
+  auto p = gemm_args(A, a_kc, B, b_kc, C, bias, aux, colsum, epi_mode, epi_i, epi_f, alpha, accumulate, M, N, K, idx_ld,
+                     force_generic);
+  PZ_HIP_CHECK(pz::gemm(p, cur_stream(A)));
+}
+
+int64_t gemm_path_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, int64_t M, int64_t N,
+                     int64_t K) {
+  auto p = gemm_args(A, a_kc, B, b_kc, C, c10::nullopt, c10::nullopt, c10::nullopt, 0, {}, {}, 1.0, false, M, N, K, 0,
+                     false);
+  return pz::gemm_path(p);
+}
+
+// ------------------------------------------------------------------------------ elementwise
+void stage_fwd_op(const Tensor& x, const Tensor& y, at::IntArrayRef ei, at::ArrayRef<double> ef) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "pz::stage_fwd: contiguous x/y");
+  PZ_HIP_CHECK(pz::stage_fwd(x.data_ptr(), dt_of(x), y.data_ptr(), dt_of(y), x.numel(), make_epi(ei, ef), cur_stream(x)));
+}
+
+void stage_bwd_op(const Tensor& g, const Tensor& y, const Tensor& dx, at::IntArrayRef ei, at::ArrayRef<double> ef) {
+  check_dev(g, "g");
+  TORCH_CHECK(g.is_contiguous() && y.is_contiguous() && dx.is_contiguous(), "pz::stage_bwd: contiguous tensors");
+  TORCH_CHECK(g.scalar_type() == y.scalar_type() && g.scalar_type() == dx.scalar_type(), "pz::stage_bwd: dtypes");
+  PZ_HIP_CHECK(pz::stage_bwd(g.data_ptr(), y.data_ptr(), dx.data_ptr(), dt_of(g), g.numel(), make_epi(ei, ef),
+                             cur_stream(g)));
+}
+
+void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid, const optional<Tensor>& loss,
+                  double loss_scale, const optional<Tensor>& dh, double grad_scale, const optional<Tensor>& colsum,
+                  const optional<Tensor>& probs, at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld) {
+  check_dev(logits, "logits");
+  TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "pz::xent_head: 2-D logits");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "pz::xent_head: int64 labels");
+  pz::XentArgs a{};
+  a.logits = logits.data_ptr();
+  a.ld = logits.stride(0);
+  a.labels = labels.data_ptr<int64_t>();
+  a.rows = static_cast<int>(logits.size(0));
+  a.rows_valid = static_cast<int>(rows_valid);
+  a.cols = static_cast<int>(logits.size(1));
+  a.dtype = dt_of(logits);
+  a.loss = ptr_or_null<float>(loss);
+  a.loss_scale = static_cast<float>(loss_scale);
+  if (dh.has_value() && dh->defined()) {
+    TORCH_CHECK(dh->scalar_type() == logits.scalar_type() && dh->stride(1) == 1, "pz::xent_head: dh");
+    a.dh = dh->data_ptr();
+    a.ld_dh = dh->stride(0);
+  }
+  a.grad_scale = static_cast<float>(grad_scale);
+  a.colsum = ptr_or_null<float>(colsum);
+  if (probs.has_value() && probs->defined()) {
+    TORCH_CHECK(probs->scalar_type() == logits.scalar_type() && probs->stride(1) == 1, "pz::xent_head: probs");
+    a.probs = probs->data_ptr();
+    a.ld_probs = probs->stride(0);
+  }
+  a.epi = make_epi(ei, ef);
+  a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
+  PZ_HIP_CHECK(pz::xent_head(a, cur_stream(logits)));
+}
+
+void mse_head_op(const Tensor& y, const Tensor& target, int64_t rows_valid, const optional<Tensor>& loss,
+                 double loss_scale, const optional<Tensor>& dh, double grad_scale, const optional<Tensor>& colsum,
+                 at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld) {
+  check_dev(y, "y");
+  TORCH_CHECK(y.dim() == 2 && target.dim() == 2 && y.stride(1) == 1 && target.stride(1) == 1, "pz::mse_head: 2-D");
+  TORCH_CHECK(y.scalar_type() == target.scalar_type(), "pz::mse_head: dtype mismatch");
+  pz::MseArgs a{};
+  a.y = y.data_ptr();
+  a.ld_y = y.stride(0);
+  a.target = target.data_ptr();
+  a.ld_t = target.stride(0);
+  a.rows = static_cast<int>(y.size(0));
+  a.rows_valid = static_cast<int>(rows_valid);
+  a.cols = static_cast<int>(y.size(1));
+  a.dtype = dt_of(y);
+  a.loss = ptr_or_null<float>(loss);
+  a.loss_scale = static_cast<float>(loss_scale);
+  if (dh.has_value() && dh->defined()) {
+    a.dh = dh->data_ptr();
+    a.ld_dh = dh->stride(0);
+  }
+  a.grad_scale = static_cast<float>(grad_scale);
+  a.colsum = ptr_or_null<float>(colsum);
+  a.epi = make_epi(ei, ef);
+  a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
+  PZ_HIP_CHECK(pz::mse_head(a, cur_stream(y)));
+}
+
+void softmax_rows_op(const Tensor& x, const Tensor& y) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.scalar_type() == y.scalar_type(), "pz::softmax_rows");
+  const int cols = static_cast<int>(x.size(-1));
+  const int rows = static_cast<int>(x.numel() / std::max<int64_t>(cols, 1));
+  PZ_HIP_CHECK(pz::softmax_rows(x.data_ptr(), y.data_ptr(), dt_of(x), rows, cols, cur_stream(x)));
+}
+
+void softmax_bwd_op(const Tensor& g, const Tensor& y, const Tensor& dx) {
+  check_dev(g, "g");
+  TORCH_CHECK(g.is_contiguous() && y.is_contiguous() && dx.is_contiguous(), "pz::softmax_bwd");
+  const int cols = static_cast<int>(y.size(-1));
+  const int rows = static_cast<int>(y.numel() / std::max<int64_t>(cols, 1));
+  PZ_HIP_CHECK(pz::softmax_bwd(g.data_ptr(), y.data_ptr(), dx.data_ptr(), dt_of(y), rows, cols, cur_stream(g)));
+}
+
+void colsum_op(const Tensor& x, const Tensor& out) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && out.scalar_type() == at::kFloat, "pz::colsum");
+  const int cols = static_cast<int>(x.size(-1));
+  const int rows = static_cast<int>(x.numel() / std::max<int64_t>(cols, 1));
+  PZ_HIP_CHECK(pz::colsum(x.data_ptr(), dt_of(x), out.data_ptr<float>(), rows, cols, cur_stream(x)));
+}
+
+void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t seed_lo, int64_t seed_hi,
+                    const Tensor& out, int64_t rows_valid, const optional<Tensor>& labels_in,
+                    const optional<Tensor>& labels_out, const optional<Tensor>& picked) {
+  check_dev(data, "data");
+  TORCH_CHECK(data.dim() == 2 && out.dim() == 2 && data.stride(1) == 1 && out.stride(1) == 1, "pz::gather_rows: 2-D");
+  TORCH_CHECK(out.size(1) == data.size(1), "pz::gather_rows: width mismatch");
+  pz::GatherArgs a{};
+  a.data = data.data_ptr();
+  a.ld_data = data.stride(0);
+  a.data_dtype = dt_of(data);
+  a.n_data = data.size(0);
+  a.indices = ptr_or_null<const int64_t>(indices);
+  a.seed_lo = static_cast<uint32_t>(seed_lo);
+  a.seed_hi = static_cast<uint32_t>(seed_hi);
+  a.out = out.data_ptr();
+  a.ld_out = out.stride(0);
+  a.out_dtype = dt_of(out);
+  a.rows = static_cast<int>(out.size(0));
+  a.rows_valid = static_cast<int>(rows_valid);
+  a.cols = static_cast<int>(out.size(1));
+  a.labels_in = ptr_or_null<const int64_t>(labels_in);
+  a.labels_out = ptr_or_null<int64_t>(labels_out);
+  a.picked = ptr_or_null<int64_t>(picked);
+  PZ_HIP_CHECK(pz::gather_rows(a, cur_stream(data)));
+}
+
+// ------------------------------------------------------------------------------- optimizer
+Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::IntArrayRef is_weight,
+                        at::IntArrayRef stat_slot, at::ArrayRef<optional<Tensor>> shadows) {
+  const size_t n = offsets.size();
+  TORCH_CHECK(numels.size() == n && is_weight.size() == n && stat_slot.size() == n && shadows.size() == n,
+              "pz::pack_segments: length mismatch");
+  Tensor out = at::empty({static_cast<int64_t>(n * sizeof(pz::OptSegment))}, at::TensorOptions().dtype(at::kByte));
+  auto* segs = reinterpret_cast<pz::OptSegment*>(out.data_ptr<uint8_t>());
+  for (size_t i = 0; i < n; ++i) {
+    pz::OptSegment s{};
+    s.offset = offsets[i];
+    s.numel = numels[i];
+    s.is_weight = static_cast<int>(is_weight[i]);
+    s.stat_slot = static_cast<int>(stat_slot[i]);
+    const auto& sh = shadows[i];
+    if (sh.has_value() && sh->defined()) {
+      TORCH_CHECK(sh->is_contiguous() && sh->numel() == numels[i], "pz::pack_segments: shadow shape");
+      s.shadow = sh->data_ptr();
+      s.shadow_dtype = dt_of(*sh);
+    }
+    std::memcpy(segs + i, &s, sizeof(s));
+  }
+  return out;
+}
+
+void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional<Tensor>& exp_avg,
+                       const optional<Tensor>& exp_avg_sq, const Tensor& segments, const Tensor& block_seg,
+                       int64_t num_segments, int64_t total_blocks, bool adam, double lr, double beta1, double beta2,
+                       double eps, double bias_c1, double bias_c2_sqrt, double grad_scale, double l2,
+                       const optional<Tensor>& stats) {
+  check_dev(params, "params");
+  TORCH_CHECK(params.scalar_type() == at::kFloat && grads.scalar_type() == at::kFloat, "pz::optimizer_step: fp32 master");
+  pz::OptArgs a{};
+  a.params = params.data_ptr<float>();
+  a.grads = grads.data_ptr<float>();
+  a.exp_avg = ptr_or_null<float>(exp_avg);
+  a.exp_avg_sq = ptr_or_null<float>(exp_avg_sq);
+  TORCH_CHECK(!adam || (a.exp_avg && a.exp_avg_sq), "pz::optimizer_step: Adam needs moment buffers");
+  a.segments = reinterpret_cast<const pz::OptSegment*>(segments.data_ptr());
+  a.num_segments = static_cast<int>(num_segments);
+  a.block_seg = block_seg.data_ptr<int64_t>();
+  a.total_blocks = static_cast<int>(total_blocks);
+  a.adam = adam;
+  a.lr = static_cast<float>(lr);
+  a.beta1 = static_cast<float>(beta1);
+  a.beta2 = static_cast<float>(beta2);
+  a.eps = static_cast<float>(eps);
+  a.bias_c1 = static_cast<float>(bias_c1);
+  a.bias_c2_sqrt = static_cast<float>(bias_c2_sqrt);
+  a.grad_scale = static_cast<float>(grad_scale);
+  a.l2_lambda = static_cast<float>(l2);
+  a.stats = ptr_or_null<double>(stats);
+  PZ_HIP_CHECK(pz::optimizer_step(a, cur_stream(params)));
+}
+
+void segment_stats_op(const Tensor& params, const Tensor& segments, const Tensor& block_seg, int64_t num_segments,
+                      int64_t total_blocks, const Tensor& stats) {
+  check_dev(params, "params");
+  PZ_HIP_CHECK(pz::segment_stats(params.data_ptr<float>(), reinterpret_cast<const pz::OptSegment*>(segments.data_ptr()),
+                                 block_seg.data_ptr<int64_t>(), static_cast<int>(num_segments),
+                                 static_cast<int>(total_blocks), stats.data_ptr<double>(), cur_stream(params)));
+}
+
+// ----------------------------------------------------------------------------------- stats
+void tensor_moments_op(const Tensor& x, int64_t row_len, int64_t rule, double thr, const Tensor& out) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && out.scalar_type() == at::kDouble && out.numel() >= 8, "pz::tensor_moments");
+  PZ_HIP_CHECK(pz::tensor_moments(x.data_ptr(), dt_of(x), x.numel(), row_len, static_cast<int>(rule),
+                                  static_cast<float>(thr), out.data_ptr<double>(), cur_stream(x)));
+}
+
+void histogram_op(const Tensor& x, const Tensor& range, int64_t bins, const Tensor& counts) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && range.scalar_type() == at::kDouble && counts.scalar_type() == at::kFloat,
+              "pz::histogram");
+  PZ_HIP_CHECK(pz::histogram(x.data_ptr(), dt_of(x), x.numel(), range.data_ptr<double>(), static_cast<int>(bins),
+                             counts.data_ptr<float>(), cur_stream(x)));
+}
+
+// ------------------------------------------------------------------------------- batchnorm
+void batchnorm_fwd_op(const Tensor& x, const Tensor& y, const Tensor& gain, const Tensor& bias,
+                      const Tensor& running_mean, const Tensor& running_var, double eps, double momentum, bool training,
+                      int64_t rows_valid, const Tensor& save_mean, const Tensor& save_invstd, const Tensor& partial,
+                      at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "pz::batchnorm_fwd: contiguous");
+  TORCH_CHECK(gain.scalar_type() == bias.scalar_type() && gain.scalar_type() == running_mean.scalar_type() &&
+                  running_mean.is_contiguous() && running_var.is_contiguous(),
+              "pz::batchnorm_fwd: parameter dtypes");
+  pz::BnArgs a{};
+  a.x = x.data_ptr();
+  a.y = y.data_ptr();
+  a.dtype = dt_of(x);
+  a.cols = static_cast<int>(x.size(-1));
+  a.rows = static_cast<int>(x.numel() / std::max<int64_t>(a.cols, 1));
+  a.rows_valid = static_cast<int>(rows_valid);
+  a.gain = gain.data_ptr();
+  a.bias = bias.data_ptr();
+  a.param_dtype = dt_of(gain);
+  a.running_mean = running_mean.data_ptr();
+  a.running_var = running_var.data_ptr();
+  a.eps = static_cast<float>(eps);
+  a.momentum = static_cast<float>(momentum);
+  a.training = training;
+  a.save_mean = save_mean.data_ptr<float>();
+  a.save_invstd = save_invstd.data_ptr<float>();
+  a.partial = partial.data_ptr<double>();
+  a.epi = make_epi(ei, ef);
+  a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
+  PZ_HIP_CHECK(pz::batchnorm_fwd(a, cur_stream(x)));
+}
+
+void batchnorm_bwd_op(const Tensor& g, const Tensor& y, const Tensor& x, const optional<Tensor>& dx, const Tensor& gain,
+                      const Tensor& bias, const Tensor& save_mean, const Tensor& save_invstd,
+                      const optional<Tensor>& dgain, const optional<Tensor>& dbias, const Tensor& partial,
+                      int64_t rows_valid, at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld) {
+  check_dev(g, "g");
+  TORCH_CHECK(g.is_contiguous() && y.is_contiguous() && x.is_contiguous(), "pz::batchnorm_bwd: contiguous");
+  pz::BnBwdArgs a{};
+  a.g = g.data_ptr();
+  a.y = y.data_ptr();
+  a.x = x.data_ptr();
+  a.dx = ptr_or_null(dx);
+  a.dtype = dt_of(x);
+  a.cols = static_cast<int>(x.size(-1));
+  a.rows = static_cast<int>(x.numel() / std::max<int64_t>(a.cols, 1));
+  a.rows_valid = static_cast<int>(rows_valid);
+  a.gain = gain.data_ptr();
+  a.bias = bias.data_ptr();
+  a.param_dtype = dt_of(gain);
+  a.save_mean = save_mean.data_ptr<float>();
+  a.save_invstd = save_invstd.data_ptr<float>();
+  a.dgain = ptr_or_null(dgain);
+  a.dbias = ptr_or_null(dbias);
+  a.partial = partial.data_ptr<double>();
+  a.epi = make_epi(ei, ef);
+  a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
+  PZ_HIP_CHECK(pz::batchnorm_bwd(a, cur_stream(g)));
+}
+
+// ------------------------------------------------------------------------------- embedding
+int idx_type(const Tensor& idx) {
+  switch (idx.scalar_type()) {
+    case at::kLong: return pz::IDX_I64;
+    case at::kFloat: return pz::IDX_F32;
+    case at::kDouble: return pz::IDX_F64;
+    default: TORCH_CHECK(false, "pz: embedding ids must be int64, float32 or float64");
+  }
+  return -1;
+}
+
+void embedding_fwd_op(const Tensor& table, const Tensor& idx, const Tensor& out) {
+  check_dev(table, "table");
+  TORCH_CHECK(idx.is_contiguous() && out.is_contiguous() && table.is_contiguous(), "pz::embedding_fwd: contiguous");
+  const int dim = static_cast<int>(table.size(1));
+  TORCH_CHECK(out.numel() == idx.numel() * dim, "pz::embedding_fwd: out shape");
+  PZ_HIP_CHECK(pz::embedding_fwd(table.data_ptr(), dt_of(table), idx.data_ptr(), idx_type(idx), idx.numel(), dim,
+                                 out.data_ptr(), dt_of(out), cur_stream(table)));
+}
+
+void embedding_bwd_op(const Tensor& dout, const Tensor& idx, const Tensor& dtable) {
+  check_dev(dout, "dout");
+  TORCH_CHECK(idx.is_contiguous() && dout.is_contiguous() && dtable.is_contiguous(), "pz::embedding_bwd: contiguous");
+  const int dim = static_cast<int>(dtable.size(1));
+  PZ_HIP_CHECK(pz::embedding_bwd(dout.data_ptr(), dt_of(dout), idx.data_ptr(), idx_type(idx), idx.numel(), dim,
+                                 dtable.data_ptr(), dt_of(dtable), cur_stream(dout)));
+}
+
+void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tensor& stats_prev, const Tensor& stats_cur,
+                      const Tensor& slot_numel, int64_t nslots, double l2, const Tensor& costs, int64_t epoch,
+                      const Tensor& ratios, int64_t ratio_row) {
+  check_dev(costs, "costs");
+  TORCH_CHECK(epoch >= 0 && epoch < costs.numel(), "pz::step_finalize: epoch out of range");
+  TORCH_CHECK(ratio_row < 0 || (ratio_row + 1) * nslots <= ratios.numel(), "pz::step_finalize: ratio row out of range");
+  pz::FinalizeArgs a{};
+  a.loss = ptr_or_null<const float>(loss);
+  a.loss_div = static_cast<float>(loss_div);
+  a.stats_prev = stats_prev.data_ptr<double>();
+  a.stats_cur = stats_cur.data_ptr<double>();
+  a.slot_numel = slot_numel.data_ptr<double>();
+  a.nslots = static_cast<int>(nslots);
+  a.l2 = static_cast<float>(l2);
+  a.costs = costs.data_ptr<float>();
+  a.epoch = static_cast<int>(epoch);
+  a.ratios = ratios.data_ptr<float>();
+  a.ratio_row = static_cast<int>(ratio_row);
+  PZ_HIP_CHECK(pz::step_finalize(a, cur_stream(costs)));
+}
+
+// ----------------------------------------------------------------------------- host (N9)
+std::string format_json_array_op(const Tensor& t, int64_t level) {
+  TORCH_CHECK(!t.is_cuda() && t.scalar_type() == at::kDouble, "pz::format_json_array: CPU float64 tensor expected");
+  std::vector<int64_t> shape(t.sizes().begin(), t.sizes().end());
+  std::vector<int64_t> strides(t.strides().begin(), t.strides().end());
+  return pz::format_json_array(t.data_ptr<double>(), shape.data(), strides.data(), static_cast<int>(t.dim()), level);
+}
+
+std::string repr_double_op(double x) { return pz::repr_double(x); }
+
+}  // namespace
+
+TORCH_LIBRARY(pz, m) {
+  m.def("gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor(a!) C, Tensor? bias, Tensor? aux, Tensor(b!)? colsum, "
+        "int epi_mode, int[] epi_i, float[] epi_f, float alpha, bool accumulate, int M, int N, int K, int idx_ld, "
+        "bool force_generic) -> ()");
+  m.def("gemm_path(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor C, int M, int N, int K) -> int");
+  m.def("stage_fwd(Tensor x, Tensor(a!) y, int[] epi_i, float[] epi_f) -> ()");
+  m.def("stage_bwd(Tensor g, Tensor y, Tensor(a!) dx, int[] epi_i, float[] epi_f) -> ()");
+  m.def("xent_head(Tensor logits, Tensor labels, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "
+        "float grad_scale, Tensor(c!)? colsum, Tensor(d!)? probs, int[] epi_i, float[] epi_f, int idx_ld) -> ()");
+  m.def("mse_head(Tensor y, Tensor target, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "
+        "float grad_scale, Tensor(c!)? colsum, int[] epi_i, float[] epi_f, int idx_ld) -> ()");
+  m.def("softmax_rows(Tensor x, Tensor(a!) y) -> ()");
+  m.def("softmax_bwd(Tensor g, Tensor y, Tensor(a!) dx) -> ()");
+  m.def("colsum(Tensor x, Tensor(a!) out) -> ()");
+  m.def("gather_rows(Tensor data, Tensor? indices, int seed_lo, int seed_hi, Tensor(a!) out, int rows_valid, "
+        "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked) -> ()");
+  m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows) -> Tensor");
+  m.def("optimizer_step(Tensor(a!) params, Tensor grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
+        "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
+        "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats) -> ()");
+  m.def("segment_stats(Tensor params, Tensor segments, Tensor block_seg, int num_segments, int total_blocks, "
+        "Tensor(a!) stats) -> ()");
+  m.def("tensor_moments(Tensor x, int row_len, int rule, float thr, Tensor(a!) out) -> ()");
+  m.def("histogram(Tensor x, Tensor range, int bins, Tensor(a!) counts) -> ()");
+  m.def("batchnorm_fwd(Tensor x, Tensor(a!) y, Tensor gain, Tensor bias, Tensor(b!) running_mean, "
+        "Tensor(c!) running_var, float eps, float momentum, bool training, int rows_valid, Tensor(d!) save_mean, "
+        "Tensor(e!) save_invstd, Tensor(f!) partial, int[] epi_i, float[] epi_f, int idx_ld) -> ()");
+  m.def("batchnorm_bwd(Tensor g, Tensor y, Tensor x, Tensor(a!)? dx, Tensor gain, Tensor bias, Tensor save_mean, "
+        "Tensor save_invstd, Tensor(b!)? dgain, Tensor(c!)? dbias, Tensor(d!) partial, int rows_valid, int[] epi_i, "
+        "float[] epi_f, int idx_ld) -> ()");
+  m.def("embedding_fwd(Tensor table, Tensor idx, Tensor(a!) out) -> ()");
+  m.def("embedding_bwd(Tensor dout, Tensor idx, Tensor(a!) dtable) -> ()");
+  m.def("step_finalize(Tensor? loss, float loss_div, Tensor(a!) stats_prev, Tensor stats_cur, Tensor slot_numel, "
+        "int nslots, float l2, Tensor(b!) costs, int epoch, Tensor(c!) ratios, int ratio_row) -> ()");
+  m.def("format_json_array(Tensor t, int level) -> str");
+  m.def("repr_double(float x) -> str");
+}
+
+TORCH_LIBRARY_IMPL(pz, CUDA, m) {
+  m.impl("gemm", TORCH_FN(gemm_op));
+  m.impl("gemm_path", TORCH_FN(gemm_path_op));
+  m.impl("stage_fwd", TORCH_FN(stage_fwd_op));
+  m.impl("stage_bwd", TORCH_FN(stage_bwd_op));
+  m.impl("xent_head", TORCH_FN(xent_head_op));
+  m.impl("mse_head", TORCH_FN(mse_head_op));
+  m.impl("softmax_rows", TORCH_FN(softmax_rows_op));
+  m.impl("softmax_bwd", TORCH_FN(softmax_bwd_op));
+  m.impl("colsum", TORCH_FN(colsum_op));
+  m.impl("gather_rows", TORCH_FN(gather_rows_op));
+  m.impl("optimizer_step", TORCH_FN(optimizer_step_op));
+  m.impl("segment_stats", TORCH_FN(segment_stats_op));
+  m.impl("tensor_moments", TORCH_FN(tensor_moments_op));
+  m.impl("histogram", TORCH_FN(histogram_op));
+  m.impl("batchnorm_fwd", TORCH_FN(batchnorm_fwd_op));
+  m.impl("batchnorm_bwd", TORCH_FN(batchnorm_bwd_op));
+  m.impl("embedding_fwd", TORCH_FN(embedding_fwd_op));
+  m.impl("embedding_bwd", TORCH_FN(embedding_bwd_op));
+  m.impl("step_finalize", TORCH_FN(step_finalize_op));
+}
+
+TORCH_LIBRARY_IMPL(pz, CPU, m) {
+  m.impl("format_json_array", TORCH_FN(format_json_array_op));
+}
+
+TORCH_LIBRARY_IMPL(pz, CompositeExplicitAutograd, m) {
+  m.impl("pack_segments", TORCH_FN(pack_segments_op));
+  m.impl("repr_double", TORCH_FN(repr_double_op));
+}

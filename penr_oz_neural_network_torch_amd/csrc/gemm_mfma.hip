@@ -1,0 +1,343 @@
+// N1 — bf16 MFMA GEMM for gfx950 with fused MLP epilogues.
+//
+// Replaces the reference's three per-layer matmuls (neural_net_model.py:117 forward `x @ W`, and
+// autograd's two `mm` for dX / dW) plus the bias add (:119), activation (:172-184), dropout (:395)
+// and bias-gradient column sum that surround them.
+//
+// Design (CDNA4-first, see /opt/skills/guides/cdna_hip_programming.md §5):
+//  * 16x16x32 bf16 MFMA (v_mfma_f32_16x16x32_bf16), fp32 accumulation. Operands are issued
+//    SWAPPED (mfma(B, A)) so each lane ends up owning 4 consecutive output COLUMNS of one row:
+//    the epilogue then loads bias / aux and stores C with 8-16 B per lane.
+//  * Both operand layouts are first-class: a K-contiguous operand is staged as [rows][64]
+//    (128-B rows, XOR-swizzled 16-B chunks, read with ds_read_b128); an M/N-contiguous operand
+//    (the reference's [in,out] weights in the forward, activations in dW = Xᵀ·dH) is staged as
+//    [64][rows] and read with the gfx950 transposing ds_read_b64_tr_b16 — no transpose kernels,
+//    no second weight copy.
+//  * global→LDS by global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave-instruction), two LDS
+//    buffers, next tile issued before the current tile's MFMAs (2-phase pipeline, T3/T4 minimum).
+//    Swizzle is applied on the per-lane SOURCE address + the read (rule 21): LDS image stays
+//    lane-linear as the DMA requires.
+//  * XCD-aware bijective block remap (T1) + grouped tile order for L2 reuse.
+//  * Tile configs 256x256 (8 waves), 256x128 (8 waves), 128x128 (4 waves, 2 blocks/CU) chosen
+//    per shape so the grid covers the 256 CUs.
+#include <type_traits>
+
+#include "pz_common.h"
+#include "pz_launch.h"
+
+namespace pz {
+namespace {
+
+constexpr int kBK = 64;
+
+PZ_DEV int swz_kc(int row) { return (row >> 1) & 7; }
+PZ_DEV int swz_mn(int krow) { return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1; }
+
+template <int BM, int BN, int WM, int WN>
+struct Cfg {
+  static constexpr int NW = WM * WN;
+  static constexpr int NT = NW * 64;
+  static constexpr int WTM = BM / WM;
+  static constexpr int WTN = BN / WN;
+  static constexpr int TM = WTM / 16;
+  static constexpr int TN = WTN / 16;
+  static constexpr int A_BYTES = BM * kBK * 2;
+  static constexpr int B_BYTES = BN * kBK * 2;
+  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
+  static constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+  static_assert(TM >= 1 && TN >= 1, "wave tile must hold at least one 16x16 MFMA tile");
+  static_assert((BM * 128) % (1024 * NW) == 0 && (BN * 128) % (1024 * NW) == 0, "stage split");
+};
+
+// K-contiguous operand rows [row0, row0+R) x k [k0, k0+64) -> LDS [R][64] (128-B rows)
+template <int R, int NW>
+PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
+                     PZ_LDS char* tile, int wave, int lane) {
+  constexpr int INSTR = R / (8 * NW);
+#pragma unroll
+  for (int i = 0; i < INSTR; ++i) {
+    const int rbase = (wave * INSTR + i) * 8;
+    const int r = rbase + (lane >> 3);
+    const int chunk = (lane & 7) ^ swz_kc(r);
+    int gr = row0 + r;
+    gr = gr < rows_valid ? gr : rows_valid - 1;
+    const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
+    __builtin_amdgcn_global_load_lds(src, (PZ_LDS void*)(tile + rbase * 128), 16, 0, 0);
+  }
+}
+
+// M/N-contiguous operand: k rows [k0, k0+64) x cols [col0, col0+R) -> LDS [64][R]
+template <int R, int NW>
+PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int cols_valid, int k0,
+                     PZ_LDS char* tile, int wave, int lane) {
+  constexpr int ROW_BYTES = R * 2;
+  constexpr int CHUNKS = R / 8;
+  constexpr int ROWS_PER = 1024 / ROW_BYTES;
+  constexpr int INSTR = (64 * ROW_BYTES) / (1024 * NW);
+#pragma unroll
+  for (int i = 0; i < INSTR; ++i) {
+    const int kbase = (wave * INSTR + i) * ROWS_PER;
+    const int kr = kbase + lane / CHUNKS;
+    const int chunk = (lane % CHUNKS) ^ swz_mn(kr);
+    int gc = col0 + chunk * 8;
+    gc = gc < cols_valid ? gc : cols_valid - 8;
+    const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
+    __builtin_amdgcn_global_load_lds(src, (PZ_LDS void*)(tile + kbase * ROW_BYTES), 16, 0, 0);
+  }
+}
+
+PZ_DEV i16x8_t frag_kc(const PZ_LDS char* tile, int row, int chunk) {
+  const int slot = chunk ^ swz_kc(row);
+  return *reinterpret_cast<const PZ_LDS i16x8_t*>(tile + row * 128 + slot * 16);
+}
+
+template <int R>
+PZ_DEV i16x8_t frag_mn(const PZ_LDS char* tile, int col16, int kbase, int lane) {
+  const int q = (lane >> 2) & 3;
+  const int p = lane & 3;
+  const int col = col16 + 4 * p;
+  const int chunk = col >> 3;
+  const int within = (col & 7) * 2;
+  const int k0 = kbase + q;
+  const int k1 = k0 + 4;
+  const PZ_LDS char* a0 = tile + k0 * (R * 2) + ((chunk ^ swz_mn(k0)) << 4) + within;
+  const PZ_LDS char* a1 = tile + k1 * (R * 2) + ((chunk ^ swz_mn(k1)) << 4) + within;
+  i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<PZ_LDS i16x4_t*>(const_cast<PZ_LDS char*>(a0)));
+  i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<PZ_LDS i16x4_t*>(const_cast<PZ_LDS char*>(a1)));
+  return i16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <typename OutT>
+PZ_DEV void load4(const OutT* p, float v[4]);
+template <>
+PZ_DEV void load4<uint16_t>(const uint16_t* p, float v[4]) {
+  const uint2 u = *reinterpret_cast<const uint2*>(p);
+  v[0] = bf2f(u.x & 0xFFFF); v[1] = bf2f(u.x >> 16); v[2] = bf2f(u.y & 0xFFFF); v[3] = bf2f(u.y >> 16);
+}
+template <>
+PZ_DEV void load4<float>(const float* p, float v[4]) {
+  const float4 u = *reinterpret_cast<const float4*>(p);
+  v[0] = u.x; v[1] = u.y; v[2] = u.z; v[3] = u.w;
+}
+template <typename OutT>
+PZ_DEV void store4(OutT* p, const float v[4]);
+template <>
+PZ_DEV void store4<uint16_t>(uint16_t* p, const float v[4]) {
+  *reinterpret_cast<uint2*>(p) = make_uint2(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]));
+}
+template <>
+PZ_DEV void store4<float>(float* p, const float v[4]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+template <int N, typename F, int I = 0>
+PZ_DEV void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, F, I + 1>(static_cast<F&&>(f));
+  }
+}
+
+// one 4-column fragment of one output row: bias / fused stage epilogue / accumulate / store
+template <typename OutT, typename AuxT>
+PZ_DEV f32x4_t epi_apply(const GemmArgs& p, f32x4_t a, f32x4_t bias4, int m, int n, OutT* __restrict__ Cp,
+                         const AuxT* __restrict__ aux) {
+  float v[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = a[r] * p.alpha;
+  const uint64_t idx = static_cast<uint64_t>(m) * static_cast<uint64_t>(p.idx_ld) + n;
+  if (p.epi_mode == EPI_BWD) {
+    float y[4];
+    load4<AuxT>(aux + static_cast<int64_t>(m) * p.ldaux + n, y);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = epi_bwd(v[r], y[r], idx + r, p.epi);
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += bias4[r];
+    if (p.epi_mode == EPI_FWD) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = epi_fwd(v[r], idx + r, p.epi);
+    }
+  }
+  OutT* dst = Cp + static_cast<int64_t>(m) * p.ldc + n;
+  if (p.accumulate) {
+    float old[4];
+    load4<OutT>(dst, old);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] += old[r];
+  }
+  store4<OutT>(dst, v);
+  return f32x4_t{v[0], v[1], v[2], v[3]};
+}
+
+PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  constexpr int GROUP = 8;
+  const int per_group = GROUP * tiles_n;
+  const int g = wgid / per_group;
+  const int first = g * GROUP;
+  const int gsz = min(tiles_m - first, GROUP);
+  const int in_group = wgid - g * per_group;
+  tm = first + in_group % gsz;
+  tn = in_group / gsz;
+}
+
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT>
+__global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
+  using C = Cfg<BM, BN, WM, WN>;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+
+  const int tiles_m = (p.M + BM - 1) / BM;
+  const int tiles_n = (p.N + BN - 1) / BN;
+  int tm, tn;
+  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int wm = wave / WN, wn = wave % WN;
+  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
+  const uint16_t* __restrict__ B = static_cast<const uint16_t*>(p.B);
+
+  f32x4_t acc[C::TM][C::TN];
+#pragma unroll
+  for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int kt, int buf) {
+    PZ_LDS char* base = smem + buf * C::STAGE_BYTES;
+    const int k0 = kt * kBK;
+    if constexpr (A_KC) stage_kc<BM, C::NW>(A, p.lda, m0, p.M, k0, base, wave, lane);
+    else stage_mn<BM, C::NW>(A, p.lda, m0, p.M, k0, base, wave, lane);
+    if constexpr (B_KC) stage_kc<BN, C::NW>(B, p.ldb, n0, p.N, k0, base + C::A_BYTES, wave, lane);
+    else stage_mn<BN, C::NW>(B, p.ldb, n0, p.N, k0, base + C::A_BYTES, wave, lane);
+  };
+
+  const int nk = p.K / kBK;
+  stage(0, 0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const PZ_LDS char* ta = smem + cur * C::STAGE_BYTES;
+    const PZ_LDS char* tb = ta + C::A_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      i16x8_t af[C::TM], bfr[C::TN];
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) {
+        if constexpr (A_KC) af[i] = frag_kc(ta, wm * C::WTM + i * 16 + (lane & 15), kk * 4 + (lane >> 4));
+        else af[i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, kk * 32 + 8 * (lane >> 4), lane);
+      }
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) {
+        if constexpr (B_KC) bfr[j] = frag_kc(tb, wn * C::WTN + j * 16 + (lane & 15), kk * 4 + (lane >> 4));
+        else bfr[j] = frag_mn<BN>(tb, wn * C::WTN + j * 16, kk * 32 + 8 * (lane >> 4), lane);
+      }
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                              __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // static_for (not #pragma unroll): the acc array must only ever be indexed by compile-time
+  // constants or it is demoted to scratch (guide §5.4 rule 20)
+  OutT* __restrict__ Cp = static_cast<OutT*>(p.C);
+  const AuxT* __restrict__ aux = static_cast<const AuxT*>(p.aux);
+  const int g4 = 4 * (lane >> 4);
+  static_for<C::TN>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const int n = n0 + wn * C::WTN + j * 16 + g4;
+    const bool n_ok = n < p.N;
+    f32x4_t bias4 = {0.f, 0.f, 0.f, 0.f};
+    if (p.bias != nullptr && n_ok) bias4 = *reinterpret_cast<const f32x4_t*>(p.bias + n);
+    f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
+    static_for<C::TM>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const int m = m0 + wm * C::WTM + i * 16 + (lane & 15);
+      if (n_ok && m < p.M) {
+        const f32x4_t v = epi_apply<OutT, AuxT>(p, acc[i][j], bias4, m, n, Cp, aux);
+        cs += v;
+      }
+    });
+    if (p.colsum != nullptr) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float s = cs[r];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        if ((lane & 15) == 0 && n + r < p.N) atomicAdd(p.colsum + n + r, s);
+      }
+    }
+  });
+}
+
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT>
+hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
+  using C = Cfg<BM, BN, WM, WN>;
+  auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(C::NT), C::LDS_BYTES, s, p);
+  return hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN, typename OutT, typename AuxT>
+hipError_t launch_layout(const GemmArgs& p, hipStream_t s) {
+  if (p.a_kc && p.b_kc) return launch_cfg<BM, BN, WM, WN, true, true, OutT, AuxT>(p, s);
+  if (p.a_kc && !p.b_kc) return launch_cfg<BM, BN, WM, WN, true, false, OutT, AuxT>(p, s);
+  if (!p.a_kc && p.b_kc) return launch_cfg<BM, BN, WM, WN, false, true, OutT, AuxT>(p, s);
+  return launch_cfg<BM, BN, WM, WN, false, false, OutT, AuxT>(p, s);
+}
+
+template <typename OutT, typename AuxT>
+hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
+  auto tiles = [&](int bm, int bn) { return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
+  constexpr int kFill = 240;  // ~ CU count: a config below this leaves CUs idle
+  if (tiles(256, 256) >= kFill) return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
+  if (tiles(256, 128) >= kFill) return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
+  return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
+}
+
+}  // namespace
+
+bool mfma_eligible(const GemmArgs& p) {
+  if (p.force_generic || p.in_dtype != DT_BF16) return false;
+  if (p.out_dtype != DT_BF16 && p.out_dtype != DT_F32) return false;
+  if (p.M < 64 || p.N < 64 || p.K < kBK || p.K % kBK != 0) return false;
+  if (p.N % 8 != 0 || p.ldc % 8 != 0) return false;
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al16(p.A) || !al16(p.B) || !al16(p.C)) return false;
+  if (p.lda % 8 != 0 || p.ldb % 8 != 0) return false;
+  if (!p.a_kc && p.M % 8 != 0) return false;
+  if (p.bias != nullptr && !al16(p.bias)) return false;
+  if (p.epi_mode == EPI_BWD) {
+    if (p.aux == nullptr || p.ldaux % 8 != 0 || (reinterpret_cast<uintptr_t>(p.aux) & 7) != 0) return false;
+    if (p.aux_dtype != DT_BF16) return false;
+  }
+  return true;
+}
+
+hipError_t gemm_mfma(const GemmArgs& p, hipStream_t s) {
+  if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);
+  return launch_tiles<float, uint16_t>(p, s);
+}
+
+}  // namespace pz

@@ -1,0 +1,150 @@
+// Shared device helpers for the pz kernels (gfx950 / CDNA4 only).
+//
+//  * bf16 <-> f32 conversions and the MFMA operand vector types
+//  * the counter-based dropout hash: a mask is a pure function of (seed, layer id, element
+//    index), so backward kernels REGENERATE masks instead of storing them
+//  * the fused "stage epilogue": y = drop_post(act(drop_pre(x))) forward, and its derivative
+//    computed from the stored stage output y backward. This is the one place that encodes the
+//    reference's layer semantics (dropout on every hidden layer output, neural_net_model.py:393-395;
+//    relu/sigmoid/tanh, :172-184) for the GEMM, head and elementwise kernels alike.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pz_types.h"
+
+#define PZ_LDS __attribute__((address_space(3)))
+#define PZ_DEV __device__ __forceinline__
+
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short i16x8_t __attribute__((ext_vector_type(8)));
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef double f64x4_t __attribute__((ext_vector_type(4)));
+
+namespace pz {
+
+constexpr int kWave = 64;
+
+// ------------------------------------------------------------------------------------------
+// conversions
+// ------------------------------------------------------------------------------------------
+PZ_DEV float bf2f(uint16_t v) { return __uint_as_float(static_cast<uint32_t>(v) << 16); }
+PZ_DEV uint16_t f2bf(float f) {  // RNE; hipcc lowers the cast to v_cvt_pk_bf16_f32 (NaN-safe)
+  __bf16 b = static_cast<__bf16>(f);
+  return __builtin_bit_cast(uint16_t, b);
+}
+PZ_DEV uint32_t pack_bf2(float lo, float hi) {
+  return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+}
+
+template <typename T> PZ_DEV float to_f(T v) { return static_cast<float>(v); }
+template <> PZ_DEV float to_f<uint16_t>(uint16_t v) { return bf2f(v); }
+template <typename T> PZ_DEV T from_f(float v) { return static_cast<T>(v); }
+template <> PZ_DEV uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
+
+// ------------------------------------------------------------------------------------------
+// counter-based dropout RNG
+// ------------------------------------------------------------------------------------------
+PZ_DEV uint32_t mix32(uint32_t x) {  // "lowbias32" integer finaliser
+  x ^= x >> 16; x *= 0x7feb352dU;
+  x ^= x >> 15; x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return x;
+}
+// 32 random bits shared by the element pair (2j, 2j+1); each element uses 16 of them
+PZ_DEV uint32_t pair_bits(uint32_t pair, uint32_t seed_lo, uint32_t seed_hi, int lid) {
+  uint32_t h = mix32(pair ^ seed_lo);
+  return mix32(h ^ (seed_hi + 0x9E3779B9U * static_cast<uint32_t>(lid + 1)));
+}
+PZ_DEV bool keep_elem(uint64_t idx, uint32_t seed_lo, uint32_t seed_hi, int lid, uint32_t thresh16) {
+  uint32_t bits = pair_bits(static_cast<uint32_t>(idx >> 1), seed_lo, seed_hi, lid);
+  uint32_t r = (idx & 1) ? (bits >> 16) : (bits & 0xFFFFu);
+  return r >= thresh16;
+}
+
+// ------------------------------------------------------------------------------------------
+// stage epilogue math (EpiSpec lives in pz_types.h)
+// ------------------------------------------------------------------------------------------
+PZ_DEV float fexp(float x) { return __expf(x); }
+PZ_DEV double fexp(double x) { return exp(x); }
+PZ_DEV float ftanh(float x) { return tanhf(x); }
+PZ_DEV double ftanh(double x) { return tanh(x); }
+
+template <typename F>
+PZ_DEV F act_fwd(F x, int act) {
+  switch (act) {
+    case ACT_RELU: return x > F(0) ? x : F(0);
+    case ACT_SIGMOID: return F(1) / (F(1) + fexp(-x));
+    case ACT_TANH: return ftanh(x);
+    default: return x;
+  }
+}
+// derivative expressed through the activation OUTPUT a
+template <typename F>
+PZ_DEV F act_grad_from_out(F a, int act) {
+  switch (act) {
+    case ACT_RELU: return a > F(0) ? F(1) : F(0);
+    case ACT_SIGMOID: return a * (F(1) - a);
+    case ACT_TANH: return F(1) - a * a;
+    default: return F(1);
+  }
+}
+
+PZ_DEV bool epi_keep(const EpiSpec& e, int lid, uint64_t idx) {
+  if (e.drop_all) return false;
+  return keep_elem(idx, e.seed_lo, e.seed_hi, lid, e.thresh16);
+}
+
+// forward: x = producing-op output (bias already added), idx = logical element index
+template <typename F>
+PZ_DEV F epi_fwd(F x, uint64_t idx, const EpiSpec& e) {
+  if (e.drop_pre >= 0) x = epi_keep(e, e.drop_pre, idx) ? x * F(e.scale) : F(0);
+  x = act_fwd(x, e.act);
+  if (e.drop_post >= 0) x = epi_keep(e, e.drop_post, idx) ? x * F(e.scale) : F(0);
+  return x;
+}
+
+// backward: g = dLoss/dy, y = stored stage output; returns dLoss/dx (x as in epi_fwd)
+template <typename F>
+PZ_DEV F epi_bwd(F g, F y, uint64_t idx, const EpiSpec& e) {
+  if (e.drop_post >= 0) {
+    if (!epi_keep(e, e.drop_post, idx)) return F(0);
+    g *= F(e.scale);
+    y *= F(e.inv_scale);
+  }
+  if (e.act != ACT_NONE) g *= act_grad_from_out(y, e.act);
+  if (e.drop_pre >= 0) {
+    if (!epi_keep(e, e.drop_pre, idx)) return F(0);
+    g *= F(e.scale);
+  }
+  return g;
+}
+
+// ------------------------------------------------------------------------------------------
+// wave / block reductions (wave64)
+// ------------------------------------------------------------------------------------------
+PZ_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+PZ_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+PZ_DEV float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+PZ_DEV double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace pz

@@ -1,0 +1,176 @@
+// Host launch API for the non-GEMM kernels (elementwise, heads, optimizer, stats, batchnorm,
+// embedding). Plain C++; bindings.cpp adapts torch tensors to these structs.
+#pragma once
+
+#include "pz_launch.h"
+
+namespace pz {
+
+// ------------------------------------------------------------------ elementwise / heads
+struct XentArgs {
+  const void* logits;   // [rows][ld]
+  int64_t ld;
+  const int64_t* labels;  // [rows]
+  int rows, rows_valid, cols;
+  int dtype;
+  float* loss;          // += sum_rows (lse - x_label) * loss_scale   (may be null)
+  float loss_scale;
+  void* dh;             // [rows][ld_dh] gradient wrt the pre-dropout logits (may be null)
+  int64_t ld_dh;
+  float grad_scale;     // usually 1/global_batch
+  float* colsum;        // += column sums of dh (bias gradient), may be null
+  void* probs;          // optional softmax output [rows][ld_probs]
+  int64_t ld_probs;
+  EpiSpec epi;          // logits' dropout (drop_pre); act must be NONE
+  int64_t idx_ld;
+};
+
+struct MseArgs {
+  const void* y;        // final stage output [rows][ld_y]
+  int64_t ld_y;
+  const void* target;   // [rows][ld_t]
+  int64_t ld_t;
+  int rows, rows_valid, cols;
+  int dtype;
+  float* loss;
+  float loss_scale;     // 1 / numel
+  void* dh;
+  int64_t ld_dh;
+  float grad_scale;     // 1 / numel
+  float* colsum;
+  EpiSpec epi;          // last stage's epilogue (derivative from y)
+  int64_t idx_ld;
+};
+
+struct GatherArgs {
+  const void* data;     // [n_data][ld_data]
+  int64_t ld_data;
+  int data_dtype;
+  int64_t n_data;
+  const int64_t* indices;   // optional explicit indices [rows_valid]
+  uint32_t seed_lo, seed_hi;
+  void* out;            // [rows][ld_out]
+  int64_t ld_out;
+  int out_dtype;
+  int rows, rows_valid, cols;
+  const int64_t* labels_in;  // optional [n_data]
+  int64_t* labels_out;       // optional [rows]
+  int64_t* picked;           // optional [rows]: chosen data index per row
+};
+
+hipError_t stage_fwd(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, const EpiSpec& e, hipStream_t s);
+hipError_t stage_bwd(const void* g, const void* y, void* dx, int dtype, int64_t n, const EpiSpec& e, hipStream_t s);
+hipError_t xent_head(const XentArgs& a, hipStream_t s);
+hipError_t mse_head(const MseArgs& a, hipStream_t s);
+hipError_t softmax_rows(const void* x, void* y, int dtype, int rows, int cols, hipStream_t s);
+hipError_t softmax_bwd(const void* g, const void* y, void* dx, int dtype, int rows, int cols, hipStream_t s);
+hipError_t colsum(const void* x, int dtype, float* out, int rows, int cols, hipStream_t s);
+hipError_t gather_rows(const GatherArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ optimizer (N6)
+// One launch updates every parameter segment of a flat fp32 buffer.
+struct OptSegment {
+  int64_t offset;       // into params / grads / m / v (elements)
+  int64_t numel;
+  int is_weight;        // L2 + update-ratio statistics apply (reference: weights only)
+  int stat_slot;        // index into stats (4 doubles per slot), -1 = none
+  void* shadow;         // optional low-precision copy written after the update
+  int shadow_dtype;
+};
+
+struct OptArgs {
+  float* params;
+  const float* grads;
+  float* exp_avg;
+  float* exp_avg_sq;
+  const OptSegment* segments;  // device array
+  int num_segments;
+  const int64_t* block_seg;    // device array: first block index of each segment (+ total)
+  int total_blocks;
+  int adam;                    // 1 Adam, 0 SGD
+  float lr;
+  float beta1, beta2, eps;
+  float bias_c1, bias_c2_sqrt; // 1 - beta1^t, sqrt(1 - beta2^t)
+  float grad_scale;            // e.g. 1 / world_size
+  float l2_lambda;             // grad += 2*l2*w for weight segments
+  double* stats;               // per slot: sum(dw), sum(dw^2), sum(w), sum(w^2)  (accumulated)
+};
+
+constexpr int kOptElemsPerBlock = 4096;
+hipError_t optimizer_step(const OptArgs& a, hipStream_t s);
+// sum of squares of each weight segment (for the L2 term before the first update)
+hipError_t segment_stats(const float* params, const OptSegment* segments, const int64_t* block_seg, int num_segments,
+                         int total_blocks, double* stats, hipStream_t s);
+
+struct FinalizeArgs {
+  const float* loss;        // accumulated loss (summed over ranks when data parallel)
+  float loss_div;           // world size
+  double* stats_prev;       // [nslots][4] stats of the weights used by this step (zeroed afterwards)
+  const double* stats_cur;  // [nslots][4] stats of the update just applied
+  const double* slot_numel; // [nslots]
+  int nslots;
+  float l2;
+  float* costs;             // costs[epoch]
+  int epoch;
+  float* ratios;            // [rows][nslots]
+  int ratio_row;            // -1: no progress point this epoch
+};
+hipError_t step_finalize(const FinalizeArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ statistics (N7)
+enum SatRule : int { SAT_NONE = 0, SAT_ABS_GT = 1, SAT_LE = 2, SAT_ROW_NORM_GT = 3, SAT_ROW_MAX_GT = 4 };
+// out (double[8]): min, max, sum, sumsq, saturated_count, count, row_count, -
+hipError_t tensor_moments(const void* x, int dtype, int64_t n, int64_t row_len, int sat_rule, float sat_thr,
+                          double* out, hipStream_t s);
+// counts[bins] (float) of x over [lo, hi] read from range (double[2] on device: lo, hi)
+hipError_t histogram(const void* x, int dtype, int64_t n, const double* range, int bins, float* counts, hipStream_t s);
+
+// ------------------------------------------------------------------ batchnorm (N4)
+struct BnArgs {
+  const void* x;          // [rows][cols] (rows = all leading dims)
+  void* y;
+  int dtype;
+  int rows, rows_valid, cols;
+  const void* gain;       // [cols] master params, dtype param_dtype
+  const void* bias;
+  int param_dtype;        // DT_F32 or DT_F64 for gain/bias/running stats
+  void* running_mean;     // [cols] updated in training mode
+  void* running_var;
+  float eps, momentum;
+  int training;
+  float* save_mean;       // [cols] fp32 workspace (training)
+  float* save_invstd;     // [cols]
+  double* partial;        // workspace [2][cols] (sum, sumsq)
+  EpiSpec epi;            // fused stage epilogue after the affine transform
+  int64_t idx_ld;
+};
+hipError_t batchnorm_fwd(const BnArgs& a, hipStream_t s);
+struct BnBwdArgs {
+  const void* g;          // dLoss/d(stage output)
+  const void* y;          // stage output (after epilogue)
+  const void* x;          // batchnorm input
+  void* dx;
+  int dtype;
+  int rows, rows_valid, cols;
+  const void* gain;
+  const void* bias;
+  int param_dtype;
+  const float* save_mean;
+  const float* save_invstd;
+  void* dgain;            // [cols] accumulate (param dtype)
+  void* dbias;
+  double* partial;        // workspace [2][cols]
+  void* dxhat_buf;        // optional workspace [rows][cols] (same dtype as x) for the epilogue grads
+  EpiSpec epi;
+  int64_t idx_ld;
+};
+hipError_t batchnorm_bwd(const BnBwdArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------------ embedding (N5)
+enum IdxType : int { IDX_I64 = 0, IDX_F32 = 1, IDX_F64 = 2 };
+hipError_t embedding_fwd(const void* table, int table_dtype, const void* idx, int idx_dtype, int64_t n_idx, int dim,
+                         void* out, int out_dtype, hipStream_t s);
+hipError_t embedding_bwd(const void* dout, int dout_dtype, const void* idx, int idx_dtype, int64_t n_idx, int dim,
+                         void* dtable, int dtable_dtype, hipStream_t s);
+
+}  // namespace pz

@@ -1,0 +1,50 @@
+// Host-side launch API of the pz HIP kernels. Plain C++ (no torch headers) so the kernel
+// translation units compile fast; bindings.cpp adapts torch tensors to these calls.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pz_types.h"
+
+namespace pz {
+
+enum DType : int { DT_BF16 = 0, DT_F32 = 1, DT_F64 = 2, DT_FP8 = 3 };
+
+enum EpiMode : int {
+  EPI_STORE = 0,  // C = alpha*AB (+bias)                      [+ optional colsum of C]
+  EPI_FWD = 1,    // C = epi_fwd(alpha*AB + bias)               (fused dropout/act/dropout)
+  EPI_BWD = 2,    // C = epi_bwd(alpha*AB, aux)                 [+ optional colsum of C]
+};
+
+// C[M][N] = op(A) · op(B); row-major C with leading dim ldc.
+//  a_kc: A stored [M][K] (K contiguous) if true, else [K][M]
+//  b_kc: B stored [N][K] (K contiguous) if true, else [K][N]
+struct GemmArgs {
+  const void* A;
+  const void* B;
+  void* C;
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  int a_kc, b_kc;
+  int in_dtype;   // DType of A and B
+  int out_dtype;  // DType of C
+  float alpha;
+  int accumulate;  // C += result (beta = 1)
+  const float* bias;  // [N] fp32 or null (EPI_STORE / EPI_FWD)
+  const void* aux;    // EPI_BWD: stored stage output y, [M][ldaux], dtype aux_dtype
+  int64_t ldaux;
+  int aux_dtype;
+  float* colsum;      // [N] fp32: atomically accumulates column sums of the final C values
+  int epi_mode;
+  EpiSpec epi;
+  int64_t idx_ld;     // logical row stride used for dropout element indices (usually N)
+  int force_generic;  // testing: bypass the MFMA path
+};
+
+// returns hipSuccess or an error; chooses the MFMA path when the shape allows
+hipError_t gemm(const GemmArgs& args, hipStream_t stream);
+// exposed for tests / benchmarks: which path gemm() would take
+int gemm_path(const GemmArgs& args);  // 0 = generic VALU, 1 = MFMA bf16
+
+}  // namespace pz

@@ -1,0 +1,123 @@
+"""Fused optimizer bound to a genuine ``torch.optim.Adam`` (reference R24).
+
+The reference persists ``torch.optim.Adam.state_dict()`` to ``optimizer_<id>.pth``
+(``neural_net_model.py:338-341, 351-354``). A GPU model keeps that object — so checkpoints stay
+interchangeable — but its ``exp_avg`` / ``exp_avg_sq`` state tensors are *views into flat device
+buffers* that the single-launch fused kernel (``pz::optimizer_step``) updates in place, and its
+per-parameter ``step`` counters are kept in sync. ``optimizer=None`` models get the reference's
+manual SGD (``p -= lr * grad``) from the same kernel.
+
+Also owned here: the per-step statistics the reference computes with clones and host syncs
+(``weight_upd_ratio``, the L2 term's ``sum(w**2)``) — accumulated in-kernel into a double-buffered
+device array and turned into ``costs[epoch]`` / ``ratios[row]`` by ``pz::step_finalize``.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+from .params import ParamStore
+
+ELEMS_PER_BLOCK = 4096  # keep in sync with kOptElemsPerBlock (csrc/pz_kernels.h)
+
+
+class FusedOptimizer:
+    def __init__(self, store: ParamStore, params: list[torch.Tensor], torch_opt: torch.optim.Optimizer | None,
+                 shadows: dict[int, torch.Tensor]):
+        self.store = store
+        self.params = params
+        self.torch_opt = torch_opt
+        self.adam = torch_opt is not None
+        dev = store.device
+        n = store.numel
+        self.exp_avg = torch.zeros(n, device=dev, dtype=torch.float32) if self.adam else None
+        self.exp_avg_sq = torch.zeros(n, device=dev, dtype=torch.float32) if self.adam else None
+        self.step_count = 0
+        if self.adam:
+            self._adopt_state()
+
+        segs = sorted(store.segments, key=lambda s: s.offset)
+        self.weight_slots = [s for s in store.segments if s.is_weight]
+        self.weight_slots.sort(key=lambda s: s.param_index)
+        slot_of = {id(s): i for i, s in enumerate(self.weight_slots)}
+        blocks = [max(1, math.ceil(s.numel / ELEMS_PER_BLOCK)) for s in segs]
+        starts, acc = [], 0
+        for b in blocks:
+            starts.append(acc)
+            acc += b
+        self.total_blocks = acc
+        packed = torch.ops.pz.pack_segments(
+            [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
+            [slot_of.get(id(s), -1) for s in segs], [shadows.get(s.offset) for s in segs])
+        self.segments = packed.to(dev)
+        self.block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
+        self.num_segments = len(segs)
+        self.nslots = len(self.weight_slots)
+        self.slot_numel = torch.tensor([float(s.numel) for s in self.weight_slots] or [1.0], dtype=torch.float64,
+                                       device=dev)
+        # double-buffered per-slot stats: sum(dw), sum(dw^2), sum(w), sum(w^2)
+        self.stats = [torch.zeros(max(1, self.nslots) * 4, device=dev, dtype=torch.float64) for _ in range(2)]
+        self.cur = 0
+
+    # ------------------------------------------------------------------------------------
+    def _adopt_state(self) -> None:
+        """Move any existing Adam state into the flat buffers and re-point the state at views."""
+        opt = self.torch_opt
+        steps = []
+        for seg in self.store.segments:
+            p = self.params[seg.param_index]
+            st = opt.state.get(p, {})
+            m_view = self.store.view(seg, self.exp_avg)
+            v_view = self.store.view(seg, self.exp_avg_sq)
+            if "exp_avg" in st:
+                m_view.copy_(st["exp_avg"].reshape(seg.shape))
+                v_view.copy_(st["exp_avg_sq"].reshape(seg.shape))
+                steps.append(float(st["step"]))
+            step_t = st.get("step")
+            if not isinstance(step_t, torch.Tensor):
+                step_t = torch.tensor(0.0, dtype=torch.float32)
+            opt.state[p] = {"step": step_t, "exp_avg": m_view, "exp_avg_sq": v_view}
+        self.step_count = int(max(steps)) if steps else 0
+
+    def sync_torch_state(self) -> None:
+        """Publish the fused step counter into the torch optimizer's state (before saving)."""
+        if not self.adam:
+            return
+        for p in self.params:
+            st = self.torch_opt.state.get(p)
+            if st is not None:
+                st["step"].fill_(float(self.step_count))
+
+    # ------------------------------------------------------------------------------------
+    def init_stats(self) -> None:
+        """sum(w^2) of the current weights into the 'previous' stats buffer (L2 term of step 0)."""
+        prev = self.stats[1 - self.cur]
+        prev.zero_()
+        self.stats[self.cur].zero_()
+        torch.ops.pz.segment_stats(self.store.flat, self.segments, self.block_seg, self.num_segments,
+                                   self.total_blocks, prev)
+
+    def step(self, grads: torch.Tensor, lr: float, l2: float, grad_scale: float) -> None:
+        stats = self.stats[self.cur]
+        if self.adam:
+            group = self.torch_opt.param_groups[0]
+            b1, b2 = group["betas"]
+            eps = group["eps"]
+            self.step_count += 1
+            bc1 = 1.0 - b1 ** self.step_count
+            bc2s = math.sqrt(1.0 - b2 ** self.step_count)
+            group["lr"] = lr
+        else:
+            b1 = b2 = eps = 0.0
+            bc1 = bc2s = 1.0
+        torch.ops.pz.optimizer_step(self.store.flat, grads, self.exp_avg, self.exp_avg_sq, self.segments,
+                                    self.block_seg, self.num_segments, self.total_blocks, self.adam, lr, b1, b2, eps,
+                                    bc1, bc2s, grad_scale, l2, stats)
+
+    def finalize(self, loss: torch.Tensor | None, world: int, l2: float, costs: torch.Tensor, epoch: int,
+                 ratios: torch.Tensor, ratio_row: int) -> None:
+        prev = self.stats[1 - self.cur]
+        torch.ops.pz.step_finalize(loss, float(world), prev, self.stats[self.cur], self.slot_numel, self.nslots, l2,
+                                   costs, epoch, ratios, ratio_row)
+        self.cur = 1 - self.cur

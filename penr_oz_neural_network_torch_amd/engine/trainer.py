@@ -1,0 +1,553 @@
+"""Device-resident fused trainer — the GPU implementation of the reference epoch loop.
+
+Reference loop (``neural_net_model.py:459-522``) per epoch: sample with replacement, build an
+input tensor from Python lists, clone all weights, forward with dropout on hidden outputs, add
+the L2 term, backward through the autograd graph, Adam / SGD, ``.item()`` the cost and the
+per-weight update ratios. Here the same math runs as an explicit schedule of ``torch.ops.pz``
+HIP kernels with nothing on the host between epochs:
+
+    gather_rows (on-device sampling + cast)  [+ embedding_fwd]
+    per stage:  GEMM(+bias+dropout+act+dropout epilogue) | batchnorm(+epilogue) | flatten(+dropout)
+    head:       xent_head / mse_head  (loss + dZ of the last stage + its bias-grad colsum)
+    per stage, reversed:
+                dW GEMM  (XᵀdZ, fp32 straight into the flat grad buffer)
+                -> async RCCL all-reduce of that bucket (data parallel)
+                dX GEMM  (dZ Wᵀ with the previous stage's epilogue derivative + bias colsum fused)
+                | batchnorm_bwd | embedding_bwd
+    optimizer_step (one launch for all params, L2 + 1/world folded in, bf16 shadows refreshed)
+    step_finalize  (cost[e], weight_upd_ratio row -> device arrays)
+
+Costs / ratios / progress timestamps are pulled off the device only in :meth:`drain` (end of
+training, or the reference's 10 s checkpoint cadence). Epochs that feed the stats dashboard
+(the last one, or a checkpoint epoch) run the *record* schedule instead: same kernels with
+unfused epilogues so every layer output and its gradient exists for ``_record_training_overall_progress``.
+
+A "stage" is a producing op plus the dropout / activation / dropout that follow it
+(``linear [drop] [act [drop]]``, ``batchnorm [drop] [act [drop]]``, ``flatten [drop]``,
+``embedding``); the algo normalisation of the reference guarantees every activation directly
+follows a linear or batchnorm.
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from datetime import datetime, timedelta
+
+import torch
+
+from ..ops import functional as PF
+from ..ops import native
+from ..parallel.dist import DataParallelContext, get_context
+from .optim import FusedOptimizer
+
+ROW_PAD = 64  # batch rows padded to the GEMM K-tile so dW = XᵀdZ stays on the MFMA path
+
+
+def _round_up(n: int, a: int) -> int:
+    return (n + a - 1) // a * a
+
+
+@dataclass
+class Stage:
+    kind: str                     # embed | flatten | gemm | bn
+    first: int                    # first layer index covered
+    layers: list[int]             # layer indices covered (for record mode)
+    act: int = PF.ACT_NONE
+    drop_pre: int = -1            # layer id of the dropout after the producing op
+    act_layer: int = -1           # layer id of the activation (if any)
+    drop_post: int = -1           # layer id of the dropout after the activation
+    in_width: int = 0
+    out_width: int = 0
+    pos_in: int = 1               # positions per sample (rows = batch * pos)
+    pos_out: int = 1
+    seg_w: object = None
+    seg_b: object = None
+    layer: object = None
+    buffers: dict = field(default_factory=dict)
+
+    @property
+    def has_epi(self) -> bool:
+        return self.act != PF.ACT_NONE or self.drop_pre >= 0 or self.drop_post >= 0
+
+
+class UnsupportedModel(Exception):
+    pass
+
+
+def compile_stages(model) -> tuple[list[Stage], str]:
+    """Group the model's layers into fused stages; returns (stages, head kind)."""
+    layers, algos = model.layers, model.algos
+    n = len(layers)
+    stages: list[Stage] = []
+    store = model._param_store
+    head = "softmax" if algos[-1] == "softmax" else "mse"
+    end = n - 1 if head == "softmax" else n
+    pos, width = 1, None
+    i = 0
+    while i < end:
+        a = algos[i]
+        hid = layers[i].hidden
+        if a == "embedding":
+            if i != 0:
+                raise UnsupportedModel("embedding must be the first layer")
+            w = layers[i].weights
+            st = Stage("embed", i, [i], seg_w=store.segment_for(i, "weights"), layer=layers[i],
+                       in_width=0, out_width=w.shape[1])
+            width = w.shape[1]
+            st.pos_in = st.pos_out = -1  # resolved from the data (block size)
+            stages.append(st)
+            i += 1
+            continue
+        if a == "flatten":
+            r = layers[i].ratio
+            st = Stage("flatten", i, [i], drop_pre=i if hid else -1, layer=layers[i])
+            st.in_width, st.out_width = width, width * r
+            stages.append(st)
+            width = width * r
+            i += 1
+            continue
+        if a in ("linear", "batchnorm"):
+            kind = "gemm" if a == "linear" else "bn"
+            st = Stage(kind, i, [i], drop_pre=i if hid else -1, layer=layers[i])
+            if kind == "gemm":
+                st.seg_w = store.segment_for(i, "weights")
+                st.seg_b = store.segment_for(i, "bias")
+                st.in_width, st.out_width = layers[i].weights.shape
+                if width is not None and width != st.in_width:
+                    raise UnsupportedModel(f"width mismatch at layer {i}: {width} vs {st.in_width}")
+            else:
+                st.seg_w = store.segment_for(i, "gain")
+                st.seg_b = store.segment_for(i, "bias")
+                st.in_width = st.out_width = layers[i].gain.shape[0]
+            width = st.out_width
+            j = i + 1
+            if j < end and algos[j] in ("relu", "sigmoid", "tanh"):
+                st.act = PF.ACT_CODES[algos[j]]
+                st.act_layer = j
+                st.drop_post = j if layers[j].hidden else -1
+                st.layers.append(j)
+                j += 1
+            stages.append(st)
+            i = j
+            continue
+        raise UnsupportedModel(f"layer {i} ({a}) cannot start a fused stage")
+    if not stages or stages[-1].kind not in ("gemm", "bn", "flatten"):
+        raise UnsupportedModel("model must end in a linear/batchnorm stage before the head")
+    if head == "softmax" and stages[-1].act != PF.ACT_NONE:
+        raise UnsupportedModel("activation directly before softmax")
+    return stages, head
+
+
+class FusedTrainer:
+    """Owns the device buffers of one GPU model's training run."""
+
+    def __init__(self, model, context: DataParallelContext | None = None):
+        native.require()
+        if model.precision.master != torch.float32:
+            raise UnsupportedModel("fused engine needs fp32 master parameters")
+        self.model = model
+        self.store = model._param_store
+        self.dev = self.store.device
+        self.compute = torch.bfloat16 if model.precision.name in ("bfloat16", "fp8") else torch.float32
+        self.ctx = context or get_context()
+        self.stages, self.head = compile_stages(model)
+        self.grads = torch.zeros(self.store.numel + 64, device=self.dev, dtype=torch.float32)
+        self.loss_slot = self.grads[self.store.numel:self.store.numel + 1]
+        self.shadows: dict[int, torch.Tensor] = {}
+        for st in self.stages:
+            if st.kind == "gemm" and self.compute != torch.float32:
+                sh = torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute)
+                sh.copy_(self.store.view(st.seg_w))
+                self.shadows[st.seg_w.offset] = sh
+        self.opt = FusedOptimizer(self.store, model.params, model.optimizer, self.shadows)
+        self.ctx.broadcast_(self.store.flat)  # identical replicas (rank 0 wins)
+        for sh_off, sh in self.shadows.items():
+            seg = next(s for s in self.store.segments if s.offset == sh_off)
+            sh.copy_(self.store.view(seg))
+        self.opt.init_stats()
+        self._rows = None
+        self._pending: list = []   # (epoch, ratio_row or None, event)
+        self._drained = 0
+        self._record = None
+        self.data = None
+
+    # ------------------------------------------------------------------------------------
+    # data
+    # ------------------------------------------------------------------------------------
+    def load_data(self, data) -> None:
+        """Training pairs (python lists) -> device tensors, once per ``train()`` call."""
+        inputs = [inp for inp, _ in data]
+        targets = [tgt for _, tgt in data]
+        first = self.stages[0]
+        if first.kind == "embed":
+            x = torch.tensor(inputs, dtype=torch.float32)
+            if x.dim() == 1:
+                x = x.unsqueeze(1)
+            self.block = x.shape[1]
+        else:
+            x = torch.tensor(inputs, dtype=torch.float32).reshape(len(inputs), -1)
+            self.block = 1
+        self.data = x.to(self.dev).contiguous()
+        if self.head == "softmax":
+            self.labels = torch.tensor([int(t[0]) for t in targets], dtype=torch.int64, device=self.dev)
+            self.targets = None
+        else:
+            self.targets = torch.tensor(targets, dtype=torch.float32).reshape(len(targets), -1).to(self.dev)
+            self.labels = None
+        seed = torch.randint(0, 2 ** 62, (1,)).item()
+        self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+
+    def _ensure_buffers(self, batch: int) -> None:
+        rows_b = _round_up(batch, ROW_PAD)
+        if self._rows == (batch, rows_b):
+            return
+        self._rows = (batch, rows_b)
+        dev, cd = self.dev, self.compute
+        pos = self.block
+        self.x_in = torch.empty(rows_b, self.data.shape[1], device=dev, dtype=torch.float32 if
+                                self.stages[0].kind == "embed" else cd)
+        self.lab = torch.empty(rows_b, device=dev, dtype=torch.int64) if self.head == "softmax" else None
+        self.picked = torch.empty(rows_b, device=dev, dtype=torch.int64)
+        self.tgt = torch.empty(rows_b, self.targets.shape[1], device=dev, dtype=cd) if self.targets is not None \
+            else None
+        for st in self.stages:
+            if st.kind == "embed":
+                st.pos_in = st.pos_out = pos
+                rows = rows_b * pos
+                st.buffers["y"] = torch.empty(rows, st.out_width, device=dev, dtype=cd)
+                st.buffers["g"] = torch.empty(rows, st.out_width, device=dev, dtype=cd)
+                continue
+            st.pos_in = pos
+            if st.kind == "flatten":
+                r = st.layer.ratio
+                pos = pos // r
+                st.pos_out = pos
+            else:
+                st.pos_out = pos
+            rows = rows_b * st.pos_out
+            st.buffers["y"] = torch.empty(rows, st.out_width, device=dev, dtype=cd)
+            st.buffers["g"] = torch.empty(rows, st.out_width, device=dev, dtype=cd)
+            if st.kind == "bn":
+                c = st.out_width
+                st.buffers["mean"] = torch.empty(c, device=dev, dtype=torch.float32)
+                st.buffers["invstd"] = torch.empty(c, device=dev, dtype=torch.float32)
+                st.buffers["partial"] = torch.empty(2 * c, device=dev, dtype=torch.float64)
+                st.buffers["bn_in_grad"] = torch.empty(rows_b * st.pos_in, st.in_width, device=dev, dtype=cd)
+        if pos != 1:
+            raise UnsupportedModel(f"head input still has {pos} positions per sample")
+        # record-mode scratch: one buffer per layer output / grad, allocated lazily
+
+    # ------------------------------------------------------------------------------------
+    # epilogue specs
+    # ------------------------------------------------------------------------------------
+    def _seed(self, epoch: int) -> tuple[int, int]:
+        lo = (self.base_seed[0] ^ (epoch * 0x9E3779B1)) & 0xFFFFFFFF
+        hi = (self.base_seed[1] + epoch * 0x85EBCA6B + self.ctx.rank * 0xC2B2AE35) & 0xFFFFFFFF
+        return lo, hi
+
+    def _epi(self, st: Stage, p: float, seed, parts=("pre", "act", "post")):
+        return PF.epi_spec(act=st.act if "act" in parts else PF.ACT_NONE,
+                           drop_pre=st.drop_pre if "pre" in parts else -1,
+                           drop_post=st.drop_post if "post" in parts else -1, p=p, seed=seed)
+
+    def _w(self, st: Stage) -> torch.Tensor:
+        """GEMM operand for the stage's weight: bf16 shadow or the fp32 master view, [in, out]."""
+        sh = self.shadows.get(st.seg_w.offset)
+        return sh if sh is not None else self.store.view(st.seg_w)
+
+    # ------------------------------------------------------------------------------------
+    # one epoch
+    # ------------------------------------------------------------------------------------
+    def begin(self, epochs: int) -> None:
+        """Size the device-side progress arrays for a ``train()`` call of ``epochs`` epochs."""
+        self._alloc_progress(epochs)
+
+    def step(self, epoch: int, lr: float, sample_size: int, dropout: float, l2: float, want_ratios: bool,
+             record: bool) -> None:
+        world = self.ctx.world_size
+        batch = max(1, sample_size // world) if world > 1 else sample_size
+        self._ensure_buffers(batch)
+        if not hasattr(self, "costs") or epoch >= self.costs.numel():
+            self._alloc_progress(epoch + 1)
+        seed = self._seed(epoch)
+        ops = torch.ops.pz
+
+        # zero the accumulated-gradient region (+ loss slot)
+        self.grads[self.store.accum_offset:].zero_()
+
+        # ---------------- sample + input
+        gseed = ((self.base_seed[0] + epoch * 0x632BE5AB) & 0xFFFFFFFF,
+                 (self.base_seed[1] ^ (self.ctx.rank * 0x27D4EB2F + epoch)) & 0xFFFFFFFF)
+        ops.gather_rows(self.data, None, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked)
+        if self.tgt is not None:
+            ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
+
+        rec = {} if record else None
+        x = self.x_in
+        prev = None
+        for st in self.stages:
+            x = self._forward_stage(st, x, batch, dropout, seed, rec)
+            prev = st
+        last = prev
+
+        # ---------------- head
+        g_pre = self._head(last, x, batch, dropout, seed, rec)
+
+        # ---------------- backward
+        handles = []
+        g = last.buffers["g"]
+        for si in range(len(self.stages) - 1, -1, -1):
+            st = self.stages[si]
+            before = self.stages[si - 1] if si > 0 else None
+            x_in = before.buffers["y"] if before is not None else self.x_in
+            g, g_pre = self._backward_stage(st, before, x_in, g, g_pre, batch, dropout, seed, rec, handles)
+
+        # ---------------- reduce + update
+        handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:]))
+        self.ctx.wait_all(handles)
+        if record:
+            self._finish_record(rec, batch, l2)
+        self.opt.step(self.grads, lr, l2, 1.0 / world)
+        row = -1
+        if want_ratios:
+            row = self._ratio_rows
+            self._ratio_rows += 1
+        self.opt.finalize(self.loss_slot, world, l2, self.costs, epoch, self.ratios, row)
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self._pending.append((epoch, row if want_ratios else None, ev))
+
+    # ------------------------------------------------------------------------------------
+    def _forward_stage(self, st: Stage, x, batch, p, seed, rec):
+        ops = torch.ops.pz
+        y = st.buffers["y"]
+        rows_valid = batch * st.pos_out
+        if st.kind == "embed":
+            ids = x  # [rows_b, T] float32 ids
+            ops.embedding_fwd(self.store.view(st.seg_w), ids, y)
+            if rec is not None:
+                rec[st.first] = y[:rows_valid]
+            return y
+        if st.kind == "flatten":
+            src = x.view(y.shape)
+            if st.drop_pre >= 0:
+                ei, ef = self._epi(st, p, seed)
+                ops.stage_fwd(src, y, ei, ef)
+            else:
+                y.copy_(src)
+            if rec is not None:
+                rec[st.first] = y[:rows_valid]
+            return y
+        if rec is None:
+            ei, ef = self._epi(st, p, seed)
+            if st.kind == "gemm":
+                bias = self.store.view(st.seg_b) if st.seg_b is not None else None
+                PF.gemm(x, True, self._w(st), False, y, bias=bias, mode=PF.EPI_FWD, epi=(ei, ef))
+            else:
+                self._bn_fwd(st, x, y, batch, ei, ef)
+            return y
+        # record mode: producing op without epilogue, then one kernel per following layer
+        z = self._scratch(("z", st.first), y)
+        none = PF.epi_spec()
+        if st.kind == "gemm":
+            bias = self.store.view(st.seg_b) if st.seg_b is not None else None
+            PF.gemm(x, True, self._w(st), False, z, bias=bias, mode=PF.EPI_STORE)
+        else:
+            self._bn_fwd(st, x, z, batch, *none)
+        out_first = self._scratch(("o", st.first), y)
+        ops.stage_fwd(z, out_first, *self._epi(st, p, seed, parts=("pre",)))
+        rec[st.first] = out_first[:rows_valid]
+        if st.act_layer >= 0:
+            ops.stage_fwd(out_first, y, *self._epi(st, p, seed, parts=("act", "post")))
+            rec[st.act_layer] = y[:rows_valid]
+        else:
+            y.copy_(out_first)
+        rec[("z", st.first)] = z
+        return y
+
+    def _bn_fwd(self, st: Stage, x, y, batch, ei, ef):
+        layer = st.layer
+        torch.ops.pz.batchnorm_fwd(x, y, self.store.view(st.seg_w), self.store.view(st.seg_b), layer.mean,
+                                   layer.variance, float(layer.eps), float(layer.momentum), True,
+                                   batch * st.pos_out, st.buffers["mean"], st.buffers["invstd"],
+                                   st.buffers["partial"], ei, ef, 0)
+
+    def _scratch(self, key, like):
+        buf = getattr(self, "_scratch_bufs", None)
+        if buf is None:
+            buf = self._scratch_bufs = {}
+        t = buf.get(key)
+        if t is None or t.shape != like.shape:
+            t = buf[key] = torch.empty_like(like)
+        return t
+
+    # ------------------------------------------------------------------------------------
+    def _head(self, last: Stage, y, batch, p, seed, rec) -> bool:
+        """Loss + gradient of the last stage. Returns True when the gradient is wrt the
+        producing op (epilogue derivative already applied), False when wrt the stage output."""
+        ops = torch.ops.pz
+        g = last.buffers["g"]
+        fuse = rec is None and last.kind == "gemm"
+        bias_grad = self.store.view(last.seg_b, self.grads) if (last.seg_b is not None and last.kind == "gemm") else None
+        ei, ef = self._epi(last, p, seed) if fuse else PF.epi_spec()
+        n = self.model.layers
+        if self.head == "softmax":
+            probs = self._scratch(("probs",), y) if rec is not None else None
+            ops.xent_head(y, self.lab, batch, self.loss_slot, 1.0 / batch, g, 1.0 / batch,
+                          bias_grad if fuse else None, probs, ei, ef, 0)
+            if rec is not None:
+                rec[len(n) - 1] = probs[:batch]
+                rec[("grad", len(n) - 2)] = g[:batch]
+        else:
+            cols = y.shape[1]
+            ops.mse_head(y, self.tgt, batch, self.loss_slot, 1.0 / (batch * cols), g, 1.0 / (batch * cols),
+                         bias_grad if fuse else None, ei, ef, 0)
+            if rec is not None:
+                rec[("grad", len(n) - 1)] = g[:batch]
+        return fuse
+
+    def _backward_stage(self, st: Stage, before: Stage | None, x_in, g, g_pre: bool, batch, p, seed, rec, handles):
+        """Consume the gradient of stage `st`; return (gradient for `before`, is_pre flag)."""
+        ops = torch.ops.pz
+        rows_valid = batch * st.pos_out
+        if st.kind == "embed":
+            gz = g if g_pre else g  # embedding has no epilogue
+            ops.embedding_bwd(gz, x_in, self.store.view(st.seg_w, self.grads))
+            return None, True
+        # bring g to the producing op (dZ)
+        if not g_pre:
+            g = self._apply_epi_bwd(st, g, batch, p, seed, rec)
+            if st.kind == "gemm" and st.seg_b is not None:
+                ops.colsum(g[:rows_valid], self.store.view(st.seg_b, self.grads))
+        if st.kind == "flatten":
+            if before is None:
+                return None, True
+            gb = g.view(before.buffers["y"].shape)
+            if rec is not None:
+                rec[("grad", before.layers[-1])] = gb[:batch * before.pos_out]
+            return gb, False
+        if st.kind == "bn":
+            dx = st.buffers["bn_in_grad"] if before is not None else None
+            layer = st.layer
+            none = PF.epi_spec()
+            ops.batchnorm_bwd(g, st.buffers["y"] if rec is None else rec[("z", st.first)], x_in, dx,
+                              self.store.view(st.seg_w), self.store.view(st.seg_b), st.buffers["mean"],
+                              st.buffers["invstd"], self.store.view(st.seg_w, self.grads),
+                              self.store.view(st.seg_b, self.grads), st.buffers["partial"], rows_valid,
+                              *none, 0)
+            del layer
+            if rec is not None and before is not None:
+                rec[("grad", before.layers[-1])] = dx[:batch * st.pos_in]
+            return dx, False
+        # GEMM stage: dW = x_inᵀ · dZ
+        w_grad = self.store.view(st.seg_w, self.grads)
+        PF.gemm(x_in, False, g, False, w_grad)
+        handles.append(self.ctx.all_reduce_async(w_grad))
+        if before is None:
+            return None, True
+        # dX = dZ · Wᵀ (+ previous stage's epilogue derivative and bias colsum when fusable)
+        dx = before.buffers["g"]
+        fuse_prev = rec is None and before.kind in ("gemm", "bn", "flatten") and before.has_epi
+        if fuse_prev:
+            ei, ef = self._epi(before, p, seed)
+            colsum = self.store.view(before.seg_b, self.grads) if (before.kind == "gemm" and before.seg_b is not None) \
+                else None
+            PF.gemm(g, True, self._w(st), True, dx, aux=before.buffers["y"], colsum=colsum, mode=PF.EPI_BWD,
+                    epi=(ei, ef))
+            return dx, True
+        no_epi_prev = before.kind in ("gemm",) and not before.has_epi and rec is None
+        colsum = None
+        if no_epi_prev and before.seg_b is not None:
+            colsum = self.store.view(before.seg_b, self.grads)
+        PF.gemm(g, True, self._w(st), True, dx, colsum=colsum, mode=PF.EPI_STORE)
+        if rec is not None:
+            rec[("grad", before.layers[-1])] = dx[:batch * before.pos_out]
+        if no_epi_prev or before.kind == "embed":
+            return dx, True
+        return dx, False
+
+    def _apply_epi_bwd(self, st: Stage, g, batch, p, seed, rec):
+        """dY (wrt stage output) -> dZ (wrt producing op); record mode keeps the per-layer grads."""
+        ops = torch.ops.pz
+        if not st.has_epi:
+            return g
+        if rec is None:
+            dz = self._scratch(("dz", st.first), g)
+            ops.stage_bwd(g, st.buffers["y"], dz, *self._epi(st, p, seed))
+            return dz
+        # record: y_act = stage output; out_first = output of the first layer of the stage
+        out_first = self._scratch(("o", st.first), g)
+        if st.act_layer >= 0:
+            g_first = self._scratch(("go", st.first), g)
+            ops.stage_bwd(g, st.buffers["y"], g_first, *self._epi(st, p, seed, parts=("act", "post")))
+            rec[("grad", st.first)] = g_first[:batch * st.pos_out]
+        else:
+            g_first = g
+        dz = self._scratch(("dz", st.first), g)
+        ops.stage_bwd(g_first, out_first, dz, *self._epi(st, p, seed, parts=("pre",)))
+        return dz
+
+    # ------------------------------------------------------------------------------------
+    # record / progress plumbing
+    # ------------------------------------------------------------------------------------
+    def _finish_record(self, rec, batch, l2):
+        n = len(self.model.layers)
+        acts, grads = [], []
+        for i in range(n):
+            a = rec.get(i)
+            if a is None:
+                raise RuntimeError(f"record mode missed layer {i}")
+            acts.append(a.detach().clone())
+            gi = rec.get(("grad", i))
+            grads.append(gi.detach().clone() if gi is not None else None)
+        wgrads = []
+        world = self.ctx.world_size
+        for i, layer in enumerate(self.model.layers):
+            seg = self.store.segment_for(i, "weights") if layer.weights is not None else None
+            if seg is None:
+                wgrads.append(None)
+                continue
+            gview = self.store.view(seg, self.grads) / world
+            wgrads.append(gview + (2.0 * l2) * self.store.view(seg))
+        self._record = {"activations": acts, "act_grads": grads, "weight_grads": wgrads}
+
+    def _alloc_progress(self, epochs: int) -> None:
+        points = math.ceil(epochs / max(1, epochs // 100)) + 1
+        self.costs = torch.zeros(max(epochs, 1), device=self.dev, dtype=torch.float32)
+        self.ratios = torch.zeros(points * max(1, self.opt.nslots), device=self.dev, dtype=torch.float32)
+        self._ratio_rows = 0
+        self._pending = []
+        self._start_event = torch.cuda.Event(enable_timing=True)
+        self._start_event.record()
+        torch.cuda.synchronize(self.dev)
+        self._start_wall = datetime.now()
+
+    def drain(self):
+        """Yield ``(epoch, cost, ratios|None, iso_time)`` for every step since the last drain."""
+        if not self._pending:
+            return []
+        torch.cuda.synchronize(self.dev)
+        costs = self.costs.cpu().tolist()
+        ratios = self.ratios.cpu().view(-1, max(1, self.opt.nslots)).tolist()
+        out = []
+        for epoch, row, ev in self._pending:
+            ms = self._start_event.elapsed_time(ev)
+            when = (self._start_wall + timedelta(milliseconds=ms)).isoformat()
+            r = ratios[row][:self.opt.nslots] if row is not None else None
+            out.append((epoch, costs[epoch], r, when))
+        self._pending = []
+        self.opt.sync_torch_state()
+        return out
+
+    def record(self):
+        if self._record is None:
+            raise RuntimeError("no record-mode step has run")
+        return self._record
+
+    # convenience for benchmarks / tests --------------------------------------------------
+    def synchronize(self) -> None:
+        torch.cuda.synchronize(self.dev)
+
+
+__all__ = ["FusedTrainer", "UnsupportedModel", "compile_stages", "time"]

@@ -1,0 +1,359 @@
+"""GPU operators with autograd, built on the ``torch.ops.pz`` HIP kernels.
+
+This is the *autograd path* used by :class:`..models.layers.Layer` ``forward`` on GPU tensors
+(``compute_output``, ``_forward`` + ``backward`` exactly as the reference calls them). The
+throughput path (:mod:`..engine`) calls the same kernels with its own explicit schedule.
+
+Every function here requires the native library; a missing ``_pz_C.so`` raises instead of
+falling back to ATen (see :mod:`.native`).
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+from torch import Tensor
+
+from . import native
+
+ACT_NONE, ACT_RELU, ACT_SIGMOID, ACT_TANH = 0, 1, 2, 3
+ACT_CODES = {"relu": ACT_RELU, "sigmoid": ACT_SIGMOID, "tanh": ACT_TANH, None: ACT_NONE, "none": ACT_NONE}
+EPI_STORE, EPI_FWD, EPI_BWD = 0, 1, 2
+SAT_CODES = {"abs_gt": 1, "le": 2, "row_norm_gt": 3, "row_max_gt": 4}
+
+
+def _ops():
+    native.require()
+    return torch.ops.pz
+
+
+# --------------------------------------------------------------------------------------------
+# epilogue specs
+# --------------------------------------------------------------------------------------------
+def epi_spec(act: int = ACT_NONE, drop_pre: int = -1, drop_post: int = -1, p: float = 0.0,
+             seed: tuple[int, int] = (0, 0)) -> tuple[list[int], list[float]]:
+    """Pack a stage epilogue ``drop_post(act(drop_pre(x)))`` for the kernels.
+
+    Dropout keeps an element iff its 16-bit counter-hash draw is ``>= round(p * 65536)``; kept
+    elements are scaled by ``1/(1-p)`` like ``torch.nn.functional.dropout``.
+    """
+    if p <= 0.0:
+        drop_pre = drop_post = -1
+    drop_all = 1 if p >= 1.0 else 0
+    thresh = min(65536, int(round(p * 65536)))
+    scale = 0.0 if drop_all else 1.0 / (1.0 - p)
+    inv_scale = 1.0 - p
+    return [act, drop_pre, drop_post, int(seed[0]) & 0xFFFFFFFF, int(seed[1]) & 0xFFFFFFFF, thresh, drop_all], \
+        [scale, inv_scale]
+
+
+def new_seed() -> tuple[int, int]:
+    """Fresh dropout seed drawn from torch's CPU generator (so ``torch.manual_seed`` controls it)."""
+    s = torch.randint(0, 2 ** 62, (1,)).item()
+    return s & 0xFFFFFFFF, (s >> 32) & 0xFFFFFFFF
+
+
+NO_EPI = epi_spec()
+
+
+# --------------------------------------------------------------------------------------------
+# GEMM front-end
+# --------------------------------------------------------------------------------------------
+def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Tensor | None = None,
+         aux: Tensor | None = None, colsum: Tensor | None = None, mode: int = EPI_STORE,
+         epi: tuple[list[int], list[float]] = NO_EPI, alpha: float = 1.0, accumulate: bool = False,
+         idx_ld: int = 0, force_generic: bool = False) -> Tensor:
+    """``out[M,N] = op(a) @ op(b)`` with a fused epilogue.
+
+    ``a_kc``: ``a`` is stored ``[M,K]`` (else ``[K,M]``); ``b_kc``: ``b`` is stored ``[N,K]`` (else ``[K,N]``).
+    """
+    M, N = out.shape
+    K = a.shape[1] if a_kc else a.shape[0]
+    _ops().gemm(a, a_kc, b, b_kc, out, bias, aux, colsum, mode, epi[0], epi[1], alpha, accumulate,
+                M, N, K, idx_ld, force_generic)
+    return out
+
+
+def gemm_path(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor) -> str:
+    M, N = out.shape
+    K = a.shape[1] if a_kc else a.shape[0]
+    return "mfma" if _ops().gemm_path(a, a_kc, b, b_kc, out, M, N, K) == 1 else "generic"
+
+
+def _as_2d(x: Tensor) -> tuple[Tensor, tuple]:
+    lead = x.shape[:-1]
+    return x.reshape(-1, x.shape[-1]).contiguous(), lead
+
+
+# --------------------------------------------------------------------------------------------
+# Linear
+# --------------------------------------------------------------------------------------------
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor, w: Tensor, b: Tensor | None):
+        squeeze = x.dim() == 1
+        x2, lead = _as_2d(x.unsqueeze(0) if squeeze else x)
+        wc = w if w.dtype == x2.dtype else w.to(x2.dtype)
+        wc = wc.contiguous()
+        out = torch.empty(x2.shape[0], wc.shape[1], device=x.device, dtype=x2.dtype)
+        bias32 = None
+        if b is not None:
+            bias32 = b.detach().float().contiguous()
+        gemm(x2, True, wc, False, out, bias=bias32)
+        ctx.save_for_backward(x2, wc)
+        ctx.has_bias = b is not None
+        ctx.w_dtype = w.dtype
+        ctx.b_dtype = b.dtype if b is not None else None
+        out = out.view(*lead, wc.shape[1])
+        return out.squeeze(0) if squeeze else out
+
+    @staticmethod
+    def backward(ctx, grad_out: Tensor):
+        x2, wc = ctx.saved_tensors
+        g2 = grad_out.reshape(-1, wc.shape[1]).to(x2.dtype).contiguous()
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.empty_like(x2)
+            gemm(g2, True, wc, True, gx)  # dX = dY @ W^T, W stored [in,out] = [N,K]
+            gx = gx.view(*grad_out.shape[:-1], wc.shape[0])
+        if ctx.needs_input_grad[1]:
+            acc_dtype = torch.float64 if x2.dtype == torch.float64 else torch.float32
+            gw = torch.empty(wc.shape, device=wc.device, dtype=acc_dtype)
+            gemm(x2, False, g2, False, gw)  # dW = X^T @ dY (K = batch)
+            gw = gw.to(ctx.w_dtype)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = torch.zeros(wc.shape[1], device=wc.device, dtype=torch.float32)
+            _ops().colsum(g2, gb)
+            gb = gb.to(ctx.b_dtype)
+            if x2.dtype == torch.float64:  # keep fp64 exactness for fp64 models
+                gb = g2.sum(0).to(ctx.b_dtype)
+        return gx, gw, gb
+
+
+def linear(x: Tensor, w: Tensor, b: Tensor | None) -> Tensor:
+    return _Linear.apply(x, w, b)
+
+
+# --------------------------------------------------------------------------------------------
+# activations / dropout (stage epilogue kernels)
+# --------------------------------------------------------------------------------------------
+class _Stage(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor, ei: list, ef: list):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        _ops().stage_fwd(xc, y, ei, ef)
+        ctx.save_for_backward(y)
+        ctx.ei, ctx.ef = ei, ef
+        return y
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        (y,) = ctx.saved_tensors
+        gc = g.contiguous().to(y.dtype)
+        dx = torch.empty_like(y)
+        _ops().stage_bwd(gc, y, dx, ctx.ei, ctx.ef)
+        return dx, None, None
+
+
+def activation(x: Tensor, algo: str) -> Tensor:
+    ei, ef = epi_spec(act=ACT_CODES[algo])
+    return _Stage.apply(x, ei, ef)
+
+
+def dropout(x: Tensor, p: float) -> Tensor:
+    if p <= 0.0:
+        return x
+    ei, ef = epi_spec(drop_pre=0, p=p, seed=new_seed())
+    return _Stage.apply(x, ei, ef)
+
+
+# --------------------------------------------------------------------------------------------
+# softmax / losses
+# --------------------------------------------------------------------------------------------
+class _Softmax(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x: Tensor):
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        _ops().softmax_rows(xc, y)
+        ctx.save_for_backward(y)
+        return y
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        (y,) = ctx.saved_tensors
+        dx = torch.empty_like(y)
+        _ops().softmax_bwd(g.contiguous().to(y.dtype), y, dx)
+        return dx
+
+
+def softmax(x: Tensor) -> Tensor:
+    return _Softmax.apply(x)
+
+
+class _CrossEntropy(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits: Tensor, labels: Tensor):
+        squeeze = logits.dim() == 1
+        l2 = (logits.unsqueeze(0) if squeeze else logits).contiguous()
+        lab = labels.reshape(-1).to(device=l2.device, dtype=torch.int64).contiguous()
+        rows = l2.shape[0]
+        loss = torch.zeros(1, device=l2.device, dtype=torch.float32)
+        dh = torch.empty_like(l2)
+        _ops().xent_head(l2, lab, rows, loss, 1.0 / rows, dh, 1.0 / rows, None, None, NO_EPI[0], NO_EPI[1], 0)
+        ctx.save_for_backward(dh)
+        ctx.squeeze = squeeze
+        return loss.reshape(()).to(logits.dtype)
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        (dh,) = ctx.saved_tensors
+        out = dh * g.to(dh.dtype)
+        return (out.squeeze(0) if ctx.squeeze else out), None
+
+
+def cross_entropy(logits: Tensor, labels: Tensor) -> Tensor:
+    return _CrossEntropy.apply(logits, labels)
+
+
+class _Mse(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, y: Tensor, target: Tensor):
+        shape = y.shape
+        y2 = y.reshape(-1, shape[-1] if y.dim() > 0 else 1).contiguous()
+        t2 = target.to(y.dtype).reshape(y2.shape).contiguous()
+        n = y2.numel()
+        loss = torch.zeros(1, device=y.device, dtype=torch.float32)
+        dh = torch.empty_like(y2)
+        _ops().mse_head(y2, t2, y2.shape[0], loss, 1.0 / n, dh, 1.0 / n, None, NO_EPI[0], NO_EPI[1], 0)
+        ctx.save_for_backward(dh)
+        ctx.shape = shape
+        return loss.reshape(()).to(y.dtype)
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        (dh,) = ctx.saved_tensors
+        return (dh * g.to(dh.dtype)).reshape(ctx.shape), None
+
+
+def mse_loss(y: Tensor, target: Tensor) -> Tensor:
+    return _Mse.apply(y, target)
+
+
+# --------------------------------------------------------------------------------------------
+# batchnorm / embedding
+# --------------------------------------------------------------------------------------------
+class _BatchNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gain, bias, rmean, rvar, eps, momentum, training):
+        cols = x.shape[-1]
+        xc = x.contiguous()
+        y = torch.empty_like(xc)
+        dev = x.device
+        save_mean = torch.empty(cols, device=dev, dtype=torch.float32)
+        save_inv = torch.empty(cols, device=dev, dtype=torch.float32)
+        partial = torch.empty(2 * cols, device=dev, dtype=torch.float64)
+        rows = xc.numel() // max(cols, 1)
+        _ops().batchnorm_fwd(xc, y, gain.detach().contiguous(), bias.detach().contiguous(), rmean, rvar, eps,
+                             momentum, training, rows, save_mean, save_inv, partial, NO_EPI[0], NO_EPI[1], 0)
+        ctx.save_for_backward(xc, y, gain, bias, save_mean, save_inv)
+        ctx.rows = rows
+        ctx.training = training
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        xc, y, gain, bias, save_mean, save_inv = ctx.saved_tensors
+        if not ctx.training:  # eval: y = gain * (x - mean) * invstd + bias
+            gc = g.contiguous().to(xc.dtype)
+            dx = gc * (gain.to(xc.dtype) * save_inv.to(xc.dtype))
+            dgain = (gc * ((xc - save_mean.to(xc.dtype)) * save_inv.to(xc.dtype))).reshape(-1, xc.shape[-1]).sum(0)
+            return dx, dgain.to(gain.dtype), gc.reshape(-1, xc.shape[-1]).sum(0).to(bias.dtype), None, None, None, \
+                None, None
+        dx = torch.empty_like(xc)
+        dgain = torch.zeros_like(gain)
+        dbias = torch.zeros_like(bias)
+        partial = torch.empty(2 * xc.shape[-1], device=xc.device, dtype=torch.float64)
+        _ops().batchnorm_bwd(g.contiguous().to(xc.dtype), y, xc, dx, gain.detach().contiguous(),
+                             bias.detach().contiguous(), save_mean, save_inv, dgain, dbias, partial, ctx.rows,
+                             NO_EPI[0], NO_EPI[1], 0)
+        return dx, dgain, dbias, None, None, None, None, None
+
+
+def batchnorm(x: Tensor, gain: Tensor, bias: Tensor, rmean: Tensor, rvar: Tensor, eps: float, momentum: float,
+              training: bool) -> tuple[Tensor, Tensor, Tensor]:
+    """Returns ``(y, running_mean, running_var)``; running stats are fresh tensors like the reference."""
+    rm = rmean.detach().reshape(-1).to(gain.dtype).clone()
+    rv = rvar.detach().reshape(-1).to(gain.dtype).clone()
+    y = _BatchNorm.apply(x, gain, bias, rm, rv, float(eps), float(momentum), bool(training))
+    return y, rm, rv
+
+
+class _Embedding(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, idx: Tensor, table: Tensor):
+        ids = idx.to(device=table.device, dtype=torch.int64).contiguous()
+        out = torch.empty(*ids.shape, table.shape[1], device=table.device, dtype=table.dtype)
+        _ops().embedding_fwd(table.detach().contiguous(), ids, out)
+        ctx.save_for_backward(ids)
+        ctx.table_shape = table.shape
+        ctx.table_dtype = table.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g: Tensor):
+        (ids,) = ctx.saved_tensors
+        acc = torch.float64 if ctx.table_dtype == torch.float64 else torch.float32
+        dtable = torch.zeros(ctx.table_shape, device=g.device, dtype=acc)
+        _ops().embedding_bwd(g.contiguous(), ids, dtable)
+        return None, dtable.to(ctx.table_dtype)
+
+
+def embedding(idx: Tensor, table: Tensor) -> Tensor:
+    return _Embedding.apply(idx, table)
+
+
+# --------------------------------------------------------------------------------------------
+# statistics (N7)
+# --------------------------------------------------------------------------------------------
+def tensor_summary(t: Tensor, algo: str | None, bins: int) -> dict:
+    """mean / unbiased std / saturation / density histogram of a GPU tensor, one D2H copy."""
+    from ..utils.stats import saturation_rule
+    x = t.detach().contiguous()
+    if x.dtype not in (torch.float32, torch.float64, torch.bfloat16):
+        x = x.float()
+    dev = x.device
+    rule, thr = saturation_rule(algo) if algo is not None else ("abs_gt", 0.0)
+    moments = torch.empty(8, device=dev, dtype=torch.float64)
+    row_len = x.shape[-1] if x.dim() > 0 else 1
+    _ops().tensor_moments(x, row_len, SAT_CODES[rule] if algo is not None else 0, thr, moments)
+    counts = None
+    if bins > 0:
+        counts = torch.zeros(bins, device=dev, dtype=torch.float32)
+        _ops().histogram(x, moments[:2], bins, counts)
+    host = torch.cat([moments, counts.double()]) if counts is not None else moments
+    host = host.cpu().tolist()
+    n = x.numel()
+    mn, mx, s, ss, sat = host[0], host[1], host[2], host[3], host[4]
+    mean = s / n if n else math.nan
+    var = (ss - s * s / n) / (n - 1) if n > 1 else math.nan
+    out = {"mean": mean, "std": math.sqrt(var) if var == var and var > 0 else (0.0 if var == var else math.nan)}
+    if algo is not None:
+        rows = n // max(row_len, 1) if rule in ("row_norm_gt", "row_max_gt") else n
+        out["saturated"] = sat / rows if rows else math.nan
+    if bins > 0:
+        lo, hi = mn, mx
+        if lo == hi:
+            lo, hi = lo - 0.5, hi + 0.5
+        width = (hi - lo) / bins
+        c = host[8:8 + bins]
+        total = sum(c)
+        edges = [lo + i * width for i in range(bins)]
+        dens = [v / (total * width) if total else 0.0 for v in c]
+        out["histogram"] = {"x": edges, "y": dens}
+    return out
+
+
+__all__ = ["gemm", "gemm_path", "linear", "activation", "dropout", "softmax", "cross_entropy", "mse_loss",
+           "batchnorm", "embedding", "tensor_summary", "epi_spec", "new_seed"]

@@ -1,0 +1,183 @@
+"""Checkpoint format (reference L5, ``neural_net_model.py:306-369``).
+
+On disk, per model id (directory ``models/`` relative to the CWD, like the reference; override
+with ``PZ_MODELS_DIR``):
+
+* ``model_<id>.json`` — ``json.dump(model_data, indent=4)`` text: ``algos``, ``layers`` (each
+  ``{"params": [W[in][out], b[out]]}`` / ``{"ratio": r}`` / batchnorm ``params`` + ``eps`` +
+  ``momentum``), ``progress``, ``training_data_buffer``, ``average_cost``,
+  ``average_cost_history``, ``stats``, ``status``.
+* ``optimizer_<id>.pth`` — ``torch.save`` of a genuine ``torch.optim.Adam.state_dict()``.
+
+What is new here (format unchanged, files are interchangeable with the reference's):
+
+* **Byte-identical fast writer.** Parameter arrays are rendered by the native formatter
+  (``torch.ops.pz.format_json_array``: shortest round-trip digits, Python ``repr`` float
+  syntax, ``indent=4`` layout) and spliced into the small JSON skeleton. The output text equals
+  ``json.dumps(data, indent=4)`` byte for byte (tested), at a fraction of the cost for
+  multi-million-parameter models. Without the native library the pure-Python path produces the
+  same bytes.
+* **Atomic replace.** Files are written to a temporary sibling and ``os.replace``-d, so a
+  concurrent ``/progress/`` poll never reads a torn file (reference race).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import tempfile
+
+import torch
+
+log = logging.getLogger(__name__)
+
+_TOKEN = "@@PZ_TENSOR_{}@@"
+
+
+def models_dir() -> str:
+    return os.environ.get("PZ_MODELS_DIR", "models")
+
+
+def model_path(model_id: str) -> str:
+    return os.path.join(models_dir(), f"model_{model_id}.json")
+
+
+def optimizer_path(model_id: str) -> str:
+    return os.path.join(models_dir(), f"optimizer_{model_id}.pth")
+
+
+# --------------------------------------------------------------------------------------------
+# JSON rendering
+# --------------------------------------------------------------------------------------------
+class TensorRef:
+    """Placeholder for a parameter tensor inside the model-data skeleton."""
+
+    __slots__ = ("tensor",)
+
+    def __init__(self, tensor: torch.Tensor):
+        self.tensor = tensor
+
+
+def _native_formatter():
+    from ..ops import native
+    return native.format_json_array if native.has_host_ops() else None
+
+
+def _format_array_py(tensor: torch.Tensor, level: int) -> str:
+    # json.dumps of a nested list at nesting depth `level` (only the continuation lines
+    # carry indentation; the opening bracket sits where the placeholder string was)
+    text = json.dumps(tensor.tolist(), indent=4)
+    if level == 0:
+        return text
+    pad = " " * (4 * level)
+    return text.replace("\n", "\n" + pad)
+
+
+def format_array(tensor: torch.Tensor, level: int) -> str:
+    t = tensor.detach()
+    if t.is_cuda or t.dtype != torch.float64:
+        t = t.to(device="cpu", dtype=torch.float64)
+    t = t.contiguous()
+    fmt = _native_formatter()
+    if fmt is not None:
+        return fmt(t, level)
+    return _format_array_py(t, level)
+
+
+def render_json(data) -> str:
+    """``json.dumps(data, indent=4)`` where ``TensorRef`` leaves render as nested lists."""
+    refs: list[torch.Tensor] = []
+
+    def swap(obj):
+        if isinstance(obj, TensorRef):
+            refs.append(obj.tensor)
+            return _TOKEN.format(len(refs) - 1)
+        if isinstance(obj, dict):
+            return {k: swap(v) for k, v in obj.items()}
+        if isinstance(obj, (list, tuple)):
+            return [swap(v) for v in obj]
+        return obj
+
+    text = json.dumps(swap(data), indent=4)
+    if not refs:
+        return text
+    pieces: list[str] = []
+    pos = 0
+    for k, tensor in enumerate(refs):
+        token = '"' + _TOKEN.format(k) + '"'
+        at = text.index(token, pos)
+        line_start = text.rfind("\n", 0, at) + 1
+        level = (at - line_start) // 4
+        pieces.append(text[pos:at])
+        pieces.append(format_array(tensor, level))
+        pos = at + len(token)
+    pieces.append(text[pos:])
+    return "".join(pieces)
+
+
+# --------------------------------------------------------------------------------------------
+# atomic file IO
+# --------------------------------------------------------------------------------------------
+def _atomic_write_text(path: str, text: str) -> None:
+    directory = os.path.dirname(path) or "."
+    fd, tmp = tempfile.mkstemp(prefix=".tmp_", dir=directory)
+    try:
+        with os.fdopen(fd, "w", encoding="utf-8") as f:
+            f.write(text)
+        os.replace(tmp, path)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+        raise
+
+
+def _atomic_torch_save(obj, path: str) -> None:
+    directory = os.path.dirname(path) or "."
+    # torch's zip writer derives the archive name from the file name: keep it a plain "x.pth"
+    fd, tmp = tempfile.mkstemp(prefix="tmp_", suffix=".pth", dir=directory)
+    os.close(fd)
+    try:
+        torch.save(obj, tmp)
+        os.replace(tmp, path)
+    except BaseException:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+        raise
+
+
+def _to_cpu(obj):
+    """Optimizer state of GPU models is saved host-side so any machine can load the ``.pth``."""
+    if isinstance(obj, torch.Tensor):
+        return obj.detach().cpu()
+    if isinstance(obj, dict):
+        return {k: _to_cpu(v) for k, v in obj.items()}
+    if isinstance(obj, list):
+        return [_to_cpu(v) for v in obj]
+    return obj
+
+
+def save(model_id: str, skeleton: dict, optimizer_state: dict | None) -> None:
+    os.makedirs(models_dir(), exist_ok=True)
+    path = model_path(model_id)
+    _atomic_write_text(path, render_json(skeleton))
+    log.info(f"Model saved successfully: {path}")
+    if optimizer_state is not None:
+        opath = optimizer_path(model_id)
+        _atomic_torch_save(_to_cpu(optimizer_state), opath)
+        log.info(f"Optimizer saved successfully: {opath}")
+
+
+def load(model_id: str) -> tuple[dict, dict | None]:
+    """Return ``(model_data, optimizer_state_or_None)``; missing model → ``FileNotFoundError``."""
+    with open(model_path(model_id), "r", encoding="utf-8") as f:
+        data = json.load(f)
+    opath = optimizer_path(model_id)
+    opt_state = torch.load(opath, weights_only=True, map_location="cpu") if os.path.exists(opath) else None
+    return data, opt_state
+
+
+def delete(model_id: str) -> None:
+    os.remove(model_path(model_id))
+    opath = optimizer_path(model_id)
+    if os.path.exists(opath):
+        os.remove(opath)
