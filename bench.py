@@ -1,0 +1,143 @@
+"""Headline benchmark: training samples/sec (whole node) of the flagship MLP on MI355X.
+
+Metric / config from BASELINE.json: "training samples/sec (whole node), 4x8192 MLP bf16 at
+1/2/4/8 MI355X" — the 4-size MLP [1024, 4096, 4096, 1024] (relu, relu, softmax; 25.2 M params)
+at batch 8192 per GPU, bf16 compute with fp32 master weights, Adam. One timed step is exactly
+the reference's per-epoch body (``neural_net_model.py:459-514``, BASELINE.md method C):
+minibatch sampling, forward with dropout 0.2 on every hidden layer output, cross-entropy on the
+logits, L2 (lambda 1e-3) on the weights, backward, Adam update, cost + weight-update-ratio
+bookkeeping — run by the fused HIP engine, with the data-parallel gradient all-reduce (RCCL over
+xGMI) overlapped with backward when launched with torchrun.
+
+    python bench.py                                  # 1 GPU, defaults
+    python bench.py --gpus 1 --steps 50 --warmup 10
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
+        --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
+
+Scaling is WEAK: each GPU processes 8192 samples per step; ``value`` is the whole-job
+samples/s. Data are synthetic (random inputs / labels of the config's shape), weights random.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+REFERENCE_SAMPLES_PER_S = {  # BASELINE.md, reference on CPU fp64 (no published numbers exist)
+    "mlp4": 2064.0,
+    "deep16x8192": 22.8,
+    "mlp8192": 3095.0,
+}
+
+CONFIGS = {
+    "mlp4": dict(sizes=[1024, 4096, 4096, 1024], algos=["relu", "relu", "softmax"], batch=8192, dtype="bfloat16",
+                 optimizer="adam", name="mlp[1024,4096,4096,1024] relu,relu,softmax (25.2M params)"),
+    "deep16x8192": dict(sizes=[8192] * 17, algos=["relu"] * 15 + ["softmax"], batch=8192, dtype="bfloat16",
+                        optimizer="stochastic", name="mlp[8192]x17 (16 hidden 8192-wide, 1.07B params)"),
+    "mlp8192": dict(sizes=[1024, 8192, 1024], algos=["relu", "softmax"], batch=8192, dtype="bfloat16",
+                    optimizer="adam", name="mlp[1024,8192,1024] relu,softmax (16.8M params)"),
+}
+
+
+def log(msg: str) -> None:
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="mlp4", choices=sorted(CONFIGS))
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: config)")
+    ap.add_argument("--dropout", type=float, default=0.2)
+    ap.add_argument("--l2", type=float, default=1e-3)
+    args = ap.parse_args(argv)
+
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
+    from penr_oz_neural_network_torch_amd.models import NeuralNetworkModel
+    from penr_oz_neural_network_torch_amd.parallel import init_from_env
+
+    ctx = init_from_env()
+    world, rank = ctx.world_size, ctx.rank
+    if world != args.gpus:
+        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    cfg = CONFIGS[args.config]
+    batch = args.batch or cfg["batch"]
+
+    torch.manual_seed(1234)
+    model = NeuralNetworkModel("bench", cfg["sizes"], "xavier", "zeros", cfg["algos"], cfg["optimizer"],
+                               dtype=cfg["dtype"], device=f"cuda:{local}")
+    trainer = FusedTrainer(model, ctx)
+    n_data = 2 * batch
+    g = torch.Generator(device="cpu").manual_seed(99 + rank)
+    inputs = torch.randn(n_data, cfg["sizes"][0], generator=g)
+    labels = torch.randint(0, cfg["sizes"][-1], (n_data,), generator=g)
+    trainer.load_tensors(inputs, labels, seed=7 + rank)
+    total = args.warmup + args.steps
+    trainer.begin(total)
+    every = max(1, total // 100)
+    global_batch = batch * world
+    lr0, decay = 1e-3, 0.999
+
+    def run(epoch: int) -> None:
+        trainer.step(epoch, lr0 * decay ** epoch, global_batch, args.dropout, args.l2,
+                     want_ratios=epoch % every == 0, record=False)
+
+    t0 = time.time()
+    for e in range(args.warmup):
+        run(e)
+    torch.cuda.synchronize()
+    log(f"rank {rank}: warmup {args.warmup} steps done in {time.time() - t0:.2f}s")
+    ctx.barrier()
+    torch.cuda.synchronize()
+    start = time.perf_counter()
+    for e in range(args.warmup, total):
+        run(e)
+        if rank == 0 and (e - args.warmup) % 50 == 49:
+            log(f"step {e - args.warmup + 1}/{args.steps}")
+    torch.cuda.synchronize()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - start
+    elapsed = ctx.all_reduce_scalar_max(elapsed)
+
+    costs = [c for _, c, _, _ in trainer.drain()]
+    finite = all(c == c and abs(c) != float("inf") for c in costs)
+    ms = elapsed * 1e3 / args.steps
+    value = global_batch * args.steps / elapsed
+    ref = REFERENCE_SAMPLES_PER_S.get(args.config)
+    if rank == 0:
+        log(f"cost first/last = {costs[0]:.4f} / {costs[-1]:.4f}, finite={finite}")
+        print(json.dumps({
+            "metric": "training samples/sec (whole node), 4x8192 MLP bf16 at 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / ref, 2) if ref else None,
+            "dtype": "bf16",
+            "data": "synthetic (random inputs/labels, random-init weights)",
+            "config": {"model": cfg["name"], "global_batch": global_batch, "per_gpu_batch": batch,
+                       "seq_len": None, "parallelism": f"dp{world}", "optimizer": cfg["optimizer"],
+                       "dropout": args.dropout, "l2": args.l2, "config_key": args.config},
+        }), flush=True)
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

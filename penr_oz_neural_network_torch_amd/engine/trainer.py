@@ -197,6 +197,25 @@ class FusedTrainer:
             self.labels = None
         seed = torch.randint(0, 2 ** 62, (1,)).item()
         self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+        self._rows = None
+
+    def load_tensors(self, inputs: torch.Tensor, targets: torch.Tensor, seed: int | None = None) -> None:
+        """Fast path for benchmarks / programmatic use: a dataset already held as tensors.
+
+        ``inputs``: ``[N, in]`` (or ``[N, T]`` token ids); ``targets``: ``[N]`` class labels for a
+        softmax head, ``[N, out]`` regression targets otherwise.
+        """
+        self.data = inputs.to(device=self.dev, dtype=torch.float32).contiguous()
+        self.block = self.data.shape[1] if self.stages[0].kind == "embed" else 1
+        if self.head == "softmax":
+            self.labels = targets.reshape(-1).to(device=self.dev, dtype=torch.int64).contiguous()
+            self.targets = None
+        else:
+            self.targets = targets.to(device=self.dev, dtype=torch.float32).reshape(len(targets), -1).contiguous()
+            self.labels = None
+        seed = torch.randint(0, 2 ** 62, (1,)).item() if seed is None else seed
+        self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
+        self._rows = None
 
     def _ensure_buffers(self, batch: int) -> None:
         rows_b = _round_up(batch, ROW_PAD)

@@ -58,13 +58,16 @@ class DataParallelContext:
         if self.enabled:
             dist.broadcast(t, src=src, group=self.group)
 
-    def all_reduce_scalar(self, value: float) -> float:
+    def all_reduce_scalar(self, value: float, op=None) -> float:
         if not self.enabled:
             return value
         dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
         t = torch.tensor([value], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, group=self.group)
+        dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t.item()
+
+    def all_reduce_scalar_max(self, value: float) -> float:
+        return self.all_reduce_scalar(value, dist.ReduceOp.MAX) if self.enabled else value
 
     def barrier(self) -> None:
         if self.enabled:

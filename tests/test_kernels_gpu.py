@@ -1,0 +1,261 @@
+"""Numerics of every HIP kernel against plain PyTorch fp32/fp64 references (run on MI355X)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from penr_oz_neural_network_torch_amd.ops import functional as PF
+from tests.helpers import keep_mask
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _ref_mm(a, a_kc, b, b_kc):
+    A = a.double() if a_kc else a.double().t()
+    B = b.double().t() if b_kc else b.double()
+    return A @ B
+
+
+@pytest.mark.parametrize("a_kc,b_kc", [(True, True), (True, False), (False, True), (False, False)])
+@pytest.mark.parametrize("shape", [(512, 384, 256), (1024, 512, 128), (300, 264, 192), (8192, 1024, 128)])
+@pytest.mark.parametrize("out_dtype", [torch.bfloat16, torch.float32])
+def test_gemm_mfma_layouts(native_lib, a_kc, b_kc, shape, out_dtype):
+    M, N, K = shape
+    g = torch.Generator(device="cpu").manual_seed(M + N + K)
+    a = torch.randn((M, K) if a_kc else (K, M), generator=g).to(DEV, torch.bfloat16)
+    b = torch.randn((N, K) if b_kc else (K, N), generator=g).to(DEV, torch.bfloat16)
+    out = torch.empty(M, N, device=DEV, dtype=out_dtype)
+    if M % 8 == 0 or a_kc:
+        assert PF.gemm_path(a, a_kc, b, b_kc, out) == "mfma"
+    PF.gemm(a, a_kc, b, b_kc, out)
+    ref = _ref_mm(a, a_kc, b, b_kc)
+    err = (out.double() - ref).abs().max().item()
+    tol = 1e-3 * math.sqrt(K) + (0.02 * ref.abs().max().item() if out_dtype == torch.bfloat16 else 0)
+    assert err < tol, err
+
+
+def test_gemm_identity_asymmetric(native_lib):
+    # A = I with an asymmetric B catches a transposed C write (guide §3)
+    n = 256
+    a = torch.eye(n, device=DEV, dtype=torch.bfloat16)
+    b = (torch.arange(n * n, device=DEV, dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
+    for b_kc in (True, False):
+        out = torch.empty(n, n, device=DEV, dtype=torch.float32)
+        PF.gemm(a, True, b, b_kc, out)
+        ref = b.float().t() if b_kc else b.float()
+        assert torch.equal(out, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64, torch.bfloat16])
+def test_gemm_generic_small(native_lib, dtype):
+    M, N, K = 37, 19, 23
+    a = torch.randn(M, K, device=DEV, dtype=dtype)
+    b = torch.randn(K, N, device=DEV, dtype=dtype)
+    bias = torch.randn(N, device=DEV, dtype=torch.float32)
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    assert PF.gemm_path(a, True, b, False, out) == "generic"
+    PF.gemm(a, True, b, False, out, bias=bias)
+    ref = a.double() @ b.double() + bias.double()
+    tol = {torch.float64: 1e-12, torch.float32: 1e-4, torch.bfloat16: 0.15}[dtype]
+    assert (out.double() - ref).abs().max().item() < tol
+
+
+@pytest.mark.parametrize("force_generic", [False, True])
+def test_gemm_fused_forward_epilogue(native_lib, force_generic):
+    M, N, K = 512, 256, 128
+    p = 0.3
+    seed = (12345, 678)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, N, device=DEV) / 8).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=3, drop_post=4, p=p, seed=seed)
+    PF.gemm(x, True, w, False, out, bias=bias, mode=PF.EPI_FWD, epi=epi, force_generic=force_generic)
+    h = x.double() @ w.double() + bias.double()
+    m1 = torch.from_numpy(keep_mask(M * N, *seed, 3, p).reshape(M, N)).to(DEV)
+    m2 = torch.from_numpy(keep_mask(M * N, *seed, 4, p).reshape(M, N)).to(DEV)
+    ref = torch.relu(h * m1 / (1 - p)) * m2 / (1 - p)
+    assert (out.double() - ref).abs().max().item() < 0.05 * ref.abs().max().item()
+    assert abs(m1.float().mean().item() - (1 - p)) < 0.01
+
+
+@pytest.mark.parametrize("act", ["relu", "sigmoid", "tanh"])
+def test_gemm_backward_epilogue_and_colsum(native_lib, act):
+    M, N, K = 256, 128, 192
+    p = 0.25
+    seed = (99, 7)
+    code = PF.ACT_CODES[act]
+    z = torch.randn(M, N, device=DEV, dtype=torch.float64)
+    m1 = torch.from_numpy(keep_mask(M * N, *seed, 1, p).reshape(M, N)).to(DEV)
+    m2 = torch.from_numpy(keep_mask(M * N, *seed, 2, p).reshape(M, N)).to(DEV)
+    fn = {"relu": torch.relu, "sigmoid": torch.sigmoid, "tanh": torch.tanh}[act]
+    z.requires_grad_()
+    y = fn(z * m1 / (1 - p)) * m2 / (1 - p)
+    gy_a = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    gy = gy_a.double() @ w.double().t()  # dY = gA @ Wᵀ (W stored [N,K] = [out,in]ᵀ layout)
+    y.backward(gy)
+    out = torch.empty(M, N, device=DEV, dtype=torch.float32)
+    colsum = torch.zeros(N, device=DEV)
+    epi = PF.epi_spec(act=code, drop_pre=1, drop_post=2, p=p, seed=seed)
+    PF.gemm(gy_a, True, w, True, out, aux=y.detach().float(), colsum=colsum, mode=PF.EPI_BWD, epi=epi)
+    ref = z.grad
+    assert (out.double() - ref).abs().max().item() < 1e-3 * ref.abs().max().item() + 1e-4
+    assert (colsum.double() - out.double().sum(0)).abs().max().item() < 1e-3
+    # MFMA path: bf16 stage output as aux (derivatives then carry bf16 rounding of y)
+    out16 = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y16 = y.detach().to(torch.bfloat16)
+    assert PF.gemm_path(gy_a, True, w, True, out16) == "mfma"
+    PF.gemm(gy_a, True, w, True, out16, aux=y16, mode=PF.EPI_BWD, epi=epi)
+    assert (out16.double() - ref).abs().max().item() < 0.03 * ref.abs().max().item()
+
+
+def test_stage_kernels_match_torch(native_lib):
+    x = torch.randn(1000, 33, device=DEV, dtype=torch.float64, requires_grad=True)
+    for algo, fn in [("relu", torch.relu), ("sigmoid", torch.sigmoid), ("tanh", torch.tanh)]:
+        y = PF.activation(x, algo)
+        yr = fn(x)
+        torch.testing.assert_close(y, yr, rtol=1e-12, atol=1e-12)
+        g = torch.randn_like(y)
+        (gx,) = torch.autograd.grad(y, x, g)
+        (gr,) = torch.autograd.grad(yr, x, g)
+        torch.testing.assert_close(gx, gr, rtol=1e-10, atol=1e-12)
+
+
+def test_dropout_statistics(native_lib):
+    x = torch.ones(4096, 256, device=DEV)
+    y = PF.dropout(x, 0.2)
+    kept = (y != 0).float().mean().item()
+    assert abs(kept - 0.8) < 0.005
+    assert torch.allclose(y[y != 0], torch.full_like(y[y != 0], 1.25))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_cross_entropy_matches_torch(native_lib, dtype):
+    logits = torch.randn(300, 27, device=DEV, dtype=dtype, requires_grad=True)
+    labels = torch.randint(0, 27, (300,), device=DEV)
+    loss = PF.cross_entropy(logits, labels)
+    ref = F.cross_entropy(logits, labels)
+    torch.testing.assert_close(loss, ref, rtol=1e-5, atol=1e-6)
+    (g,) = torch.autograd.grad(loss, logits)
+    (gr,) = torch.autograd.grad(ref, logits)
+    torch.testing.assert_close(g, gr, rtol=1e-5, atol=1e-7)
+
+
+def test_xent_head_fused_dropout_colsum(native_lib):
+    B, C = 256, 64
+    p = 0.2
+    seed = (5, 6)
+    logits = torch.randn(B, C, device=DEV)
+    labels = torch.randint(0, C, (B,), device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    dh = torch.empty(B, C, device=DEV)
+    colsum = torch.zeros(C, device=DEV)
+    ei, ef = PF.epi_spec(drop_pre=9, p=p, seed=seed)
+    torch.ops.pz.xent_head(logits, labels, B, loss, 1.0 / B, dh, 1.0 / B, colsum, None, ei, ef, 0)
+    lref = F.cross_entropy(logits.double(), labels)
+    assert abs(loss.item() - lref.item()) < 1e-5
+    m = torch.from_numpy(keep_mask(B * C, *seed, 9, p).reshape(B, C)).to(DEV)
+    dref = (torch.softmax(logits.double(), 1) - F.one_hot(labels, C)) / B * m / (1 - p)
+    assert (dh.double() - dref).abs().max().item() < 1e-6
+    assert (colsum.double() - dref.sum(0)).abs().max().item() < 1e-5
+
+
+def test_mse_and_softmax(native_lib):
+    y = torch.randn(64, 10, device=DEV, dtype=torch.float64, requires_grad=True)
+    t = torch.randn(64, 10, device=DEV, dtype=torch.float64)
+    loss = PF.mse_loss(y, t)
+    ref = F.mse_loss(y, t)
+    torch.testing.assert_close(loss, ref, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(torch.autograd.grad(loss, y)[0], torch.autograd.grad(ref, y)[0], rtol=1e-6, atol=1e-9)
+    s = PF.softmax(y)
+    torch.testing.assert_close(s, torch.softmax(y, -1), rtol=1e-12, atol=1e-12)
+
+
+def test_adam_matches_torch(native_lib):
+    from penr_oz_neural_network_torch_amd.engine.optim import FusedOptimizer
+    from penr_oz_neural_network_torch_amd.engine.params import ParamStore
+    from penr_oz_neural_network_torch_amd.models.layers import LinearLayer
+    torch.manual_seed(0)
+    layers = [LinearLayer(33, 65, "random"), LinearLayer(65, 7, "random")]
+    ref_params = [p.detach().float().clone().to(DEV).requires_grad_() for l in layers for p in l.params]
+    store = ParamStore.adopt(layers, torch.device(DEV), torch.float32)
+    params = [p for l in layers for p in l.params]
+    opt = torch.optim.Adam(params, betas=(0.9, 0.99), eps=1e-7)
+    fused = FusedOptimizer(store, params, opt, {})
+    ref_opt = torch.optim.Adam(ref_params, lr=0.01, betas=(0.9, 0.99), eps=1e-7)
+    grads = torch.zeros(store.numel, device=DEV)
+    for it in range(5):
+        for seg in store.segments:
+            g = torch.randn(seg.shape, device=DEV)
+            store.view(seg, grads).copy_(g)
+            ref_params[seg.param_index].grad = g.clone()
+        fused.step(grads, 0.01, 0.0, 1.0)
+        ref_opt.step()
+    for seg in store.segments:
+        torch.testing.assert_close(store.view(seg), ref_params[seg.param_index].detach(), rtol=1e-5, atol=1e-6)
+
+
+def test_histogram_and_moments(native_lib):
+    x = torch.randn(10000, 7, device=DEV, dtype=torch.float64) * 3 + 1
+    s = PF.tensor_summary(x, "tanh", 100)
+    h = torch.histogram(x.cpu(), density=True)
+    assert abs(s["mean"] - x.mean().item()) < 1e-9
+    assert abs(s["std"] - x.std().item()) < 1e-9
+    assert abs(s["saturated"] - (x.abs() > 0.97).double().mean().item()) < 1e-12
+    np.testing.assert_allclose(s["histogram"]["x"], h.bin_edges[:-1].tolist(), rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(s["histogram"]["y"], h.hist.tolist(), rtol=1e-6, atol=1e-9)
+    e = torch.randn(50, 3, 10, device=DEV) * 2
+    se = PF.tensor_summary(e, "embedding", 100)
+    assert abs(se["saturated"] - (torch.norm(e, dim=-1) > 5.0).float().mean().item()) < 1e-9
+    sm = PF.tensor_summary(torch.softmax(e, -1), "softmax", 0)
+    assert abs(sm["saturated"] - (torch.softmax(e, -1).max(-1).values > 0.97).float().mean().item()) < 1e-9
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_batchnorm_matches_reference_formula(native_lib, dtype):
+    x = torch.randn(500, 3, 16, device=DEV, dtype=dtype, requires_grad=True)
+    gain = torch.rand(16, device=DEV, dtype=dtype, requires_grad=True)
+    bias = torch.randn(16, device=DEV, dtype=dtype, requires_grad=True)
+    rm = torch.zeros(16, device=DEV, dtype=dtype)
+    rv = torch.ones(16, device=DEV, dtype=dtype)
+    y, rm2, rv2 = PF.batchnorm(x, gain, bias, rm, rv, 1e-5, 0.1, True)
+    mean = x.mean((0, 1), keepdim=True)
+    var = x.var((0, 1), keepdim=True)
+    yr = gain * (x - mean) / torch.sqrt(var + 1e-5) + bias
+    tol = 1e-9 if dtype == torch.float64 else 1e-4
+    torch.testing.assert_close(y, yr, rtol=tol, atol=tol)
+    torch.testing.assert_close(rm2, (0.1 * mean).reshape(-1).detach(), rtol=tol, atol=tol)
+    g = torch.randn_like(y)
+    got = torch.autograd.grad(y, (x, gain, bias), g)
+    ref = torch.autograd.grad(yr, (x, gain, bias), g)
+    for a, b in zip(got, ref):
+        torch.testing.assert_close(a, b, rtol=1e-4 if dtype == torch.float32 else 1e-7,
+                                   atol=1e-4 if dtype == torch.float32 else 1e-9)
+
+
+def test_embedding_forward_backward(native_lib):
+    table = torch.randn(27, 10, device=DEV, dtype=torch.float64, requires_grad=True)
+    ids = torch.randint(0, 27, (64, 3), device=DEV).double()
+    out = PF.embedding(ids, table)
+    ref = table[ids.long()]
+    torch.testing.assert_close(out, ref)
+    g = torch.randn_like(out)
+    torch.testing.assert_close(torch.autograd.grad(out, table, g)[0], torch.autograd.grad(ref, table, g)[0],
+                               rtol=1e-12, atol=1e-12)
+
+
+def test_gather_rows_sampling(native_lib):
+    data = torch.arange(1000 * 4, device=DEV, dtype=torch.float32).view(1000, 4)
+    labels = torch.arange(1000, device=DEV)
+    out = torch.empty(128, 4, device=DEV, dtype=torch.bfloat16)
+    lab = torch.empty(128, device=DEV, dtype=torch.int64)
+    picked = torch.empty(128, device=DEV, dtype=torch.int64)
+    torch.ops.pz.gather_rows(data, None, 11, 22, out, 100, labels, lab, picked)
+    assert torch.equal(lab[:100], picked[:100])
+    assert (picked[:100] >= 0).all() and (picked[:100] < 1000).all()
+    torch.testing.assert_close(out[:100].float(), data[picked[:100]].to(torch.bfloat16).float())
+    assert (out[100:] == 0).all()
