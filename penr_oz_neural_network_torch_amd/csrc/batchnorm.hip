@@ -47,7 +47,7 @@ __global__ void __launch_bounds__(256) bn_col_sums_kernel(const T* __restrict__ 
 
 template <typename P>
 __global__ void bn_finalize_kernel(const double* partial, int n, int cols, P* running_mean, P* running_var, float eps,
-                                   float momentum, int training, float* save_mean, float* save_invstd) {
+                                   float momentum, int training, double* save_mean, double* save_invstd) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
   double mean, var;
@@ -61,8 +61,8 @@ __global__ void bn_finalize_kernel(const double* partial, int n, int cols, P* ru
     mean = static_cast<double>(running_mean[c]);
     var = static_cast<double>(running_var[c]);
   }
-  save_mean[c] = static_cast<float>(mean);
-  save_invstd[c] = static_cast<float>(1.0 / sqrt(var + eps));
+  save_mean[c] = mean;
+  save_invstd[c] = 1.0 / sqrt(var + static_cast<double>(eps));
 }
 
 template <typename T, typename P>

@@ -49,16 +49,14 @@ T* ptr_or_null(const optional<Tensor>& t) {
 pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
   pz::EpiSpec e{};
   e.act = pz::ACT_NONE;
-  e.drop_pre = -1;
-  e.drop_post = -1;
   e.scale = 1.f;
   e.inv_scale = 1.f;
-  if (ei.size() >= 7) {
+  if (ei.size() >= 7) {  // [act, drop_pre, drop_post, key_pre, key_post, thresh16, drop_all]
     e.act = static_cast<int>(ei[0]);
-    e.drop_pre = static_cast<int>(ei[1]);
-    e.drop_post = static_cast<int>(ei[2]);
-    e.seed_lo = static_cast<uint32_t>(ei[3]);
-    e.seed_hi = static_cast<uint32_t>(ei[4]);
+    e.drop_pre = ei[1] != 0;
+    e.drop_post = ei[2] != 0;
+    e.key_pre = static_cast<uint32_t>(ei[3]);
+    e.key_post = static_cast<uint32_t>(ei[4]);
     e.thresh16 = static_cast<uint32_t>(ei[5]);
     e.drop_all = static_cast<int>(ei[6]);
   }
@@ -364,8 +362,8 @@ void batchnorm_fwd_op(const Tensor& x, const Tensor& y, const Tensor& gain, cons
   a.eps = static_cast<float>(eps);
   a.momentum = static_cast<float>(momentum);
   a.training = training;
-  a.save_mean = save_mean.data_ptr<float>();
-  a.save_invstd = save_invstd.data_ptr<float>();
+  a.save_mean = save_mean.data_ptr<double>();
+  a.save_invstd = save_invstd.data_ptr<double>();
   a.partial = partial.data_ptr<double>();
   a.epi = make_epi(ei, ef);
   a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
@@ -390,8 +388,8 @@ void batchnorm_bwd_op(const Tensor& g, const Tensor& y, const Tensor& x, const o
   a.gain = gain.data_ptr();
   a.bias = bias.data_ptr();
   a.param_dtype = dt_of(gain);
-  a.save_mean = save_mean.data_ptr<float>();
-  a.save_invstd = save_invstd.data_ptr<float>();
+  a.save_mean = save_mean.data_ptr<double>();
+  a.save_invstd = save_invstd.data_ptr<double>();
   a.dgain = ptr_or_null(dgain);
   a.dbias = ptr_or_null(dbias);
   a.partial = partial.data_ptr<double>();

@@ -50,16 +50,42 @@ int grid_for(int64_t n) {
 // ---------------------------------------------------------------------------------------------
 // cross-entropy head: one wave per row
 // ---------------------------------------------------------------------------------------------
+// Row blocks: a 256-thread block owns kHeadRows rows (4 waves x kHeadRows/4 rows each). The
+// bias-gradient column sums are accumulated in LDS (ds_add_f32) and flushed with ONE global
+// atomic per column per block — per-element global atomics made this kernel 20x slower.
+constexpr int kHeadRows = 16;
+
+PZ_DEV void block_loss_flush(float* loss, float v, float* red) {
+  v = wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss, red[0] + red[1] + red[2] + red[3]);
+}
+
+PZ_DEV void block_colsum_flush(float* colsum, const float* cs, int cols) {
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256)
+    if (cs[c] != 0.f) atomicAdd(colsum + c, cs[c]);
+}
+
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
+  extern __shared__ float cs_lds[];  // [cols] when a.colsum (LDS column partials)
+  __shared__ float red[4];
   const T* __restrict__ logits = static_cast<const T*>(a.logits);
   T* __restrict__ dh = static_cast<T*>(a.dh);
   T* __restrict__ probs = static_cast<T*>(a.probs);
   const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  __shared__ float loss_part[4];
-  float row_loss = 0.f;
-  if (row < a.rows) {
+  const int wave = threadIdx.x >> 6;
+  const bool cs_on = a.colsum != nullptr && dh != nullptr;
+  if (cs_on) {
+    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = 0.f;
+    __syncthreads();
+  }
+  float loss_acc = 0.f;
+  for (int rr = 0; rr < kHeadRows / 4; ++rr) {
+    const int row = blockIdx.x * kHeadRows + wave * (kHeadRows / 4) + rr;
+    if (row >= a.rows) break;
     const T* lr = logits + static_cast<int64_t>(row) * a.ld;
     if (row < a.rows_valid) {
       F mx = -INFINITY;
@@ -73,7 +99,7 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
       const int64_t label = a.labels[row];
       const F lse = mx + log(se);
       const F inv = F(1) / se;
-      if (lane == 0) row_loss = static_cast<float>((lse - static_cast<F>(ldd<T>(lr, label))) * static_cast<F>(a.loss_scale));
+      if (lane == 0) loss_acc += static_cast<float>((lse - static_cast<F>(ldd<T>(lr, label))) * static_cast<F>(a.loss_scale));
       for (int c = lane; c < a.cols; c += 64) {
         const F pr = fexp(static_cast<F>(ldd<T>(lr, c)) - mx) * inv;
         if (probs != nullptr) std_<T>(probs, static_cast<int64_t>(row) * a.ld_probs + c, static_cast<double>(pr));
@@ -82,18 +108,104 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
           const uint64_t idx = static_cast<uint64_t>(row) * static_cast<uint64_t>(a.idx_ld) + c;
           g = epi_bwd<F>(g, F(0), idx, a.epi);
           std_<T>(dh, static_cast<int64_t>(row) * a.ld_dh + c, static_cast<double>(g));
-          if (a.colsum != nullptr) atomicAdd(a.colsum + c, static_cast<float>(g));
+          if (cs_on) atomicAdd(&cs_lds[c], static_cast<float>(g));
         }
       }
     } else if (dh != nullptr) {
       for (int c = lane; c < a.cols; c += 64) std_<T>(dh, static_cast<int64_t>(row) * a.ld_dh + c, 0.0);
     }
   }
-  if (a.loss != nullptr) {
-    if (lane == 0) loss_part[threadIdx.x >> 6] = row_loss;
+  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red);
+  if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
+}
+
+// bf16 fast path: every lane holds NCH chunks of 8 logits in registers (one read of the row),
+// 16-B loads / stores, dropout masks two hashes per 4 elements.
+template <int NCH>
+__global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
+  extern __shared__ float cs_lds[];
+  __shared__ float red[4];
+  const uint16_t* __restrict__ logits = static_cast<const uint16_t*>(a.logits);
+  uint16_t* __restrict__ dh = static_cast<uint16_t*>(a.dh);
+  uint16_t* __restrict__ probs = static_cast<uint16_t*>(a.probs);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const bool cs_on = a.colsum != nullptr && dh != nullptr;
+  if (cs_on) {
+    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = 0.f;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(a.loss, loss_part[0] + loss_part[1] + loss_part[2] + loss_part[3]);
   }
+  float loss_acc = 0.f;
+  for (int rr = 0; rr < kHeadRows / 4; ++rr) {
+    const int row = blockIdx.x * kHeadRows + wave * (kHeadRows / 4) + rr;
+    if (row >= a.rows) break;
+    const uint16_t* lr = logits + static_cast<int64_t>(row) * a.ld;
+    float v[NCH][8];
+    bool ok[NCH];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c0 = (lane + 64 * j) * 8;
+      ok[j] = c0 < a.cols;
+      uint4 u = ok[j] ? *reinterpret_cast<const uint4*>(lr + c0) : make_uint4(0, 0, 0, 0);
+      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[j][2 * e] = bf2f(w[e] & 0xFFFF); v[j][2 * e + 1] = bf2f(w[e] >> 16); }
+    }
+    if (row < a.rows_valid) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+        if (ok[j])
+#pragma unroll
+          for (int e = 0; e < 8; ++e) mx = fmaxf(mx, v[j][e]);
+      mx = wave_max(mx);
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          v[j][e] = ok[j] ? __expf(v[j][e] - mx) : 0.f;
+          se += v[j][e];
+        }
+      se = wave_sum(se);
+      const int64_t label = a.labels[row];
+      const float inv = 1.f / se;
+      if (lane == 0) loss_acc += (mx + __logf(se) - bf2f(lr[label])) * a.loss_scale;
+#pragma unroll
+      for (int j = 0; j < NCH; ++j) {
+        if (!ok[j]) continue;
+        const int c0 = (lane + 64 * j) * 8;
+        float pr[8], g[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          pr[e] = v[j][e] * inv;
+          g[e] = (pr[e] - (c0 + e == label ? 1.f : 0.f)) * a.grad_scale;
+        }
+        if (probs != nullptr)
+          *reinterpret_cast<uint4*>(probs + static_cast<int64_t>(row) * a.ld_probs + c0) =
+              make_uint4(pack_bf2(pr[0], pr[1]), pack_bf2(pr[2], pr[3]), pack_bf2(pr[4], pr[5]), pack_bf2(pr[6], pr[7]));
+        if (dh != nullptr) {
+          const uint64_t idx = static_cast<uint64_t>(row) * static_cast<uint64_t>(a.idx_ld) + c0;
+          const float zero4[4] = {0.f, 0.f, 0.f, 0.f};
+          epi_bwd4(g, zero4, idx, a.epi);
+          epi_bwd4(g + 4, zero4, idx + 4, a.epi);
+          *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + c0) =
+              make_uint4(pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7]));
+          if (cs_on)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) atomicAdd(&cs_lds[c0 + e], g[e]);
+        }
+      }
+    } else if (dh != nullptr) {
+#pragma unroll
+      for (int j = 0; j < NCH; ++j)
+        if (ok[j])
+          *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + (lane + 64 * j) * 8) =
+              make_uint4(0, 0, 0, 0);
+    }
+  }
+  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red);
+  if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -101,32 +213,38 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
 // ---------------------------------------------------------------------------------------------
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) mse_head_kernel(MseArgs a) {
+  extern __shared__ float cs_lds[];
+  __shared__ float red[4];
   const T* __restrict__ y = static_cast<const T*>(a.y);
   const T* __restrict__ t = static_cast<const T*>(a.target);
   T* __restrict__ dh = static_cast<T*>(a.dh);
-  __shared__ float part[4];
-  float acc = 0.f;
-  const int64_t n = static_cast<int64_t>(a.rows) * a.cols;
-  for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
-    const int64_t r = i / a.cols, c = i - r * a.cols;
-    F g = F(0);
-    if (r < a.rows_valid) {
-      const F yv = static_cast<F>(ldd<T>(y, r * a.ld_y + c));
-      const F d = yv - static_cast<F>(ldd<T>(t, r * a.ld_t + c));
-      acc += static_cast<float>(d * d * static_cast<F>(a.loss_scale));
-      g = epi_bwd<F>(F(2) * d * static_cast<F>(a.grad_scale), yv, static_cast<uint64_t>(r * a.idx_ld + c), a.epi);
-    }
-    if (dh != nullptr) {
-      std_<T>(dh, r * a.ld_dh + c, static_cast<double>(g));
-      if (a.colsum != nullptr && g != F(0)) atomicAdd(a.colsum + c, static_cast<float>(g));
-    }
-  }
-  if (a.loss != nullptr) {
-    acc = wave_sum(acc);
-    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = acc;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const bool cs_on = a.colsum != nullptr && dh != nullptr;
+  if (cs_on) {
+    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = 0.f;
     __syncthreads();
-    if (threadIdx.x == 0) atomicAdd(a.loss, part[0] + part[1] + part[2] + part[3]);
   }
+  float acc = 0.f;
+  for (int rr = 0; rr < kHeadRows / 4; ++rr) {
+    const int64_t r = static_cast<int64_t>(blockIdx.x) * kHeadRows + wave * (kHeadRows / 4) + rr;
+    if (r >= a.rows) break;
+    for (int c = lane; c < a.cols; c += 64) {
+      F g = F(0);
+      if (r < a.rows_valid) {
+        const F yv = static_cast<F>(ldd<T>(y, r * a.ld_y + c));
+        const F d = yv - static_cast<F>(ldd<T>(t, r * a.ld_t + c));
+        acc += static_cast<float>(d * d * static_cast<F>(a.loss_scale));
+        g = epi_bwd<F>(F(2) * d * static_cast<F>(a.grad_scale), yv, static_cast<uint64_t>(r * a.idx_ld + c), a.epi);
+      }
+      if (dh != nullptr) {
+        std_<T>(dh, r * a.ld_dh + c, static_cast<double>(g));
+        if (cs_on) atomicAdd(&cs_lds[c], static_cast<float>(g));
+      }
+    }
+  }
+  if (a.loss != nullptr) block_loss_flush(a.loss, acc, red);
+  if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -249,22 +367,57 @@ hipError_t stage_bwd(const void* g, const void* y, void* dx, int dtype, int64_t 
   return hipGetLastError();
 }
 
-hipError_t xent_head(const XentArgs& a, hipStream_t s) {
-  if (a.rows <= 0) return hipSuccess;
-  PZ_DISPATCH_FLOAT(a.dtype, T, {
-    using F = typename MathOf<T>::type;
-    hipLaunchKernelGGL((xent_head_kernel<T, F>), dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
-  });
+constexpr int kMaxLdsCols = 16384;  // 64 KiB of fp32 column partials
+
+hipError_t xent_head(const XentArgs& in, hipStream_t s) {
+  if (in.rows <= 0) return hipSuccess;
+  XentArgs a = in;
+  float* colsum_direct = nullptr;
+  if (a.colsum != nullptr && a.cols > kMaxLdsCols) {  // too wide for LDS partials: separate pass
+    colsum_direct = a.colsum;
+    a.colsum = nullptr;
+  }
+  const size_t lds = a.colsum != nullptr ? sizeof(float) * a.cols : 0;
+  const dim3 grid((a.rows + kHeadRows - 1) / kHeadRows);
+  const bool vec = a.dtype == DT_BF16 && a.cols % 8 == 0 && a.ld % 8 == 0 && (a.dh == nullptr || a.ld_dh % 8 == 0) &&
+                   (a.probs == nullptr || a.ld_probs % 8 == 0) && a.idx_ld % 2 == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.logits) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dh) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.probs) & 15) == 0;
+  if (vec && a.cols <= 512) hipLaunchKernelGGL(xent_head_bf16_kernel<1>, grid, dim3(256), lds, s, a);
+  else if (vec && a.cols <= 1024) hipLaunchKernelGGL(xent_head_bf16_kernel<2>, grid, dim3(256), lds, s, a);
+  else if (vec && a.cols <= 2048) hipLaunchKernelGGL(xent_head_bf16_kernel<4>, grid, dim3(256), lds, s, a);
+  else {
+    PZ_DISPATCH_FLOAT(a.dtype, T, {
+      using F = typename MathOf<T>::type;
+      hipLaunchKernelGGL((xent_head_kernel<T, F>), grid, dim3(256), lds, s, a);
+    });
+  }
+  if (colsum_direct != nullptr && a.dh != nullptr) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return colsum(a.dh, a.dtype, colsum_direct, a.rows, a.cols, s);  // ld_dh == cols required
+  }
   return hipGetLastError();
 }
 
-hipError_t mse_head(const MseArgs& a, hipStream_t s) {
-  const int64_t n = static_cast<int64_t>(a.rows) * a.cols;
-  if (n <= 0) return hipSuccess;
+hipError_t mse_head(const MseArgs& in, hipStream_t s) {
+  if (in.rows <= 0 || in.cols <= 0) return hipSuccess;
+  MseArgs a = in;
+  float* colsum_direct = nullptr;
+  if (a.colsum != nullptr && a.cols > kMaxLdsCols) {
+    colsum_direct = a.colsum;
+    a.colsum = nullptr;
+  }
+  const size_t lds = a.colsum != nullptr ? sizeof(float) * a.cols : 0;
   PZ_DISPATCH_FLOAT(a.dtype, T, {
     using F = typename MathOf<T>::type;
-    hipLaunchKernelGGL((mse_head_kernel<T, F>), dim3(grid_for(n)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((mse_head_kernel<T, F>), dim3((a.rows + kHeadRows - 1) / kHeadRows), dim3(256), lds, s, a);
   });
+  if (colsum_direct != nullptr && a.dh != nullptr) {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return colsum(a.dh, a.dtype, colsum_direct, a.rows, a.cols, s);
+  }
   return hipGetLastError();
 }
 

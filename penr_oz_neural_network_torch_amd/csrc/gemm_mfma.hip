@@ -4,21 +4,26 @@
 // autograd's two `mm` for dX / dW) plus the bias add (:119), activation (:172-184), dropout (:395)
 // and bias-gradient column sum that surround them.
 //
-// Design (CDNA4-first, see /opt/skills/guides/cdna_hip_programming.md §5):
+// Design (CDNA4-first, /opt/skills/guides/cdna_hip_programming.md §5):
 //  * 16x16x32 bf16 MFMA (v_mfma_f32_16x16x32_bf16), fp32 accumulation. Operands are issued
-//    SWAPPED (mfma(B, A)) so each lane ends up owning 4 consecutive output COLUMNS of one row:
-//    the epilogue then loads bias / aux and stores C with 8-16 B per lane.
-//  * Both operand layouts are first-class: a K-contiguous operand is staged as [rows][64]
-//    (128-B rows, XOR-swizzled 16-B chunks, read with ds_read_b128); an M/N-contiguous operand
-//    (the reference's [in,out] weights in the forward, activations in dW = Xᵀ·dH) is staged as
-//    [64][rows] and read with the gfx950 transposing ds_read_b64_tr_b16 — no transpose kernels,
-//    no second weight copy.
-//  * global→LDS by global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave-instruction), two LDS
-//    buffers, next tile issued before the current tile's MFMAs (2-phase pipeline, T3/T4 minimum).
-//    Swizzle is applied on the per-lane SOURCE address + the read (rule 21): LDS image stays
-//    lane-linear as the DMA requires.
+//    SWAPPED (mfma(B, A)) so each lane owns 4 consecutive output COLUMNS of one row: the epilogue
+//    loads bias / aux and stores C with 8-16 B per lane.
+//  * Both operand layouts are first-class. A K-contiguous operand is staged as [rows][32 k]
+//    (64-B rows, 16-B chunks XOR-swizzled per 4-row group, read with ds_read_b128); an
+//    M/N-contiguous operand (the reference's [in,out] weights in the forward, activations in
+//    dW = XᵀdZ) is staged as [32 k][rows] and read with the gfx950 transposing
+//    ds_read_b64_tr_b16 — no transpose kernels, no second weight copy.
+//  * global->LDS by global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave-instruction; swizzle on the
+//    per-lane SOURCE address + the read, rule 21).
+//  * Pipeline: a ring of NS = 4 LDS slots, each one 32-deep K step. Loads run NS-1 = 3 steps
+//    ahead; each step waits with a COUNTED `s_waitcnt vmcnt(2G)` (G = LDS-DMA instructions per
+//    wave per step) so the two younger steps stay in flight across the raw `s_barrier` — never a
+//    vmcnt(0) drain in the loop (guide "Pipelining across barriers", T3/T4). One barrier per step
+//    covers both hazards: RAW (every wave's DMA for slot t landed) and WAR (every wave's reads of
+//    slot t-1, which the step re-fills, completed: lgkmcnt(0) before the barrier).
+//  * MFMA clusters bracketed by s_setprio(1)/(0) (T5).
 //  * XCD-aware bijective block remap (T1) + grouped tile order for L2 reuse.
-//  * Tile configs 256x256 (8 waves), 256x128 (8 waves), 128x128 (4 waves, 2 blocks/CU) chosen
+//  * Tile configs 256x256 (8 waves), 256x128 (8 waves), 128x128 (4 waves, 2 blocks/CU), chosen
 //    per shape so the grid covers the 256 CUs.
 #include <type_traits>
 
@@ -28,9 +33,13 @@
 namespace pz {
 namespace {
 
-constexpr int kBK = 64;
+constexpr int kBK = 32;  // K depth of one ring slot
+constexpr int kNS = 4;   // ring slots
 
-PZ_DEV int swz_kc(int row) { return (row >> 1) & 7; }
+// K-contiguous slot [rows][32]: 64-B rows = 4 chunks; chunk XOR for conflict-free ds_read_b128
+// under the gfx950 b128 lane grouping (row groups of 4 rows map to permutation {0,2,3,1})
+PZ_DEV int swz_kc(int row) { return (120 >> (2 * ((row >> 2) & 3))) & 3; }
+// M/N-contiguous slot [32][R]: chunk XOR so a half-wave's transposed reads hit 16 distinct slots
 PZ_DEV int swz_mn(int krow) { return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1; }
 
 template <int BM, int BN, int WM, int WN>
@@ -43,37 +52,62 @@ struct Cfg {
   static constexpr int TN = WTN / 16;
   static constexpr int A_BYTES = BM * kBK * 2;
   static constexpr int B_BYTES = BN * kBK * 2;
-  static constexpr int STAGE_BYTES = A_BYTES + B_BYTES;
-  static constexpr int LDS_BYTES = 2 * STAGE_BYTES;
+  static constexpr int SLOT_BYTES = A_BYTES + B_BYTES;
+  static constexpr int LDS_BYTES = kNS * SLOT_BYTES;
+  static constexpr int GA = A_BYTES / 1024 / NW;  // LDS-DMA instructions per wave per slot
+  static constexpr int GB = B_BYTES / 1024 / NW;
+  static constexpr int G = GA + GB;
   static_assert(TM >= 1 && TN >= 1, "wave tile must hold at least one 16x16 MFMA tile");
-  static_assert((BM * 128) % (1024 * NW) == 0 && (BN * 128) % (1024 * NW) == 0, "stage split");
+  static_assert(GA >= 1 && GB >= 1 && GA * 1024 * NW == A_BYTES && GB * 1024 * NW == B_BYTES, "stage split");
+  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 };
 
-// K-contiguous operand rows [row0, row0+R) x k [k0, k0+64) -> LDS [R][64] (128-B rows)
+// LDS-DMA of 16 B per lane into wave-uniform LDS byte address `lds` (+ lane*16).
+// Inline asm ON PURPOSE: with the builtin, hipcc tracks the DMA as a pending LDS write and puts
+// an `s_waitcnt vmcnt(0)` in front of the next ds_read — draining the whole ring every step.
+// Hidden in asm, the DMA is counted only by our own `s_waitcnt vmcnt(N)` (guide §5.7 item 1).
+PZ_DEV void glds16(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
+      : "memory");
+}
+
+PZ_DEV uint32_t lds_addr(const PZ_LDS char* p) {
+  return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
+}
+
+// K-contiguous operand rows [row0, row0+R) x k [k0, k0+32) -> slot [R][32]
 template <int R, int NW>
 PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
                      PZ_LDS char* tile, int wave, int lane) {
-  constexpr int INSTR = R / (8 * NW);
+  constexpr int INSTR = R / (16 * NW);  // 16 rows of 64 B per 1-KiB instruction
 #pragma unroll
   for (int i = 0; i < INSTR; ++i) {
-    const int rbase = (wave * INSTR + i) * 8;
-    const int r = rbase + (lane >> 3);
-    const int chunk = (lane & 7) ^ swz_kc(r);
+    const int rbase = (wave * INSTR + i) * 16;
+    const int r = rbase + (lane >> 2);
+    const int chunk = (lane & 3) ^ swz_kc(r);
     int gr = row0 + r;
     gr = gr < rows_valid ? gr : rows_valid - 1;
     const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
-    __builtin_amdgcn_global_load_lds(src, (PZ_LDS void*)(tile + rbase * 128), 16, 0, 0);
+    glds16(src, lds_addr(tile + rbase * 64));
   }
 }
 
-// M/N-contiguous operand: k rows [k0, k0+64) x cols [col0, col0+R) -> LDS [64][R]
+// M/N-contiguous operand: k rows [k0, k0+32) x cols [col0, col0+R) -> slot [32][R]
 template <int R, int NW>
 PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int cols_valid, int k0,
                      PZ_LDS char* tile, int wave, int lane) {
   constexpr int ROW_BYTES = R * 2;
   constexpr int CHUNKS = R / 8;
   constexpr int ROWS_PER = 1024 / ROW_BYTES;
-  constexpr int INSTR = (64 * ROW_BYTES) / (1024 * NW);
+  constexpr int INSTR = (kBK * ROW_BYTES) / (1024 * NW);
 #pragma unroll
   for (int i = 0; i < INSTR; ++i) {
     const int kbase = (wave * INSTR + i) * ROWS_PER;
@@ -82,13 +116,13 @@ PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int c
     int gc = col0 + chunk * 8;
     gc = gc < cols_valid ? gc : cols_valid - 8;
     const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
-    __builtin_amdgcn_global_load_lds(src, (PZ_LDS void*)(tile + kbase * ROW_BYTES), 16, 0, 0);
+    glds16(src, lds_addr(tile + kbase * ROW_BYTES));
   }
 }
 
 PZ_DEV i16x8_t frag_kc(const PZ_LDS char* tile, int row, int chunk) {
   const int slot = chunk ^ swz_kc(row);
-  return *reinterpret_cast<const PZ_LDS i16x8_t*>(tile + row * 128 + slot * 16);
+  return *reinterpret_cast<const PZ_LDS i16x8_t*>(tile + row * 64 + slot * 16);
 }
 
 template <int R>
@@ -102,9 +136,14 @@ PZ_DEV i16x8_t frag_mn(const PZ_LDS char* tile, int col16, int kbase, int lane) 
   const int k1 = k0 + 4;
   const PZ_LDS char* a0 = tile + k0 * (R * 2) + ((chunk ^ swz_mn(k0)) << 4) + within;
   const PZ_LDS char* a1 = tile + k1 * (R * 2) + ((chunk ^ swz_mn(k1)) << 4) + within;
-  i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<PZ_LDS i16x4_t*>(const_cast<PZ_LDS char*>(a0)));
-  i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(reinterpret_cast<PZ_LDS i16x4_t*>(const_cast<PZ_LDS char*>(a1)));
+  i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((PZ_LDS i16x4_t*)(a0));
+  i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((PZ_LDS i16x4_t*)(a1));
   return i16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+}
+
+template <int N>
+PZ_DEV void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
 }
 
 template <typename OutT>
@@ -149,15 +188,11 @@ PZ_DEV f32x4_t epi_apply(const GemmArgs& p, f32x4_t a, f32x4_t bias4, int m, int
   if (p.epi_mode == EPI_BWD) {
     float y[4];
     load4<AuxT>(aux + static_cast<int64_t>(m) * p.ldaux + n, y);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] = epi_bwd(v[r], y[r], idx + r, p.epi);
+    epi_bwd4(v, y, idx, p.epi);
   } else {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] += bias4[r];
-    if (p.epi_mode == EPI_FWD) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = epi_fwd(v[r], idx + r, p.epi);
-    }
+    if (p.epi_mode == EPI_FWD) epi_fwd4(v, idx, p.epi);
   }
   OutT* dst = Cp + static_cast<int64_t>(m) * p.ldc + n;
   if (p.accumulate) {
@@ -208,8 +243,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
-  auto stage = [&](int kt, int buf) {
-    PZ_LDS char* base = smem + buf * C::STAGE_BYTES;
+  auto stage = [&](int kt, int slot) {
+    PZ_LDS char* base = smem + slot * C::SLOT_BYTES;
     const int k0 = kt * kBK;
     if constexpr (A_KC) stage_kc<BM, C::NW>(A, p.lda, m0, p.M, k0, base, wave, lane);
     else stage_mn<BM, C::NW>(A, p.lda, m0, p.M, k0, base, wave, lane);
@@ -218,34 +253,41 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   };
 
   const int nk = p.K / kBK;
-  stage(0, 0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
-    const PZ_LDS char* ta = smem + cur * C::STAGE_BYTES;
+#pragma unroll
+  for (int s = 0; s < kNS - 1; ++s)
+    if (s < nk) stage(s, s);
+
+  for (int t = 0; t < nk; ++t) {
+    // slot t landed: everything newer than step t (at most NS-2 steps) may stay in flight
+    const int newer = nk - 1 - t;
+    if (newer >= 2) wait_vm<2 * C::G>();
+    else if (newer == 1) wait_vm<C::G>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + kNS - 1 < nk) stage(t + kNS - 1, (t + kNS - 1) % kNS);
+
+    const PZ_LDS char* ta = smem + (t % kNS) * C::SLOT_BYTES;
     const PZ_LDS char* tb = ta + C::A_BYTES;
+    i16x8_t af[C::TM], bfr[C::TN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      i16x8_t af[C::TM], bfr[C::TN];
-#pragma unroll
-      for (int i = 0; i < C::TM; ++i) {
-        if constexpr (A_KC) af[i] = frag_kc(ta, wm * C::WTM + i * 16 + (lane & 15), kk * 4 + (lane >> 4));
-        else af[i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, kk * 32 + 8 * (lane >> 4), lane);
-      }
-#pragma unroll
-      for (int j = 0; j < C::TN; ++j) {
-        if constexpr (B_KC) bfr[j] = frag_kc(tb, wn * C::WTN + j * 16 + (lane & 15), kk * 4 + (lane >> 4));
-        else bfr[j] = frag_mn<BN>(tb, wn * C::WTN + j * 16, kk * 32 + 8 * (lane >> 4), lane);
-      }
-#pragma unroll
-      for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-        for (int j = 0; j < C::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
-                                                              __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j], 0, 0, 0);
+    for (int j = 0; j < C::TN; ++j) {
+      if constexpr (B_KC) bfr[j] = frag_kc(tb, wn * C::WTN + j * 16 + (lane & 15), lane >> 4);
+      else bfr[j] = frag_mn<BN>(tb, wn * C::WTN + j * 16, 8 * (lane >> 4), lane);
     }
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i) {
+      if constexpr (A_KC) af[i] = frag_kc(ta, wm * C::WTM + i * 16 + (lane & 15), lane >> 4);
+      else af[i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, 8 * (lane >> 4), lane);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                            __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -264,10 +306,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     static_for<C::TM>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       const int m = m0 + wm * C::WTM + i * 16 + (lane & 15);
-      if (n_ok && m < p.M) {
-        const f32x4_t v = epi_apply<OutT, AuxT>(p, acc[i][j], bias4, m, n, Cp, aux);
-        cs += v;
-      }
+      if (n_ok && m < p.M) cs += epi_apply<OutT, AuxT>(p, acc[i][j], bias4, m, n, Cp, aux);
     });
     if (p.colsum != nullptr) {
 #pragma unroll
@@ -327,6 +366,7 @@ bool mfma_eligible(const GemmArgs& p) {
   if (!al16(p.A) || !al16(p.B) || !al16(p.C)) return false;
   if (p.lda % 8 != 0 || p.ldb % 8 != 0) return false;
   if (!p.a_kc && p.M % 8 != 0) return false;
+  if (p.idx_ld % 2 != 0) return false;  // 4-element epilogue groups start at even element indices
   if (p.bias != nullptr && !al16(p.bias)) return false;
   if (p.epi_mode == EPI_BWD) {
     if (p.aux == nullptr || p.ldaux % 8 != 0 || (reinterpret_cast<uintptr_t>(p.aux) & 7) != 0) return false;

@@ -55,13 +55,10 @@ PZ_DEV uint32_t mix32(uint32_t x) {  // "lowbias32" integer finaliser
   return x;
 }
 // 32 random bits shared by the element pair (2j, 2j+1); each element uses 16 of them
-PZ_DEV uint32_t pair_bits(uint32_t pair, uint32_t seed_lo, uint32_t seed_hi, int lid) {
-  uint32_t h = mix32(pair ^ seed_lo);
-  return mix32(h ^ (seed_hi + 0x9E3779B9U * static_cast<uint32_t>(lid + 1)));
-}
-PZ_DEV bool keep_elem(uint64_t idx, uint32_t seed_lo, uint32_t seed_hi, int lid, uint32_t thresh16) {
-  uint32_t bits = pair_bits(static_cast<uint32_t>(idx >> 1), seed_lo, seed_hi, lid);
-  uint32_t r = (idx & 1) ? (bits >> 16) : (bits & 0xFFFFu);
+PZ_DEV uint32_t pair_bits(uint32_t pair, uint32_t key) { return mix32(pair ^ key); }
+PZ_DEV bool keep_elem(uint64_t idx, uint32_t key, uint32_t thresh16) {
+  const uint32_t bits = pair_bits(static_cast<uint32_t>(idx >> 1), key);
+  const uint32_t r = (idx & 1) ? (bits >> 16) : (bits & 0xFFFFu);
   return r >= thresh16;
 }
 
@@ -93,34 +90,84 @@ PZ_DEV F act_grad_from_out(F a, int act) {
   }
 }
 
-PZ_DEV bool epi_keep(const EpiSpec& e, int lid, uint64_t idx) {
+PZ_DEV bool epi_keep(const EpiSpec& e, uint32_t key, uint64_t idx) {
   if (e.drop_all) return false;
-  return keep_elem(idx, e.seed_lo, e.seed_hi, lid, e.thresh16);
+  return keep_elem(idx, key, e.thresh16);
 }
 
 // forward: x = producing-op output (bias already added), idx = logical element index
 template <typename F>
 PZ_DEV F epi_fwd(F x, uint64_t idx, const EpiSpec& e) {
-  if (e.drop_pre >= 0) x = epi_keep(e, e.drop_pre, idx) ? x * F(e.scale) : F(0);
+  if (e.drop_pre) x = epi_keep(e, e.key_pre, idx) ? x * F(e.scale) : F(0);
   x = act_fwd(x, e.act);
-  if (e.drop_post >= 0) x = epi_keep(e, e.drop_post, idx) ? x * F(e.scale) : F(0);
+  if (e.drop_post) x = epi_keep(e, e.key_post, idx) ? x * F(e.scale) : F(0);
   return x;
 }
 
 // backward: g = dLoss/dy, y = stored stage output; returns dLoss/dx (x as in epi_fwd)
 template <typename F>
 PZ_DEV F epi_bwd(F g, F y, uint64_t idx, const EpiSpec& e) {
-  if (e.drop_post >= 0) {
-    if (!epi_keep(e, e.drop_post, idx)) return F(0);
+  if (e.drop_post) {
+    if (!epi_keep(e, e.key_post, idx)) return F(0);
     g *= F(e.scale);
     y *= F(e.inv_scale);
   }
   if (e.act != ACT_NONE) g *= act_grad_from_out(y, e.act);
-  if (e.drop_pre >= 0) {
-    if (!epi_keep(e, e.drop_pre, idx)) return F(0);
+  if (e.drop_pre) {
+    if (!epi_keep(e, e.key_pre, idx)) return F(0);
     g *= F(e.scale);
   }
   return g;
+}
+
+// 4 consecutive elements starting at an EVEN index: two hashes per dropout layer
+PZ_DEV void keep4(const EpiSpec& e, uint32_t key, uint64_t idx, float m[4]) {
+  if (e.drop_all) { m[0] = m[1] = m[2] = m[3] = 0.f; return; }
+  const uint32_t p0 = static_cast<uint32_t>(idx >> 1);
+  const uint32_t b0 = mix32(p0 ^ key), b1 = mix32((p0 + 1) ^ key);
+  m[0] = (b0 & 0xFFFFu) >= e.thresh16 ? e.scale : 0.f;
+  m[1] = (b0 >> 16) >= e.thresh16 ? e.scale : 0.f;
+  m[2] = (b1 & 0xFFFFu) >= e.thresh16 ? e.scale : 0.f;
+  m[3] = (b1 >> 16) >= e.thresh16 ? e.scale : 0.f;
+}
+
+PZ_DEV void epi_fwd4(float v[4], uint64_t idx, const EpiSpec& e) {
+  if (e.drop_pre) {
+    float m[4];
+    keep4(e, e.key_pre, idx, m);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= m[r];
+  }
+  if (e.act != ACT_NONE) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = act_fwd(v[r], e.act);
+  }
+  if (e.drop_post) {
+    float m[4];
+    keep4(e, e.key_post, idx, m);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] *= m[r];
+  }
+}
+
+PZ_DEV void epi_bwd4(float g[4], const float y_in[4], uint64_t idx, const EpiSpec& e) {
+  float y[4] = {y_in[0], y_in[1], y_in[2], y_in[3]};
+  if (e.drop_post) {
+    float m[4];
+    keep4(e, e.key_post, idx, m);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) { g[r] *= m[r]; y[r] *= e.inv_scale; }
+  }
+  if (e.act != ACT_NONE) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[r] *= act_grad_from_out(y[r], e.act);
+  }
+  if (e.drop_pre) {
+    float m[4];
+    keep4(e, e.key_pre, idx, m);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) g[r] *= m[r];
+  }
 }
 
 // ------------------------------------------------------------------------------------------

@@ -138,8 +138,8 @@ struct BnArgs {
   void* running_var;
   float eps, momentum;
   int training;
-  float* save_mean;       // [cols] fp32 workspace (training)
-  float* save_invstd;     // [cols]
+  double* save_mean;      // [cols] workspace: statistics used by this pass
+  double* save_invstd;    // [cols]
   double* partial;        // workspace [2][cols] (sum, sumsq)
   EpiSpec epi;            // fused stage epilogue after the affine transform
   int64_t idx_ld;
@@ -155,8 +155,8 @@ struct BnBwdArgs {
   const void* gain;
   const void* bias;
   int param_dtype;
-  const float* save_mean;
-  const float* save_invstd;
+  const double* save_mean;
+  const double* save_invstd;
   void* dgain;            // [cols] accumulate (param dtype)
   void* dbias;
   double* partial;        // workspace [2][cols]

@@ -7,12 +7,17 @@ namespace pz {
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_SIGMOID = 2, ACT_TANH = 3 };
 
-// stage epilogue spec, passed by value inside kernel argument structs
+// Stage epilogue spec, passed by value inside kernel argument structs.
+// Dropout masks are a pure function of (key, element index): element pair j = idx/2 draws
+// bits = mix32(j ^ key); element idx uses the low (even idx) or high (odd idx) 16 bits and is
+// kept iff they are >= thresh16. Keys are derived per (seed, layer id) on the host
+// (ops/functional.py: layer_key), so each layer's mask is independent and the backward pass
+// regenerates it instead of reading a stored mask.
 struct EpiSpec {
   int act;            // Act applied between the two dropouts
-  int drop_pre;       // layer id of the dropout right after the producing op, -1 = none
-  int drop_post;      // layer id of the dropout after the activation, -1 = none
-  uint32_t seed_lo, seed_hi;
+  int drop_pre;       // != 0: dropout right after the producing op (key_pre)
+  int drop_post;      // != 0: dropout after the activation (key_post)
+  uint32_t key_pre, key_post;
   uint32_t thresh16;  // drop element iff its 16-bit draw < thresh16  (thresh16 = round(p * 65536))
   float scale;        // 1 / (1 - p)
   float inv_scale;    // (1 - p)

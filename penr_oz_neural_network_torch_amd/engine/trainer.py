@@ -249,8 +249,8 @@ class FusedTrainer:
             st.buffers["g"] = torch.empty(rows, st.out_width, device=dev, dtype=cd)
             if st.kind == "bn":
                 c = st.out_width
-                st.buffers["mean"] = torch.empty(c, device=dev, dtype=torch.float32)
-                st.buffers["invstd"] = torch.empty(c, device=dev, dtype=torch.float32)
+                st.buffers["mean"] = torch.empty(c, device=dev, dtype=torch.float64)
+                st.buffers["invstd"] = torch.empty(c, device=dev, dtype=torch.float64)
                 st.buffers["partial"] = torch.empty(2 * c, device=dev, dtype=torch.float64)
                 st.buffers["bn_in_grad"] = torch.empty(rows_b * st.pos_in, st.in_width, device=dev, dtype=cd)
         if pos != 1:

@@ -30,12 +30,32 @@ def _ops():
 # --------------------------------------------------------------------------------------------
 # epilogue specs
 # --------------------------------------------------------------------------------------------
+_M32 = 0xFFFFFFFF
+
+
+def mix32(x: int) -> int:
+    """The kernels' 32-bit integer finaliser ("lowbias32"), host side."""
+    x &= _M32
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & _M32
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & _M32
+    x ^= x >> 16
+    return x
+
+
+def layer_key(seed: tuple[int, int], lid: int) -> int:
+    """Per-(seed, layer) dropout key: the mask bit of element pair j is ``mix32(j ^ key)``."""
+    return mix32((seed[0] & _M32) ^ mix32((seed[1] + 0x9E3779B9 * (lid + 1)) & _M32))
+
+
 def epi_spec(act: int = ACT_NONE, drop_pre: int = -1, drop_post: int = -1, p: float = 0.0,
              seed: tuple[int, int] = (0, 0)) -> tuple[list[int], list[float]]:
     """Pack a stage epilogue ``drop_post(act(drop_pre(x)))`` for the kernels.
 
-    Dropout keeps an element iff its 16-bit counter-hash draw is ``>= round(p * 65536)``; kept
-    elements are scaled by ``1/(1-p)`` like ``torch.nn.functional.dropout``.
+    ``drop_pre`` / ``drop_post`` are the reference layer indices whose dropout is applied (-1 =
+    none). Dropout keeps an element iff its 16-bit counter-hash draw is ``>= round(p * 65536)``;
+    kept elements are scaled by ``1/(1-p)`` like ``torch.nn.functional.dropout``.
     """
     if p <= 0.0:
         drop_pre = drop_post = -1
@@ -43,8 +63,9 @@ def epi_spec(act: int = ACT_NONE, drop_pre: int = -1, drop_post: int = -1, p: fl
     thresh = min(65536, int(round(p * 65536)))
     scale = 0.0 if drop_all else 1.0 / (1.0 - p)
     inv_scale = 1.0 - p
-    return [act, drop_pre, drop_post, int(seed[0]) & 0xFFFFFFFF, int(seed[1]) & 0xFFFFFFFF, thresh, drop_all], \
-        [scale, inv_scale]
+    kpre = layer_key(seed, drop_pre) if drop_pre >= 0 else 0
+    kpost = layer_key(seed, drop_post) if drop_post >= 0 else 0
+    return [act, int(drop_pre >= 0), int(drop_post >= 0), kpre, kpost, thresh, drop_all], [scale, inv_scale]
 
 
 def new_seed() -> tuple[int, int]:
@@ -251,8 +272,8 @@ class _BatchNorm(torch.autograd.Function):
         xc = x.contiguous()
         y = torch.empty_like(xc)
         dev = x.device
-        save_mean = torch.empty(cols, device=dev, dtype=torch.float32)
-        save_inv = torch.empty(cols, device=dev, dtype=torch.float32)
+        save_mean = torch.empty(cols, device=dev, dtype=torch.float64)
+        save_inv = torch.empty(cols, device=dev, dtype=torch.float64)
         partial = torch.empty(2 * cols, device=dev, dtype=torch.float64)
         rows = xc.numel() // max(cols, 1)
         _ops().batchnorm_fwd(xc, y, gain.detach().contiguous(), bias.detach().contiguous(), rmean, rvar, eps,

@@ -1,6 +1,8 @@
 """Independent (numpy) re-implementations used as references by the kernel tests."""
 import numpy as np
 
+from penr_oz_neural_network_torch_amd.ops.functional import layer_key
+
 M32 = np.uint64(0xFFFFFFFF)
 
 
@@ -17,10 +19,8 @@ def _mix32(x: np.ndarray) -> np.ndarray:
 def keep_mask(numel: int, seed_lo: int, seed_hi: int, lid: int, p: float) -> np.ndarray:
     """Dropout keep-mask of the pz kernels for logical element indices 0..numel-1."""
     thresh = min(65536, int(round(p * 65536)))
+    key = np.uint64(layer_key((seed_lo, seed_hi), lid))
     idx = np.arange(numel, dtype=np.uint64)
-    pair = idx >> np.uint64(1)
-    h = _mix32(pair ^ np.uint64(seed_lo))
-    k = (np.uint64(seed_hi) + np.uint64(0x9E3779B9) * np.uint64(lid + 1)) & M32
-    bits = _mix32(h ^ k)
+    bits = _mix32((idx >> np.uint64(1)) ^ key)
     r = np.where(idx & np.uint64(1), bits >> np.uint64(16), bits & np.uint64(0xFFFF))
     return r >= np.uint64(thresh)

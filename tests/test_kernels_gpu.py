@@ -210,9 +210,9 @@ def test_histogram_and_moments(native_lib):
     np.testing.assert_allclose(s["histogram"]["y"], h.hist.tolist(), rtol=1e-6, atol=1e-9)
     e = torch.randn(50, 3, 10, device=DEV) * 2
     se = PF.tensor_summary(e, "embedding", 100)
-    assert abs(se["saturated"] - (torch.norm(e, dim=-1) > 5.0).float().mean().item()) < 1e-9
+    assert abs(se["saturated"] - (torch.norm(e, dim=-1) > 5.0).double().mean().item()) < 1e-12
     sm = PF.tensor_summary(torch.softmax(e, -1), "softmax", 0)
-    assert abs(sm["saturated"] - (torch.softmax(e, -1).max(-1).values > 0.97).float().mean().item()) < 1e-9
+    assert abs(sm["saturated"] - (torch.softmax(e, -1).max(-1).values > 0.97).double().mean().item()) < 1e-12
 
 
 @pytest.mark.parametrize("dtype", [torch.float64, torch.float32])

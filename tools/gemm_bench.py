@@ -1,0 +1,74 @@
+"""Micro-benchmark of the pz MFMA GEMM on the flagship step's shapes (+ hipBLASLt reference).
+
+Each case runs 30 timed launches after 5 warm-ups on random bf16 data; prints TFLOP/s for the
+fused-epilogue variant, the plain-store variant, and torch.matmul on the same operands.
+"""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, ".")
+from penr_oz_neural_network_torch_amd.ops import functional as PF  # noqa: E402
+
+
+def timeit(fn, n=30, w=5):
+    for _ in range(w):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e-3
+
+
+def main():
+    dev = "cuda"
+    B = 8192
+    cases = [  # name, M, N, K, a_kc, b_kc, out dtype, mode
+        ("fwd_L1", B, 4096, 1024, True, False, torch.bfloat16, "fwd"),
+        ("fwd_L2", B, 4096, 4096, True, False, torch.bfloat16, "fwd"),
+        ("fwd_L3", B, 1024, 4096, True, False, torch.bfloat16, "fwd_nodrop"),
+        ("dX_L3", B, 4096, 1024, True, True, torch.bfloat16, "bwd"),
+        ("dX_L2", B, 4096, 4096, True, True, torch.bfloat16, "bwd"),
+        ("dW_L3", 4096, 1024, B, False, False, torch.float32, "store"),
+        ("dW_L2", 4096, 4096, B, False, False, torch.float32, "store"),
+        ("dW_L1", 1024, 4096, B, False, False, torch.float32, "store"),
+    ]
+    only = sys.argv[1:] or None
+    out = {}
+    for name, M, N, K, akc, bkc, odt, mode in cases:
+        if only and name not in only:
+            continue
+        a = torch.randn((M, K) if akc else (K, M), device=dev).to(torch.bfloat16)
+        b = torch.randn((N, K) if bkc else (K, N), device=dev).to(torch.bfloat16)
+        c = torch.empty(M, N, device=dev, dtype=odt)
+        bias = torch.randn(N, device=dev)
+        aux = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        colsum = torch.zeros(N, device=dev)
+        epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=0.2, seed=(1, 2))
+        if mode == "fwd":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=epi)
+        elif mode == "fwd_nodrop":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD,
+                                    epi=PF.epi_spec(drop_pre=3, p=0.2, seed=(1, 2)))
+        elif mode == "bwd":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, aux=aux, colsum=colsum, mode=PF.EPI_BWD, epi=epi)
+        else:
+            fused = lambda: PF.gemm(a, akc, b, bkc, c)
+        plain = lambda: PF.gemm(a, akc, b, bkc, c)
+        A = a if akc else a.t()
+        Bm = b.t() if bkc else b
+        ref = lambda: torch.matmul(A, Bm)
+        fl = 2.0 * M * N * K
+        r = {"fused_TF": round(fl / timeit(fused) / 1e12, 1), "plain_TF": round(fl / timeit(plain) / 1e12, 1),
+             "hipblaslt_TF": round(fl / timeit(ref) / 1e12, 1)}
+        out[name] = r
+        print(name, r, flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
