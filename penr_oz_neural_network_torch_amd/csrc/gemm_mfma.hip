@@ -177,23 +177,16 @@ PZ_DEV void static_for(F&& f) {
   }
 }
 
-// one 4-column fragment of one output row: bias / fused stage epilogue / accumulate / store
+// fp32-output store epilogue (dW / plain GEMMs): alpha, bias, optional accumulate, 16-B stores.
+// The fused stage epilogues only exist for bf16 outputs (epilogue_lds); mfma_eligible routes
+// anything else to the generic kernel.
 template <typename OutT, typename AuxT>
 PZ_DEV f32x4_t epi_apply(const GemmArgs& p, f32x4_t a, f32x4_t bias4, int m, int n, OutT* __restrict__ Cp,
                          const AuxT* __restrict__ aux) {
+  (void)aux;
   float v[4];
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = a[r] * p.alpha;
-  const uint64_t idx = static_cast<uint64_t>(m) * static_cast<uint64_t>(p.idx_ld) + n;
-  if (p.epi_mode == EPI_BWD) {
-    float y[4];
-    load4<AuxT>(aux + static_cast<int64_t>(m) * p.ldaux + n, y);
-    epi_bwd4(v, y, idx, p.epi);
-  } else {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) v[r] += bias4[r];
-    if (p.epi_mode == EPI_FWD) epi_fwd4(v, idx, p.epi);
-  }
+  for (int r = 0; r < 4; ++r) v[r] = a[r] * p.alpha + bias4[r];
   OutT* dst = Cp + static_cast<int64_t>(m) * p.ldc + n;
   if (p.accumulate) {
     float old[4];
@@ -218,6 +211,8 @@ PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
   tm = first + in_group % gsz;
   tn = in_group / gsz;
 }
+
+#include "gemm_epilogue.h"
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
@@ -296,6 +291,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   OutT* __restrict__ Cp = static_cast<OutT*>(p.C);
   const AuxT* __restrict__ aux = static_cast<const AuxT*>(p.aux);
   const int g4 = 4 * (lane >> 4);
+  if constexpr (std::is_same<OutT, uint16_t>::value) {
+    epilogue_lds<BM, BN, WM, WN>(p, acc, smem, m0, n0, wm, wn, lane);
+  } else {
   static_for<C::TN>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
     const int n = n0 + wn * C::WTN + j * 16 + g4;
@@ -320,6 +318,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
       }
     }
   });
+  }
 }
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT>
@@ -367,9 +366,12 @@ bool mfma_eligible(const GemmArgs& p) {
   if (p.lda % 8 != 0 || p.ldb % 8 != 0) return false;
   if (!p.a_kc && p.M % 8 != 0) return false;
   if (p.idx_ld % 2 != 0) return false;  // 4-element epilogue groups start at even element indices
+  // fused stage epilogues: bf16 output only; accumulate: fp32 output only
+  if (p.out_dtype == DT_F32 && p.epi_mode != EPI_STORE) return false;
+  if (p.out_dtype == DT_BF16 && p.accumulate) return false;
   if (p.bias != nullptr && !al16(p.bias)) return false;
   if (p.epi_mode == EPI_BWD) {
-    if (p.aux == nullptr || p.ldaux % 8 != 0 || (reinterpret_cast<uintptr_t>(p.aux) & 7) != 0) return false;
+    if (p.aux == nullptr || p.ldaux % 8 != 0 || !al16(p.aux)) return false;
     if (p.aux_dtype != DT_BF16) return false;
   }
   return true;

@@ -23,6 +23,8 @@ typedef short i16x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x16_t __attribute__((ext_vector_type(16)));
 typedef double f64x4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2_t __attribute__((ext_vector_type(2)));  // LDS-friendly (HIP uint2/uint4 are not)
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
 
 namespace pz {
 
