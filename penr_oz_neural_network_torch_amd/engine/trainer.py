@@ -283,7 +283,9 @@ class FusedTrainer:
         self._alloc_progress(epochs)
 
     def step(self, epoch: int, lr: float, sample_size: int, dropout: float, l2: float, want_ratios: bool,
-             record: bool) -> None:
+             record: bool, indices: torch.Tensor | None = None) -> None:
+        """One training epoch. ``indices`` (int64, this rank's ``batch`` rows) overrides the
+        on-device sampler — used by the data-parallel equivalence tests."""
         world = self.ctx.world_size
         batch = max(1, sample_size // world) if world > 1 else sample_size
         self._ensure_buffers(batch)
@@ -298,7 +300,12 @@ class FusedTrainer:
         # ---------------- sample + input
         gseed = ((self.base_seed[0] + epoch * 0x632BE5AB) & 0xFFFFFFFF,
                  (self.base_seed[1] ^ (self.ctx.rank * 0x27D4EB2F + epoch)) & 0xFFFFFFFF)
-        ops.gather_rows(self.data, None, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked)
+        idx = None
+        if indices is not None:
+            idx = indices.to(device=self.dev, dtype=torch.int64).contiguous()
+            if idx.numel() < batch:
+                raise ValueError(f"need {batch} indices, got {idx.numel()}")
+        ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked)
         if self.tgt is not None:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 

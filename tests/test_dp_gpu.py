@@ -1,0 +1,84 @@
+"""Data-parallel equivalence: a 2-rank step == a 1-rank step on the concatenated batch.
+
+Both ranks share the box's single GPU and talk over ``gloo`` (RCCL refuses two ranks on one
+device); the code path under test — bucketed async all-reduce issued during backward, 1/world
+folded into the optimizer, loss averaged through the gradient buffer — is the one that runs
+over RCCL/xGMI on a full node.
+"""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [128, 256, 256, 64]
+ALGOS = ["relu", "tanh", "softmax"]
+N, B = 1024, 256  # dataset rows, per-rank batch
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _data():
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(N, SIZES[0], generator=g)
+    y = torch.randint(0, SIZES[-1], (N,), generator=g)
+    idx = torch.randint(0, N, (2 * B,), generator=g)
+    return x, y, idx
+
+
+def _build(optimizer):
+    from penr_oz_neural_network_torch_amd.models import NeuralNetworkModel
+    torch.manual_seed(0)
+    return NeuralNetworkModel("dp", SIZES, "xavier", "random", ALGOS, optimizer, dtype="float32", device="cuda:0")
+
+
+def _rank_main(rank, world, port, optimizer, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
+    from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
+    model = _build(optimizer)
+    tr = FusedTrainer(model, DataParallelContext(rank, world))
+    x, y, idx = _data()
+    tr.load_tensors(x, y, seed=3)
+    tr.begin(2)
+    for e in range(2):
+        tr.step(e, 0.01, 2 * B, 0.0, 1e-3, want_ratios=True, record=False, indices=idx[rank * B:(rank + 1) * B])
+    costs = [c for _, c, _, _ in tr.drain()]
+    if rank == 0:
+        torch.save({"flat": model._param_store.flat.cpu(), "costs": costs}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
+def test_two_rank_step_equals_single_rank(tmp_path, optimizer):
+    out = str(tmp_path / "dp.pt")
+    mp.start_processes(_rank_main, args=(2, _free_port(), optimizer, out), nprocs=2, start_method="spawn")
+    dp = torch.load(out, weights_only=True)
+
+    from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
+    model = _build(optimizer)
+    tr = FusedTrainer(model)
+    x, y, idx = _data()
+    tr.load_tensors(x, y, seed=3)
+    tr.begin(2)
+    for e in range(2):
+        tr.step(e, 0.01, 2 * B, 0.0, 1e-3, want_ratios=True, record=False, indices=idx)
+    costs = [c for _, c, _, _ in tr.drain()]
+    for a, b in zip(dp["costs"], costs):
+        assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (dp["costs"], costs)
+    d = (dp["flat"] - model._param_store.flat.cpu()).abs()
+    if optimizer == "adam":  # sign-noise flips of ~lr on near-zero gradients are legitimate
+        assert (d > 1e-3).double().mean().item() < 1e-3
+        assert d.mean().item() < 1e-5
+    else:
+        assert d.max().item() < 1e-6, d.max().item()
