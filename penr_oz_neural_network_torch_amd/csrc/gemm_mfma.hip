@@ -25,6 +25,7 @@
 //  * XCD-aware bijective block remap (T1) + grouped tile order for L2 reuse.
 //  * Tile configs 256x256 (8 waves), 256x128 (8 waves), 128x128 (4 waves, 2 blocks/CU), chosen
 //    per shape so the grid covers the 256 CUs.
+#include <cstdlib>
 #include <type_traits>
 
 #include "pz_common.h"
@@ -214,7 +215,7 @@ PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
 
 #include "gemm_epilogue.h"
 
-template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT>
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
   using C = Cfg<BM, BN, WM, WN>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -247,24 +248,19 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     else stage_mn<BN, C::NW>(B, p.ldb, n0, p.N, k0, base + C::A_BYTES, wave, lane);
   };
 
-  const int nk = p.K / kBK;
+  auto mfma_step = [&](const i16x8_t (&af)[C::TM], const i16x8_t (&bfr)[C::TN]) {
+    if constexpr (VAR == 0) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-  for (int s = 0; s < kNS - 1; ++s)
-    if (s < nk) stage(s, s);
-
-  for (int t = 0; t < nk; ++t) {
-    // slot t landed: everything newer than step t (at most NS-2 steps) may stay in flight
-    const int newer = nk - 1 - t;
-    if (newer >= 2) wait_vm<2 * C::G>();
-    else if (newer == 1) wait_vm<C::G>();
-    else wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t + kNS - 1 < nk) stage(t + kNS - 1, (t + kNS - 1) % kNS);
-
-    const PZ_LDS char* ta = smem + (t % kNS) * C::SLOT_BYTES;
+    for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
+                                                            __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j], 0, 0, 0);
+    if constexpr (VAR == 0) __builtin_amdgcn_s_setprio(0);
+  };
+  auto read_frags = [&](int slot, i16x8_t (&af)[C::TM], i16x8_t (&bfr)[C::TN]) {
+    const PZ_LDS char* ta = smem + slot * C::SLOT_BYTES;
     const PZ_LDS char* tb = ta + C::A_BYTES;
-    i16x8_t af[C::TM], bfr[C::TN];
 #pragma unroll
     for (int j = 0; j < C::TN; ++j) {
       if constexpr (B_KC) bfr[j] = frag_kc(tb, wn * C::WTN + j * 16 + (lane & 15), lane >> 4);
@@ -275,14 +271,63 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
       if constexpr (A_KC) af[i] = frag_kc(ta, wm * C::WTM + i * 16 + (lane & 15), lane >> 4);
       else af[i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, 8 * (lane >> 4), lane);
     }
-    __builtin_amdgcn_s_setprio(1);
+  };
+  auto barrier = [] {
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int nk = p.K / kBK;
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i)
-#pragma unroll
-      for (int j = 0; j < C::TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
-                                                            __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+  for (int s = 0; s < kNS - 1; ++s)
+    if (s < nk) stage(s, s);
+
+  if constexpr (C::NW == 8) {
+    // Ping-pong (8 waves = 2 per SIMD). Waves 0-3 and 4-7 sit on the same four SIMDs and run one
+    // barrier interval apart: while one wave of a SIMD issues its MFMA block (setprio 1) its
+    // partner issues the next step's LDS-DMA + fragment reads into the MFMA gaps. Per wave and
+    // step t: R_t = {stage t+3, wait until step t+1 landed, read slot t, lgkmcnt(0)} | barrier |
+    // M_t = {MFMAs} | barrier. Hazards: slot t+1 is waited for by BOTH groups during R_t, at
+    // least one barrier before either group reads it in R_{t+1}; slot (t+3)%4 = (t-1)%4 was
+    // last read in R_{t-1} and every wave retired those reads (lgkmcnt(0)) before the barrier
+    // that precedes R_t of either group.
+    const int grp = wave >> 2;
+    wait_vm<(kNS - 2) * C::G>();  // step 0 landed (steps 1, 2 may still fly; nk >= 3 not assumed)
+    if (nk < 3) wait_vm<0>();
+    barrier();
+    if (grp == 1) barrier();
+    if constexpr (VAR == 1) {
+      if (grp == 1) __builtin_amdgcn_s_setprio(1);
+    }
+    for (int t = 0; t < nk; ++t) {
+      if (t + kNS - 1 < nk) stage(t + kNS - 1, (t + kNS - 1) % kNS);
+      const int newer = min(nk - 1, t + kNS - 1) - (t + 1);  // steps issued after step t+1
+      if (newer >= 2) wait_vm<2 * C::G>();
+      else if (newer == 1) wait_vm<C::G>();
+      else wait_vm<0>();
+      i16x8_t af[C::TM], bfr[C::TN];
+      read_frags(t % kNS, af, bfr);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier();
+      mfma_step(af, bfr);
+      barrier();
+    }
+    if (grp == 0) barrier();
+    if constexpr (VAR == 1) __builtin_amdgcn_s_setprio(0);
+  } else
+  for (int t = 0; t < nk; ++t) {
+    // slot t landed: everything newer than step t (at most NS-2 steps) may stay in flight
+    const int newer = nk - 1 - t;
+    if (newer >= 2) wait_vm<2 * C::G>();
+    else if (newer == 1) wait_vm<C::G>();
+    else wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + kNS - 1 < nk) stage(t + kNS - 1, (t + kNS - 1) % kNS);
+    i16x8_t af[C::TM], bfr[C::TN];
+    read_frags(t % kNS, af, bfr);
+    mfma_step(af, bfr);
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -321,10 +366,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   }
 }
 
-template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT>
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
   using C = Cfg<BM, BN, WM, WN>;
-  auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT>;
+  auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -337,18 +382,29 @@ hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int BM, int BN, int WM, int WN, typename OutT, typename AuxT>
+template <int BM, int BN, int WM, int WN, typename OutT, typename AuxT, int VAR = 0>
 hipError_t launch_layout(const GemmArgs& p, hipStream_t s) {
-  if (p.a_kc && p.b_kc) return launch_cfg<BM, BN, WM, WN, true, true, OutT, AuxT>(p, s);
-  if (p.a_kc && !p.b_kc) return launch_cfg<BM, BN, WM, WN, true, false, OutT, AuxT>(p, s);
-  if (!p.a_kc && p.b_kc) return launch_cfg<BM, BN, WM, WN, false, true, OutT, AuxT>(p, s);
-  return launch_cfg<BM, BN, WM, WN, false, false, OutT, AuxT>(p, s);
+  if (p.a_kc && p.b_kc) return launch_cfg<BM, BN, WM, WN, true, true, OutT, AuxT, VAR>(p, s);
+  if (p.a_kc && !p.b_kc) return launch_cfg<BM, BN, WM, WN, true, false, OutT, AuxT, VAR>(p, s);
+  if (!p.a_kc && p.b_kc) return launch_cfg<BM, BN, WM, WN, false, true, OutT, AuxT, VAR>(p, s);
+  return launch_cfg<BM, BN, WM, WN, false, false, OutT, AuxT, VAR>(p, s);
 }
 
 template <typename OutT, typename AuxT>
 hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   auto tiles = [&](int bm, int bn) { return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
   constexpr int kFill = 240;  // ~ CU count: a config below this leaves CUs idle
+  static const int forced = [] {  // experiments: PZ_GEMM_TILE=1 (256x256x4 waves) 2 (256x256x8) 3 (256x128) 4 (128x128)
+    const char* e = getenv("PZ_GEMM_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  switch (forced) {
+    case 1: return launch_layout<256, 256, 2, 4, OutT, AuxT, 1>(p, s);
+    case 2: return launch_layout<256, 256, 2, 4, OutT, AuxT, 2>(p, s);
+    case 3: return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
+    case 4: return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
+    default: break;
+  }
   if (tiles(256, 256) >= kFill) return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
   if (tiles(256, 128) >= kFill) return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
   return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
