@@ -71,7 +71,8 @@ pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
 pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C,
                        const optional<Tensor>& bias, const optional<Tensor>& aux, const optional<Tensor>& colsum,
                        int64_t epi_mode, at::IntArrayRef epi_i, at::ArrayRef<double> epi_f, double alpha,
-                       bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld, bool force_generic) {
+                       bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld, bool force_generic,
+                       const optional<Tensor>& mask = c10::nullopt) {
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "pz::gemm: 2-D operands expected");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "pz::gemm: unit inner stride expected");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "pz::gemm: A/B dtype mismatch");
@@ -112,23 +113,31 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   p.epi = make_epi(epi_i, epi_f);
   p.idx_ld = idx_ld > 0 ? idx_ld : N;
   p.force_generic = force_generic;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->dim() == 2 && mask->stride(1) == 1 && mask->size(0) >= M &&
+                    mask->size(1) >= (N + 63) / 64 * 8,
+                "pz::gemm: mask must be uint8 [M, ceil(N/64)*8]");
+    p.mask = mask->data_ptr<uint8_t>();
+    p.ldmask = mask->stride(0);
+  }
   return p;
 }
 
 void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, const optional<Tensor>& bias,
              const optional<Tensor>& aux, const optional<Tensor>& colsum, int64_t epi_mode, at::IntArrayRef epi_i,
              at::ArrayRef<double> epi_f, double alpha, bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld,
-             bool force_generic) {
+             bool force_generic, const optional<Tensor>& mask) {
   check_dev(A, "A");
   auto p = gemm_args(A, a_kc, B, b_kc, C, bias, aux, colsum, epi_mode, epi_i, epi_f, alpha, accumulate, M, N, K, idx_ld,
-                     force_generic);
+                     force_generic, mask);
+  TORCH_CHECK(p.mask == nullptr || pz::gemm_path(p) == 1, "pz::gemm: a mask epilogue needs an MFMA-eligible shape");
   PZ_HIP_CHECK(pz::gemm(p, cur_stream(A)));
 }
 
 int64_t gemm_path_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, int64_t M, int64_t N,
                      int64_t K) {
   auto p = gemm_args(A, a_kc, B, b_kc, C, c10::nullopt, c10::nullopt, c10::nullopt, 0, {}, {}, 1.0, false, M, N, K, 0,
-                     false);
+                     false, c10::nullopt);
   return pz::gemm_path(p);
 }
 
@@ -462,7 +471,7 @@ std::string repr_double_op(double x) { return pz::repr_double(x); }
 TORCH_LIBRARY(pz, m) {
   m.def("gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor(a!) C, Tensor? bias, Tensor? aux, Tensor(b!)? colsum, "
         "int epi_mode, int[] epi_i, float[] epi_f, float alpha, bool accumulate, int M, int N, int K, int idx_ld, "
-        "bool force_generic) -> ()");
+        "bool force_generic, Tensor(c!)? mask=None) -> ()");
   m.def("gemm_path(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor C, int M, int N, int K) -> int");
   m.def("stage_fwd(Tensor x, Tensor(a!) y, int[] epi_i, float[] epi_f) -> ()");
   m.def("stage_bwd(Tensor g, Tensor y, Tensor(a!) dx, int[] epi_i, float[] epi_f) -> ()");

@@ -6,7 +6,10 @@
 //      per enabled transform (bias, dropout-pre, activation, dropout-post or their derivatives).
 //      Branches sit outside the unrolled fragment loops, so the code is the SUM of the passes,
 //      not their product (a per-fragment switch produced ~5k basic blocks and I-cache stalls);
-//   3. results go to the LDS image as bf16 and leave it as full 16-B-per-lane row segments.
+//   3. results go to the LDS image as bf16 and leave it as full 16-B-per-lane row segments;
+//   4. ReLU stages: the forward also writes a 1-bit-per-element mask of y > 0, and the backward
+//      reads 8 mask bytes per accumulator row instead of the 512-B aux row segment (dX GEMMs
+//      with K = 1024 spent a third of their time streaming the bf16 aux tile).
 // Image layout: row r holds BN bf16; 16-B chunk c of row r lives at chunk c ^ (r & 15).
 #pragma once
 
@@ -68,6 +71,18 @@ PZ_DEV void act_bwd_row(f32x4_t (&v)[TN], const PZ_LDS char* img, int ml, int nl
 #undef PZ_ACTB_LOOP
 }
 
+// v *= relu'(.) from the stage's ReLU bitmask: `bits` = the 64 mask bits of the wave's 64 columns
+// of this row (bit c = column c of the wave tile); fragment j, element r sits at 16j + g4 + r
+template <int TN>
+PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[TN], u32x2_t bits, int g4) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const uint32_t w = bits[j >> 1] >> (16 * (j & 1) + g4);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[j][r] = ((w >> r) & 1u) ? v[j][r] : 0.f;
+  }
+}
+
 template <int BM, int BN, int WM, int WN>
 PZ_DEV void epilogue_lds(const GemmArgs& p, f32x4_t (&acc)[BM / WM / 16][BN / WN / 16], PZ_LDS char* smem, int m0,
                          int n0, int wm, int wn, int lane) {
@@ -88,9 +103,24 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, f32x4_t (&acc)[BM / WM / 16][BN / WN
   const uint32_t pair0 =
       static_cast<uint32_t>((static_cast<uint64_t>(m0 + ml0) * static_cast<uint64_t>(p.idx_ld) + n0 + nl0) >> 1);
   const uint32_t row_pairs = static_cast<uint32_t>(p.idx_ld) * 8u;  // 16 rows down, in pairs
+  static_assert(C::WTN == 64, "the ReLU bitmask epilogue assumes 64-column wave tiles");
+  const bool use_mask = p.mask != nullptr;
+
+  // ReLU bitmask (EPI_BWD): 8 bytes per accumulator row, issued before the barrier so the
+  // loads fly while the slower waves finish their last MFMAs
+  u32x2_t mbits[TM];
+  if (bwd && use_mask) {
+    const uint8_t* mrow = p.mask + (n0 + wn * C::WTN) / 8;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int m = m0 + ml0 + 16 * i;
+      mbits[i] = m < p.M ? *reinterpret_cast<const u32x2_t*>(mrow + static_cast<int64_t>(m) * p.ldmask)
+                         : u32x2_t{0u, 0u};
+    }
+  }
 
   __syncthreads();  // every wave is done reading the ring
-  if (bwd) {
+  if (bwd && !use_mask) {
     const uint16_t* __restrict__ aux = static_cast<const uint16_t*>(p.aux);
     u32x4_t v[PASSES];
 #pragma unroll
@@ -130,7 +160,8 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, f32x4_t (&acc)[BM / WM / 16][BN / WN
       }
     } else {
       if (e.drop_post) dropout_row(v, e, e.key_post, pr0);
-      if (e.act != ACT_NONE) act_bwd_row<BN>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
+      if (use_mask) act_bwd_mask_row(v, mbits[i], g4);
+      else if (e.act != ACT_NONE) act_bwd_row<BN>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
       if (e.drop_pre) dropout_row(v, e, e.key_pre, pr0);
     }
 #pragma unroll
@@ -165,6 +196,18 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, f32x4_t (&acc)[BM / WM / 16][BN / WN
     const int r = s * ROWS_PER_PASS + my_row;
     const int gm = m0 + r, gn = n0 + my_chunk * 8;
     const u32x4_t v = *reinterpret_cast<const PZ_LDS u32x4_t*>(smem + cimg_off<BN>(r, my_chunk * 8));
-    if (gm < p.M && gn < p.N) *reinterpret_cast<u32x4_t*>(Cp + static_cast<int64_t>(gm) * p.ldc + gn) = v;
+    if (gm < p.M && gn < p.N) {
+      *reinterpret_cast<u32x4_t*>(Cp + static_cast<int64_t>(gm) * p.ldc + gn) = v;
+      if (!bwd && use_mask) {  // bit b = element gn+b > 0 (bf16: sign clear, magnitude nonzero)
+        uint32_t byte = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t lo = v[q] & 0xFFFFu, hi = v[q] >> 16;
+          byte |= ((lo - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q);
+          byte |= ((hi - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q + 1);
+        }
+        p.mask[static_cast<int64_t>(gm) * p.ldmask + gn / 8] = static_cast<uint8_t>(byte);
+      }
+    }
   }
 }

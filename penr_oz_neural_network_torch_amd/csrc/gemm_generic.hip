@@ -141,6 +141,7 @@ int gemm_path(const GemmArgs& p) { return mfma_eligible(p) ? 1 : 0; }
 
 hipError_t gemm(const GemmArgs& p, hipStream_t s) {
   if (mfma_eligible(p)) return gemm_mfma(p, s);
+  if (p.mask != nullptr) return hipErrorInvalidValue;  // bitmask epilogues exist on the MFMA path only
   return gemm_generic(p, s);
 }
 

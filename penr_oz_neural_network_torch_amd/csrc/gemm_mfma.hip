@@ -15,9 +15,9 @@
 //    ds_read_b64_tr_b16 — no transpose kernels, no second weight copy.
 //  * global->LDS by global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave-instruction; swizzle on the
 //    per-lane SOURCE address + the read, rule 21).
-//  * Pipeline: a ring of NS = 4 LDS slots, each one 32-deep K step. Loads run NS-1 = 3 steps
-//    ahead; each step waits with a COUNTED `s_waitcnt vmcnt(2G)` (G = LDS-DMA instructions per
-//    wave per step) so the two younger steps stay in flight across the raw `s_barrier` — never a
+//  * Pipeline: a ring of NS = 4 LDS slots, each one 32-deep K step. Loads run NS-1 steps
+//    ahead; each step waits with a COUNTED `s_waitcnt vmcnt((NS-2)G)` (G = LDS-DMA instructions per
+//    wave per step) so the NS-2 younger steps stay in flight across the raw `s_barrier` — never a
 //    vmcnt(0) drain in the loop (guide "Pipelining across barriers", T3/T4). One barrier per step
 //    covers both hazards: RAW (every wave's DMA for slot t landed) and WAR (every wave's reads of
 //    slot t-1, which the step re-fills, completed: lgkmcnt(0) before the barrier).
@@ -35,7 +35,6 @@ namespace pz {
 namespace {
 
 constexpr int kBK = 32;  // K depth of one ring slot
-constexpr int kNS = 4;   // ring slots
 
 // K-contiguous slot [rows][32]: 64-B rows = 4 chunks; chunk XOR for conflict-free ds_read_b128
 // under the gfx950 b128 lane grouping (row groups of 4 rows map to permutation {0,2,3,1})
@@ -45,6 +44,10 @@ PZ_DEV int swz_mn(int krow) { return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 
 
 template <int BM, int BN, int WM, int WN>
 struct Cfg {
+  // ring depth in 32-deep K slots. Measured on the step's GEMMs: 5 slots for 256x256 (160 KiB)
+  // and 6 for 256x128 are 2-4% SLOWER than 4 (the DMA stream is throughput-, not latency-bound),
+  // and 5 slots for 128x128 drop it to one workgroup per CU (-20%).
+  static constexpr int NS = 4;
   static constexpr int NW = WM * WN;
   static constexpr int NT = NW * 64;
   static constexpr int WTM = BM / WM;
@@ -54,7 +57,7 @@ struct Cfg {
   static constexpr int A_BYTES = BM * kBK * 2;
   static constexpr int B_BYTES = BN * kBK * 2;
   static constexpr int SLOT_BYTES = A_BYTES + B_BYTES;
-  static constexpr int LDS_BYTES = kNS * SLOT_BYTES;
+  static constexpr int LDS_BYTES = NS * SLOT_BYTES;
   static constexpr int GA = A_BYTES / 1024 / NW;  // LDS-DMA instructions per wave per slot
   static constexpr int GB = B_BYTES / 1024 / NW;
   static constexpr int G = GA + GB;
@@ -145,6 +148,17 @@ PZ_DEV i16x8_t frag_mn(const PZ_LDS char* tile, int col16, int kbase, int lane) 
 template <int N>
 PZ_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// wait until at most n (<= MAXN) younger ring steps of G LDS-DMA instructions each are in flight
+template <int G, int MAXN>
+PZ_DEV void wait_newer(int n) {
+  if constexpr (MAXN == 0) {
+    wait_vm<0>();
+  } else {
+    if (n >= MAXN) wait_vm<MAXN * G>();
+    else wait_newer<G, MAXN - 1>(n);
+  }
 }
 
 template <typename OutT>
@@ -249,14 +263,14 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   };
 
   auto mfma_step = [&](const i16x8_t (&af)[C::TM], const i16x8_t (&bfr)[C::TN]) {
-    if constexpr (VAR == 0) __builtin_amdgcn_s_setprio(1);
+    __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
       for (int j = 0; j < C::TN; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
                                                             __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j], 0, 0, 0);
-    if constexpr (VAR == 0) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
   };
   auto read_frags = [&](int slot, i16x8_t (&af)[C::TM], i16x8_t (&bfr)[C::TN]) {
     const PZ_LDS char* ta = smem + slot * C::SLOT_BYTES;
@@ -278,55 +292,107 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  auto stage_a = [&](int kt) {
+    PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
+    if constexpr (A_KC) stage_kc<BM, C::NW>(A, p.lda, m0, p.M, kt * kBK, base, wave, lane);
+    else stage_mn<BM, C::NW>(A, p.lda, m0, p.M, kt * kBK, base, wave, lane);
+  };
+  auto stage_b = [&](int kt) {
+    PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
+    if constexpr (B_KC) stage_kc<BN, C::NW>(B, p.ldb, n0, p.N, kt * kBK, base, wave, lane);
+    else stage_mn<BN, C::NW>(B, p.ldb, n0, p.N, kt * kBK, base, wave, lane);
+  };
+
   const int nk = p.K / kBK;
+  constexpr int NS = C::NS;
+  // K-contiguous operands in the 8-wave schedule are staged in PAIRS of steps (t, t+1), the two
+  // 64-B halves of every 128-B row line back to back: one L2 request per line instead of two.
+  constexpr bool PAIR = C::NW == 8 && NS == 4 && (A_KC || B_KC) && VAR != 4;
+  if constexpr (PAIR) {
+    for (int s = 0; s < (A_KC ? 2 : 3); ++s)
+      if (s < nk) stage_a(s);
+    for (int s = 0; s < (B_KC ? 2 : 3); ++s)
+      if (s < nk) stage_b(s);
+  } else {
 #pragma unroll
-  for (int s = 0; s < kNS - 1; ++s)
-    if (s < nk) stage(s, s);
+    for (int s = 0; s < NS - 1; ++s)
+      if (s < nk) stage(s, s);
+  }
 
   if constexpr (C::NW == 8) {
     // Ping-pong (8 waves = 2 per SIMD). Waves 0-3 and 4-7 sit on the same four SIMDs and run one
     // barrier interval apart: while one wave of a SIMD issues its MFMA block (setprio 1) its
     // partner issues the next step's LDS-DMA + fragment reads into the MFMA gaps. Per wave and
-    // step t: R_t = {stage t+3, wait until step t+1 landed, read slot t, lgkmcnt(0)} | barrier |
-    // M_t = {MFMAs} | barrier. Hazards: slot t+1 is waited for by BOTH groups during R_t, at
-    // least one barrier before either group reads it in R_{t+1}; slot (t+3)%4 = (t-1)%4 was
-    // last read in R_{t-1} and every wave retired those reads (lgkmcnt(0)) before the barrier
-    // that precedes R_t of either group.
+    // step t: R_t = {stage t+NS-1, wait until step t+1 landed, read slot t, lgkmcnt(0)} |
+    // barrier | M_t = {MFMAs} | barrier. Hazards: slot t+1 is waited for by BOTH groups during
+    // R_t, at least one barrier before either group reads it in R_{t+1}; slot (t+NS-1)%NS =
+    // (t-1)%NS was last read in R_{t-1} and every wave retired those reads (lgkmcnt(0)) before
+    // the barrier that precedes R_t of either group.
+    //
+    // PAIR staging: even steps t stage K-contiguous operands for t+2 and t+3, M/N-contiguous
+    // ones stage t+3 every step (A before B, pair halves adjacent). In steady state (t+4 < nk)
+    // the instructions younger than the last one of step t+1 are: even t: 2G; odd t: whatever
+    // of steps t+2, t+3 was issued after it (per layout below). Tail steps drain to vmcnt(0).
     const int grp = wave >> 2;
-    wait_vm<(kNS - 2) * C::G>();  // step 0 landed (steps 1, 2 may still fly; nk >= 3 not assumed)
-    if (nk < 3) wait_vm<0>();
+    if constexpr (PAIR) wait_vm<0>();
+    else wait_newer<C::G, NS - 2>(min(nk, NS - 1) - 1);  // step 0 landed
     barrier();
     if (grp == 1) barrier();
-    if constexpr (VAR == 1) {
-      if (grp == 1) __builtin_amdgcn_s_setprio(1);
-    }
+    constexpr int ODD_INFLIGHT = A_KC && B_KC ? C::GB : (A_KC ? C::GA + 2 * C::GB : C::GA + C::GB);
     for (int t = 0; t < nk; ++t) {
-      if (t + kNS - 1 < nk) stage(t + kNS - 1, (t + kNS - 1) % kNS);
-      const int newer = min(nk - 1, t + kNS - 1) - (t + 1);  // steps issued after step t+1
-      if (newer >= 2) wait_vm<2 * C::G>();
-      else if (newer == 1) wait_vm<C::G>();
-      else wait_vm<0>();
+      if constexpr (PAIR) {
+        if (VAR != 2) {
+          if (A_KC) {
+            if ((t & 1) == 0 && t + 2 < nk) stage_a(t + 2);
+            if ((t & 1) == 0 && t + 3 < nk) stage_a(t + 3);
+          } else if (t + 3 < nk) {
+            stage_a(t + 3);
+          }
+          if (B_KC) {
+            if ((t & 1) == 0 && t + 2 < nk) stage_b(t + 2);
+            if ((t & 1) == 0 && t + 3 < nk) stage_b(t + 3);
+          } else if (t + 3 < nk) {
+            stage_b(t + 3);
+          }
+        }
+        if (t + 4 < nk) {
+          if (t & 1) wait_vm<ODD_INFLIGHT>();
+          else wait_vm<2 * C::G>();
+        } else {
+          wait_vm<0>();
+        }
+      } else {
+        if (VAR != 2 && t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
+        wait_newer<C::G, NS - 2>(min(nk - 1, t + NS - 1) - (t + 1));  // step t+1 landed
+      }
       i16x8_t af[C::TM], bfr[C::TN];
-      read_frags(t % kNS, af, bfr);
+      if constexpr (VAR == 3) {  // perf probe: no fragment reads
+#pragma unroll
+        for (int i = 0; i < C::TM; ++i) af[i] = i16x8_t{(short)i, 1, 2, 3, 4, 5, 6, (short)t};
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j) bfr[j] = i16x8_t{(short)j, 1, 2, 3, 4, 5, 6, (short)t};
+      } else {
+        read_frags(t % NS, af, bfr);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier();
-      mfma_step(af, bfr);
+      if constexpr (VAR != 1) mfma_step(af, bfr);
+      else {  // perf probe: no MFMAs (keep the fragments live)
+#pragma unroll
+        for (int i = 0; i < C::TM; ++i) acc[i][0][0] += static_cast<float>(af[i][0] + bfr[i % C::TN][1]);
+      }
       barrier();
     }
     if (grp == 0) barrier();
-    if constexpr (VAR == 1) __builtin_amdgcn_s_setprio(0);
   } else
   for (int t = 0; t < nk; ++t) {
     // slot t landed: everything newer than step t (at most NS-2 steps) may stay in flight
-    const int newer = nk - 1 - t;
-    if (newer >= 2) wait_vm<2 * C::G>();
-    else if (newer == 1) wait_vm<C::G>();
-    else wait_vm<0>();
+    wait_newer<C::G, NS - 2>(min(nk - 1, t + NS - 2) - t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    if (t + kNS - 1 < nk) stage(t + kNS - 1, (t + kNS - 1) % kNS);
+    if (t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
     i16x8_t af[C::TM], bfr[C::TN];
-    read_frags(t % kNS, af, bfr);
+    read_frags(t % NS, af, bfr);
     mfma_step(af, bfr);
   }
 
@@ -394,15 +460,18 @@ template <typename OutT, typename AuxT>
 hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   auto tiles = [&](int bm, int bn) { return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
   constexpr int kFill = 240;  // ~ CU count: a config below this leaves CUs idle
-  static const int forced = [] {  // experiments: PZ_GEMM_TILE=1 (256x256x4 waves) 2 (256x256x8) 3 (256x128) 4 (128x128)
+  static const int forced = [] {  // experiments: PZ_GEMM_TILE=1 (256x256) 2 (256x128) 3 (128x128)
     const char* e = getenv("PZ_GEMM_TILE");
     return e ? atoi(e) : 0;
   }();
   switch (forced) {
-    case 1: return launch_layout<256, 256, 2, 4, OutT, AuxT, 1>(p, s);
-    case 2: return launch_layout<256, 256, 2, 4, OutT, AuxT, 2>(p, s);
-    case 3: return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
-    case 4: return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
+    case 11: return launch_layout<256, 256, 2, 4, OutT, AuxT, 1>(p, s);
+    case 12: return launch_layout<256, 256, 2, 4, OutT, AuxT, 2>(p, s);
+    case 13: return launch_layout<256, 256, 2, 4, OutT, AuxT, 3>(p, s);
+    case 14: return launch_layout<256, 256, 2, 4, OutT, AuxT, 4>(p, s);
+    case 1: return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
+    case 2: return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
+    case 3: return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
     default: break;
   }
   if (tiles(256, 256) >= kFill) return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
@@ -426,6 +495,11 @@ bool mfma_eligible(const GemmArgs& p) {
   if (p.out_dtype == DT_F32 && p.epi_mode != EPI_STORE) return false;
   if (p.out_dtype == DT_BF16 && p.accumulate) return false;
   if (p.bias != nullptr && !al16(p.bias)) return false;
+  if (p.mask != nullptr) {
+    if (p.out_dtype != DT_BF16 || p.ldmask % 8 != 0 || (reinterpret_cast<uintptr_t>(p.mask) & 7) != 0) return false;
+    if (p.epi_mode == EPI_BWD ? p.epi.act != ACT_RELU : p.epi_mode != EPI_FWD) return false;
+    return true;
+  }
   if (p.epi_mode == EPI_BWD) {
     if (p.aux == nullptr || p.ldaux % 8 != 0 || !al16(p.aux)) return false;
     if (p.aux_dtype != DT_BF16) return false;

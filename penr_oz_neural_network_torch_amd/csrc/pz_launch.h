@@ -40,6 +40,11 @@ struct GemmArgs {
   EpiSpec epi;
   int64_t idx_ld;     // logical row stride used for dropout element indices (usually N)
   int force_generic;  // testing: bypass the MFMA path
+  // ReLU bitmask [M][ldmask bytes], bit (n & 7) of byte n / 8 = (y[m][n] > 0). EPI_FWD writes it
+  // (from the final stage output); EPI_BWD with act == RELU reads it INSTEAD of aux: 1/16 of
+  // the bytes of re-reading the stored bf16 activation. MFMA path only.
+  uint8_t* mask;
+  int64_t ldmask;
 };
 
 // returns hipSuccess or an error; chooses the MFMA path when the shape allows

@@ -255,10 +255,29 @@ class FusedTrainer:
                 st.buffers["bn_in_grad"] = torch.empty(rows_b * st.pos_in, st.in_width, device=dev, dtype=cd)
         if pos != 1:
             raise UnsupportedModel(f"head input still has {pos} positions per sample")
+        self._plan_relu_masks(rows_b)
         # record-mode scratch: one buffer per layer output / grad, allocated lazily
 
     # ------------------------------------------------------------------------------------
     # epilogue specs
+    def _plan_relu_masks(self, rows_b: int) -> None:
+        """ReLU GEMM stages feeding a GEMM stage keep a 1-bit mask of ``y > 0`` next to ``y``: the
+        next stage's dX GEMM reads it (8 B per 64 columns) instead of re-reading ``y`` (128 B)."""
+        for i, st in enumerate(self.stages):
+            st.buffers.pop("mask", None)
+            if st.kind != "gemm" or st.act != PF.ACT_RELU or i + 1 >= len(self.stages):
+                continue
+            nxt = self.stages[i + 1]
+            x = self.stages[i - 1].buffers["y"] if i > 0 else self.x_in
+            if nxt.kind != "gemm" or x.dtype != torch.bfloat16:
+                continue
+            if PF.gemm_path(x, True, self._w(st), False, st.buffers["y"]) != "mfma":
+                continue
+            if PF.gemm_path(nxt.buffers["g"], True, self._w(nxt), True, st.buffers["g"]) != "mfma":
+                continue
+            st.buffers["mask"] = torch.empty(rows_b * st.pos_out, PF.relu_mask_cols(st.out_width),
+                                             device=self.dev, dtype=torch.uint8)
+
     # ------------------------------------------------------------------------------------
     def _seed(self, epoch: int) -> tuple[int, int]:
         lo = (self.base_seed[0] ^ (epoch * 0x9E3779B1)) & 0xFFFFFFFF
@@ -369,7 +388,8 @@ class FusedTrainer:
             ei, ef = self._epi(st, p, seed)
             if st.kind == "gemm":
                 bias = self.store.view(st.seg_b) if st.seg_b is not None else None
-                PF.gemm(x, True, self._w(st), False, y, bias=bias, mode=PF.EPI_FWD, epi=(ei, ef))
+                PF.gemm(x, True, self._w(st), False, y, bias=bias, mode=PF.EPI_FWD, epi=(ei, ef),
+                        mask=st.buffers.get("mask"))
             else:
                 self._bn_fwd(st, x, y, batch, ei, ef)
             return y
@@ -479,8 +499,9 @@ class FusedTrainer:
             ei, ef = self._epi(before, p, seed)
             colsum = self.store.view(before.seg_b, self.grads) if (before.kind == "gemm" and before.seg_b is not None) \
                 else None
-            PF.gemm(g, True, self._w(st), True, dx, aux=before.buffers["y"], colsum=colsum, mode=PF.EPI_BWD,
-                    epi=(ei, ef))
+            mask = before.buffers.get("mask")
+            PF.gemm(g, True, self._w(st), True, dx, aux=None if mask is not None else before.buffers["y"],
+                    colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask)
             return dx, True
         no_epi_prev = before.kind in ("gemm",) and not before.has_epi and rec is None
         colsum = None

@@ -113,6 +113,36 @@ def test_gemm_backward_epilogue_and_colsum(native_lib, act):
     assert (out16.double() - ref).abs().max().item() < 0.03 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (8192 + 64, 1024 + 64, 256), (256, 4096, 64)])
+def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
+    """EPI_FWD writes bit(y > 0); EPI_BWD reading those bits == EPI_BWD reading y (bit-identical)."""
+    p, seed = 0.2, (5, 11)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, N, device=DEV) / 8).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    mask = torch.full((M, PF.relu_mask_cols(N)), 0xAB, device=DEV, dtype=torch.uint8)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=3, drop_post=4, p=p, seed=seed)
+    PF.gemm(x, True, w, False, y, bias=bias, mode=PF.EPI_FWD, epi=epi, mask=mask)
+    bits = torch.stack([(mask[:, :N // 8].int() >> b) & 1 for b in range(8)], dim=2).reshape(M, N)
+    assert torch.equal(bits.bool(), y.float() > 0)
+    # backward: dX = dZ @ Wᵀ with the ReLU derivative from the bits vs from y
+    gz = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    wt = torch.randn(N, K, device=DEV).to(torch.bfloat16)
+    out_aux = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    out_bit = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    cs_aux = torch.zeros(N, device=DEV)
+    cs_bit = torch.zeros(N, device=DEV)
+    PF.gemm(gz, True, wt, True, out_aux, aux=y, colsum=cs_aux, mode=PF.EPI_BWD, epi=epi)
+    PF.gemm(gz, True, wt, True, out_bit, colsum=cs_bit, mode=PF.EPI_BWD, epi=epi, mask=mask)
+    assert torch.equal(out_aux, out_bit)
+    torch.testing.assert_close(cs_aux, cs_bit, rtol=1e-5, atol=1e-3)
+    ref = (gz.double() @ wt.double().t()) * (y.double() > 0)
+    m1 = torch.from_numpy(keep_mask(M * N, *seed, 3, p).reshape(M, N)).to(DEV)
+    ref = ref * m1 / (1 - p) * (torch.from_numpy(keep_mask(M * N, *seed, 4, p).reshape(M, N)).to(DEV) / (1 - p))
+    assert (out_bit.double() - ref).abs().max().item() < 0.02 * ref.abs().max().item()
+
+
 def test_stage_kernels_match_torch(native_lib):
     x = torch.randn(1000, 33, device=DEV, dtype=torch.float64, requires_grad=True)
     for algo, fn in [("relu", torch.relu), ("sigmoid", torch.sigmoid), ("tanh", torch.tanh)]:
