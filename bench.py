@@ -32,6 +32,7 @@ REFERENCE_SAMPLES_PER_S = {  # BASELINE.md, reference on CPU fp64 (no published 
     "mlp4": 2064.0,
     "deep16x8192": 22.8,
     "mlp8192": 3095.0,
+    "mlp8192_bf16": 3095.0,
 }
 
 CONFIGS = {
@@ -39,9 +40,13 @@ CONFIGS = {
                  optimizer="adam", name="mlp[1024,4096,4096,1024] relu,relu,softmax (25.2M params)"),
     "deep16x8192": dict(sizes=[8192] * 17, algos=["relu"] * 15 + ["softmax"], batch=8192, dtype="bfloat16",
                         optimizer="stochastic", name="mlp[8192]x17 (16 hidden 8192-wide, 1.07B params)"),
-    "mlp8192": dict(sizes=[1024, 8192, 1024], algos=["relu", "softmax"], batch=8192, dtype="bfloat16",
-                    optimizer="adam", name="mlp[1024,8192,1024] relu,softmax (16.8M params)"),
+    # BASELINE config 5: fp8 weights/activations on the e4m3 MFMA (forward GEMMs), bf16 backward
+    "mlp8192": dict(sizes=[1024, 8192, 1024], algos=["relu", "softmax"], batch=8192, dtype="fp8",
+                    optimizer="adam", name="mlp[1024,8192,1024] relu,softmax (16.8M params), fp8 e4m3 fwd GEMMs"),
+    "mlp8192_bf16": dict(sizes=[1024, 8192, 1024], algos=["relu", "softmax"], batch=8192, dtype="bfloat16",
+                         optimizer="adam", name="mlp[1024,8192,1024] relu,softmax (16.8M params)"),
 }
+DTYPE_LABEL = {"bfloat16": "bf16", "fp8": "fp8", "float32": "fp32"}
 
 
 def log(msg: str) -> None:
@@ -128,7 +133,7 @@ def main(argv=None) -> int:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / ref, 2) if ref else None,
-            "dtype": "bf16",
+            "dtype": DTYPE_LABEL[cfg["dtype"]],
             "data": "synthetic (random inputs/labels, random-init weights)",
             "config": {"model": cfg["name"], "global_batch": global_batch, "per_gpu_batch": batch,
                        "seq_len": None, "parallelism": f"dp{world}", "optimizer": cfg["optimizer"],

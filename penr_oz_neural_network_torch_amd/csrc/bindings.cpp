@@ -73,6 +73,7 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
                        int64_t epi_mode, at::IntArrayRef epi_i, at::ArrayRef<double> epi_f, double alpha,
                        bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld, bool force_generic,
                        const optional<Tensor>& mask = c10::nullopt) {
+  // (fp8 extras are attached by gemm_fp8_extras below)
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "pz::gemm: 2-D operands expected");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "pz::gemm: unit inner stride expected");
   TORCH_CHECK(A.scalar_type() == B.scalar_type(), "pz::gemm: A/B dtype mismatch");
@@ -123,13 +124,38 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   return p;
 }
 
+const float* f32_scalar_ptr(const optional<Tensor>& t, const char* what) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= 1, "pz::gemm: ", what, " must be an fp32 device scalar");
+  return t->data_ptr<float>();
+}
+
 void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, const optional<Tensor>& bias,
              const optional<Tensor>& aux, const optional<Tensor>& colsum, int64_t epi_mode, at::IntArrayRef epi_i,
              at::ArrayRef<double> epi_f, double alpha, bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld,
-             bool force_generic, const optional<Tensor>& mask) {
+             bool force_generic, const optional<Tensor>& mask, const optional<Tensor>& scale_a,
+             const optional<Tensor>& scale_b, const optional<Tensor>& out8, const optional<Tensor>& out8_qscale,
+             const optional<Tensor>& amax) {
   check_dev(A, "A");
   auto p = gemm_args(A, a_kc, B, b_kc, C, bias, aux, colsum, epi_mode, epi_i, epi_f, alpha, accumulate, M, N, K, idx_ld,
                      force_generic, mask);
+  p.scale_a = f32_scalar_ptr(scale_a, "scale_a");
+  p.scale_b = f32_scalar_ptr(scale_b, "scale_b");
+  if (out8.has_value() && out8->defined()) {
+    TORCH_CHECK(out8->scalar_type() == at::kFloat8_e4m3fn && out8->dim() == 2 && out8->stride(1) == 1 &&
+                    out8->size(0) >= M && out8->size(1) >= N,
+                "pz::gemm: out8 must be float8_e4m3fn [M, N]");
+    p.out8 = static_cast<uint8_t*>(out8->data_ptr());
+    p.ldout8 = out8->stride(0);
+    p.out8_qscale = f32_scalar_ptr(out8_qscale, "out8_qscale");
+    TORCH_CHECK(p.out8_qscale != nullptr, "pz::gemm: out8 needs out8_qscale");
+  }
+  if (amax.has_value() && amax->defined()) {
+    TORCH_CHECK(amax->scalar_type() == at::kFloat, "pz::gemm: amax must be fp32");
+    p.amax = amax->data_ptr<float>();
+  }
+  TORCH_CHECK((p.out8 == nullptr && p.in_dtype != pz::DT_FP8) || pz::gemm_path(p) == 1,
+              "pz::gemm: fp8 operands / outputs need an MFMA-eligible shape");
   TORCH_CHECK(p.mask == nullptr || pz::gemm_path(p) == 1, "pz::gemm: a mask epilogue needs an MFMA-eligible shape");
   PZ_HIP_CHECK(pz::gemm(p, cur_stream(A)));
 }
@@ -435,6 +461,44 @@ void embedding_bwd_op(const Tensor& dout, const Tensor& idx, const Tensor& dtabl
                                  dtable.data_ptr(), dt_of(dtable), cur_stream(dout)));
 }
 
+// ------------------------------------------------------------------------------------ fp8
+void amax_abs_op(const Tensor& x, const Tensor& amax) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.is_contiguous() && amax.scalar_type() == at::kFloat, "pz::amax_abs: contiguous x, fp32 amax");
+  PZ_HIP_CHECK(pz::amax_abs(x.data_ptr(), dt_of(x), x.numel(), amax.data_ptr<float>(), cur_stream(x)));
+}
+
+void scale_update_op(const Tensor& amax, const Tensor& qs, double headroom, bool reset) {
+  check_dev(amax, "amax");
+  TORCH_CHECK(amax.scalar_type() == at::kFloat && qs.scalar_type() == at::kFloat && qs.numel() >= 2 * amax.numel(),
+              "pz::scale_update: fp32 amax[n], qs[2n]");
+  PZ_HIP_CHECK(pz::scale_update(amax.data_ptr<float>(), qs.data_ptr<float>(), static_cast<int>(amax.numel()),
+                                static_cast<float>(headroom), reset, cur_stream(amax)));
+}
+
+void quant_transpose_op(const Tensor& w, const Tensor& out, const Tensor& qs) {
+  check_dev(w, "w");
+  TORCH_CHECK(w.scalar_type() == at::kFloat && w.dim() == 2 && w.stride(1) == 1, "pz::quant_transpose: fp32 [K,N] w");
+  TORCH_CHECK(out.scalar_type() == at::kFloat8_e4m3fn && out.dim() == 2 && out.stride(1) == 1 &&
+                  out.size(0) == w.size(1) && out.size(1) == w.size(0) && out.stride(0) % 4 == 0,
+              "pz::quant_transpose: out must be e4m3 [N,K]");
+  PZ_HIP_CHECK(pz::quant_transpose(w.data_ptr<float>(), w.stride(0), static_cast<int>(w.size(0)),
+                                   static_cast<int>(w.size(1)), static_cast<uint8_t*>(out.data_ptr()), out.stride(0),
+                                   qs.data_ptr<float>(), cur_stream(w)));
+}
+
+void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, const optional<Tensor>& amax) {
+  check_dev(x, "x");
+  TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && out.dim() == 2 && out.stride(1) == 1 &&
+                  out.scalar_type() == at::kFloat8_e4m3fn && out.size(0) >= x.size(0) && out.size(1) >= x.size(1) &&
+                  out.stride(0) % 4 == 0,
+              "pz::quantize_rows: x [rows, cols], out e4m3 [rows, cols]");
+  PZ_HIP_CHECK(pz::quantize_rows(x.data_ptr(), dt_of(x), x.stride(0), static_cast<int>(x.size(0)),
+                                 static_cast<int>(x.size(1)), static_cast<uint8_t*>(out.data_ptr()), out.stride(0),
+                                 qs.data_ptr<float>(), amax.has_value() ? amax->data_ptr<float>() : nullptr,
+                                 cur_stream(x)));
+}
+
 void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tensor& stats_prev, const Tensor& stats_cur,
                       const Tensor& slot_numel, int64_t nslots, double l2, const Tensor& costs, int64_t epoch,
                       const Tensor& ratios, int64_t ratio_row) {
@@ -471,7 +535,8 @@ std::string repr_double_op(double x) { return pz::repr_double(x); }
 TORCH_LIBRARY(pz, m) {
   m.def("gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor(a!) C, Tensor? bias, Tensor? aux, Tensor(b!)? colsum, "
         "int epi_mode, int[] epi_i, float[] epi_f, float alpha, bool accumulate, int M, int N, int K, int idx_ld, "
-        "bool force_generic, Tensor(c!)? mask=None) -> ()");
+        "bool force_generic, Tensor(c!)? mask=None, Tensor? scale_a=None, Tensor? scale_b=None, "
+        "Tensor(d!)? out8=None, Tensor? out8_qscale=None, Tensor(e!)? amax=None) -> ()");
   m.def("gemm_path(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor C, int M, int N, int K) -> int");
   m.def("stage_fwd(Tensor x, Tensor(a!) y, int[] epi_i, float[] epi_f) -> ()");
   m.def("stage_bwd(Tensor g, Tensor y, Tensor(a!) dx, int[] epi_i, float[] epi_f) -> ()");
@@ -502,6 +567,10 @@ TORCH_LIBRARY(pz, m) {
   m.def("embedding_bwd(Tensor dout, Tensor idx, Tensor(a!) dtable) -> ()");
   m.def("step_finalize(Tensor? loss, float loss_div, Tensor(a!) stats_prev, Tensor stats_cur, Tensor slot_numel, "
         "int nslots, float l2, Tensor(b!) costs, int epoch, Tensor(c!) ratios, int ratio_row) -> ()");
+  m.def("amax_abs(Tensor x, Tensor(a!) amax) -> ()");
+  m.def("scale_update(Tensor(a!) amax, Tensor(b!) qs, float headroom, bool reset) -> ()");
+  m.def("quant_transpose(Tensor w, Tensor(a!) out, Tensor qs) -> ()");
+  m.def("quantize_rows(Tensor x, Tensor(a!) out, Tensor qs, Tensor(b!)? amax) -> ()");
   m.def("format_json_array(Tensor t, int level) -> str");
   m.def("repr_double(float x) -> str");
 }
@@ -526,6 +595,10 @@ TORCH_LIBRARY_IMPL(pz, CUDA, m) {
   m.impl("embedding_fwd", TORCH_FN(embedding_fwd_op));
   m.impl("embedding_bwd", TORCH_FN(embedding_bwd_op));
   m.impl("step_finalize", TORCH_FN(step_finalize_op));
+  m.impl("amax_abs", TORCH_FN(amax_abs_op));
+  m.impl("scale_update", TORCH_FN(scale_update_op));
+  m.impl("quant_transpose", TORCH_FN(quant_transpose_op));
+  m.impl("quantize_rows", TORCH_FN(quantize_rows_op));
 }
 
 TORCH_LIBRARY_IMPL(pz, CPU, m) {

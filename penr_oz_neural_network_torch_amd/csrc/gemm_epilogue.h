@@ -9,8 +9,14 @@
 //   3. results go to the LDS image as bf16 and leave it as full 16-B-per-lane row segments;
 //   4. ReLU stages: the forward also writes a 1-bit-per-element mask of y > 0, and the backward
 //      reads 8 mask bytes per accumulator row instead of the 512-B aux row segment (dX GEMMs
-//      with K = 1024 spent a third of their time streaming the bf16 aux tile).
+//      with K = 1024 spent a third of their time streaming the bf16 aux tile);
+//   5. fp8 consumers: the forward can also emit an e4m3 copy of y (scaled by a device-side
+//      quantisation factor) and the tile's amax (delayed scaling for the next step).
 // Image layout: row r holds BN bf16; 16-B chunk c of row r lives at chunk c ^ (r & 15).
+//
+// The accumulator layout is abstracted by a fragment LAYOUT: every lane owns, per accumulator
+// ROW i, COLS groups of 4 consecutive output columns of ONE output row:
+//   m = wave_m0 + MSTEP*i + m_lane(lane),  n = wave_n0 + n_off(j) + n_lane(lane) + r  (r < 4).
 #pragma once
 
 template <int BN>
@@ -19,22 +25,48 @@ PZ_DEV uint32_t cimg_off(int r, int col) {  // byte offset of element (r, col), 
   return static_cast<uint32_t>(r * (BN * 2) + ((c ^ (r & 15)) << 4) + ((col & 4) << 1));
 }
 
-// The passes below work on ONE fragment row (the TN 4-element fragments of accumulator row i);
-// the epilogue walks the rows so only one row's temporaries are live at a time.
+// 16x16x32 bf16 MFMA issued as mfma(B, A): acc[TM][TN] f32x4, lane -> m = lane&15, n = 4*(lane>>4)
+template <int TM_, int TN_>
+struct Lay16 {
+  static constexpr int ROWS = TM_, COLS = TN_, MSTEP = 16, RED = 16;
+  PZ_DEV static int m_lane(int lane) { return lane & 15; }
+  PZ_DEV static int n_lane(int lane) { return 4 * (lane >> 4); }
+  static constexpr int n_off(int j) { return 16 * j; }
+  template <class Acc>
+  PZ_DEV static f32x4_t get(const Acc& acc, int i, int j) { return acc[i][j]; }
+};
 
-// dropout: v[j][r] *= mask (scale or 0); pr0 = element-pair index of fragment (i, 0)
-template <int TN>
-PZ_DEV void dropout_row(f32x4_t (&v)[TN], const EpiSpec& e, uint32_t key, uint32_t pr0) {
+// 32x32x64 f8 MFMA issued as mfma(B, A): acc[TM][TN] f32x16, lane -> m = lane&31,
+// n = 8*(reg>>2) + 4*(lane>>5) + (reg&3): column group j = (block j>>2, register quad j&3)
+template <int TM_, int TN_>
+struct Lay32 {
+  static constexpr int ROWS = TM_, COLS = 4 * TN_, MSTEP = 32, RED = 32;
+  PZ_DEV static int m_lane(int lane) { return lane & 31; }
+  PZ_DEV static int n_lane(int lane) { return 4 * (lane >> 5); }
+  static constexpr int n_off(int j) { return 32 * (j >> 2) + 8 * (j & 3); }
+  template <class Acc>
+  PZ_DEV static f32x4_t get(const Acc& acc, int i, int j) {
+    const int q = 4 * (j & 3);
+    return f32x4_t{acc[i][j >> 2][q], acc[i][j >> 2][q + 1], acc[i][j >> 2][q + 2], acc[i][j >> 2][q + 3]};
+  }
+};
+
+// The passes below work on ONE accumulator row (its COLS 4-element groups); the epilogue walks
+// the rows so only one row's temporaries are live at a time.
+
+// dropout: v[j][r] *= mask (scale or 0); pr_row = element-pair index of column group 0
+template <class L>
+PZ_DEV void dropout_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, uint32_t key, uint32_t pr_row) {
   if (e.drop_all) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) v[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < L::COLS; ++j) v[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
     return;
   }
   const uint32_t th = e.thresh16;
   const float sc = e.scale;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const uint32_t pr = pr0 + static_cast<uint32_t>(j) * 8u;
+  for (int j = 0; j < L::COLS; ++j) {
+    const uint32_t pr = pr_row + static_cast<uint32_t>(L::n_off(j) / 2);
     const uint32_t b0 = mix32(pr ^ key), b1 = mix32((pr + 1u) ^ key);
     v[j][0] *= (b0 & 0xFFFFu) >= th ? sc : 0.f;
     v[j][1] *= (b0 >> 16) >= th ? sc : 0.f;
@@ -43,10 +75,10 @@ PZ_DEV void dropout_row(f32x4_t (&v)[TN], const EpiSpec& e, uint32_t key, uint32
   }
 }
 
-template <int TN>
-PZ_DEV void act_fwd_row(f32x4_t (&v)[TN], int act) {
+template <int COLS>
+PZ_DEV void act_fwd_row(f32x4_t (&v)[COLS], int act) {
 #define PZ_ACT_LOOP(expr)                                                       \
-  _Pragma("unroll") for (int j = 0; j < TN; ++j) _Pragma("unroll") for (int r = 0; r < 4; ++r) { \
+  _Pragma("unroll") for (int j = 0; j < COLS; ++j) _Pragma("unroll") for (int r = 0; r < 4; ++r) { \
     const float x = v[j][r]; v[j][r] = (expr); }
   // branch-free fast forms (the result is rounded to bf16): sigmoid = 1/(1+e^-x),
   // tanh = 1 - 2/(e^{2x}+1) (saturates correctly for |x| large, e^{2x} -> inf or 0)
@@ -56,14 +88,15 @@ PZ_DEV void act_fwd_row(f32x4_t (&v)[TN], int act) {
 #undef PZ_ACT_LOOP
 }
 
-// v *= act'(a) with a = y * yscale; y (stored stage output) read per fragment from the LDS image
-template <int BN, int TN>
-PZ_DEV void act_bwd_row(f32x4_t (&v)[TN], const PZ_LDS char* img, int ml, int nl0, int act, float yscale) {
-#define PZ_ACTB_LOOP(expr)                                                                           \
-  _Pragma("unroll") for (int j = 0; j < TN; ++j) {                                                   \
-    const u32x2_t y = *reinterpret_cast<const PZ_LDS u32x2_t*>(img + cimg_off<BN>(ml, nl0 + 16 * j)); \
-    const float ys[4] = {bf2f(y[0] & 0xFFFF), bf2f(y[0] >> 16), bf2f(y[1] & 0xFFFF), bf2f(y[1] >> 16)};  \
-    _Pragma("unroll") for (int r = 0; r < 4; ++r) { const float a = ys[r] * yscale; v[j][r] *= (expr); } \
+// v *= act'(a) with a = y * yscale; y (stored stage output) read per group from the LDS image;
+// ml = tile row, nl = tile column of group 0
+template <int BN, class L>
+PZ_DEV void act_bwd_row(f32x4_t (&v)[L::COLS], const PZ_LDS char* img, int ml, int nl, int act, float yscale) {
+#define PZ_ACTB_LOOP(expr)                                                                                 \
+  _Pragma("unroll") for (int j = 0; j < L::COLS; ++j) {                                                    \
+    const u32x2_t y = *reinterpret_cast<const PZ_LDS u32x2_t*>(img + cimg_off<BN>(ml, nl + L::n_off(j)));  \
+    const float ys[4] = {bf2f(y[0] & 0xFFFF), bf2f(y[0] >> 16), bf2f(y[1] & 0xFFFF), bf2f(y[1] >> 16)};     \
+    _Pragma("unroll") for (int r = 0; r < 4; ++r) { const float a = ys[r] * yscale; v[j][r] *= (expr); }    \
   }
   if (act == ACT_RELU) { PZ_ACTB_LOOP(a > 0.f ? 1.f : 0.f) }
   else if (act == ACT_SIGMOID) { PZ_ACTB_LOOP(a * (1.f - a)) }
@@ -71,49 +104,60 @@ PZ_DEV void act_bwd_row(f32x4_t (&v)[TN], const PZ_LDS char* img, int ml, int nl
 #undef PZ_ACTB_LOOP
 }
 
-// v *= relu'(.) from the stage's ReLU bitmask: `bits` = the 64 mask bits of the wave's 64 columns
-// of this row (bit c = column c of the wave tile); fragment j, element r sits at 16j + g4 + r
-template <int TN>
-PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[TN], u32x2_t bits, int g4) {
+// v *= relu'(.) from the stage's ReLU bitmask: `bits` = the 64 mask bits of the wave's 64
+// columns of this row; group j element r is bit n_off(j) + n_lane + r (never straddles a word)
+template <class L>
+PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], u32x2_t bits, int nlane) {
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const uint32_t w = bits[j >> 1] >> (16 * (j & 1) + g4);
+  for (int j = 0; j < L::COLS; ++j) {
+    const uint32_t w = bits[L::n_off(j) >> 5] >> ((L::n_off(j) & 31) + nlane);
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[j][r] = ((w >> r) & 1u) ? v[j][r] : 0.f;
   }
 }
 
-template <int BM, int BN, int WM, int WN>
-PZ_DEV void epilogue_lds(const GemmArgs& p, f32x4_t (&acc)[BM / WM / 16][BN / WN / 16], PZ_LDS char* smem, int m0,
-                         int n0, int wm, int wn, int lane) {
-  using C = Cfg<BM, BN, WM, WN>;
-  constexpr int TM = C::TM, TN = C::TN;
-  static_assert(BM * BN * 2 <= C::LDS_BYTES, "C tile must fit the ring's LDS");
+// 8 fp32 -> 8 e4m3 bytes (OCP, saturating at +-448)
+PZ_DEV u32x2_t to_e4m3x8(const float (&x)[8], float qs) {
+  u32x2_t out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = fminf(fmaxf(x[4 * h + q] * qs, -448.f), 448.f);
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w, true);
+    out[h] = static_cast<uint32_t>(w);
+  }
+  return out;
+}
+
+template <int BM, int BN, int WM, int WN, class L, bool FWD_ONLY = false, class Acc>
+PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0, int n0, int wm, int wn, int lane,
+                         float alpha) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int ROWS = L::ROWS, COLS = L::COLS;
   constexpr int CHUNKS_PER_ROW = BN / 8;
-  constexpr int ROWS_PER_PASS = C::NT / CHUNKS_PER_ROW;
+  constexpr int ROWS_PER_PASS = NT / CHUNKS_PER_ROW;
   constexpr int PASSES = BM / ROWS_PER_PASS;
+  static_assert(WTN == 64, "the ReLU bitmask epilogue assumes 64-column wave tiles");
   const int tid = threadIdx.x;
   const int my_row = tid / CHUNKS_PER_ROW, my_chunk = tid % CHUNKS_PER_ROW;
-  const bool bwd = p.epi_mode == EPI_BWD;
+  const bool bwd = !FWD_ONLY && p.epi_mode == EPI_BWD;  // FWD_ONLY: no colsum / backward code
   const EpiSpec& e = p.epi;
-  const int g4 = 4 * (lane >> 4);
-  const int ml0 = wm * C::WTM + (lane & 15);  // + i*16
-  const int nl0 = wn * C::WTN + g4;           // + j*16
-  // element index of fragment (i, j) = (m0+ml0+16i) * idx_ld + n0+nl0+16j; pairs = idx / 2
-  const uint32_t pair0 =
-      static_cast<uint32_t>((static_cast<uint64_t>(m0 + ml0) * static_cast<uint64_t>(p.idx_ld) + n0 + nl0) >> 1);
-  const uint32_t row_pairs = static_cast<uint32_t>(p.idx_ld) * 8u;  // 16 rows down, in pairs
-  static_assert(C::WTN == 64, "the ReLU bitmask epilogue assumes 64-column wave tiles");
+  const int ml0 = wm * WTM + L::m_lane(lane);  // + MSTEP*i
+  const int nlane = L::n_lane(lane);
+  const int nl0 = wn * WTN + nlane;            // + n_off(j)
   const bool use_mask = p.mask != nullptr;
 
   // ReLU bitmask (EPI_BWD): 8 bytes per accumulator row, issued before the barrier so the
   // loads fly while the slower waves finish their last MFMAs
-  u32x2_t mbits[TM];
+  u32x2_t mbits[ROWS];
   if (bwd && use_mask) {
-    const uint8_t* mrow = p.mask + (n0 + wn * C::WTN) / 8;
+    const uint8_t* mrow = p.mask + (n0 + wn * WTN) / 8;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + ml0 + 16 * i;
+    for (int i = 0; i < ROWS; ++i) {
+      const int m = m0 + ml0 + L::MSTEP * i;
       mbits[i] = m < p.M ? *reinterpret_cast<const u32x2_t*>(mrow + static_cast<int64_t>(m) * p.ldmask)
                          : u32x2_t{0u, 0u};
     }
@@ -138,59 +182,65 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, f32x4_t (&acc)[BM / WM / 16][BN / WN
 
   // ---- the stage math: per accumulator row, one pass per enabled transform, then bf16 into the
   // LDS image. Each lane only rewrites the cells whose y it read itself (no barrier needed).
-  f32x4_t bias4[TN];
+  f32x4_t bias4[COLS];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + nl0 + 16 * j;
+  for (int j = 0; j < COLS; ++j) {
+    const int n = n0 + nl0 + L::n_off(j);
     bias4[j] = (!bwd && p.bias != nullptr && n < p.N) ? *reinterpret_cast<const f32x4_t*>(p.bias + n)
                                                        : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
-  static_for<TM>([&](auto ic) {
-    constexpr int i = decltype(ic)::value;
-    f32x4_t (&v)[TN] = acc[i];
-    const uint32_t pr0 = pair0 + static_cast<uint32_t>(i) * row_pairs;
-    const int ml = ml0 + 16 * i;
+  f32x4_t cs[COLS];
 #pragma unroll
-    for (int j = 0; j < TN; ++j) v[j] = v[j] * p.alpha + bias4[j];
+  for (int j = 0; j < COLS; ++j) cs[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const uint64_t col0 = static_cast<uint64_t>(n0 + nl0);
+  static_for<ROWS>([&](auto ic) {
+    constexpr int i = decltype(ic)::value;
+    const int ml = ml0 + L::MSTEP * i;
+    const uint32_t pr_row =
+        static_cast<uint32_t>((static_cast<uint64_t>(m0 + ml) * static_cast<uint64_t>(p.idx_ld) + col0) >> 1);
+    f32x4_t v[COLS];
+#pragma unroll
+    for (int j = 0; j < COLS; ++j) v[j] = L::get(acc, i, j) * alpha + bias4[j];
     if (!bwd) {
       if (p.epi_mode == EPI_FWD) {
-        if (e.drop_pre) dropout_row(v, e, e.key_pre, pr0);
-        if (e.act != ACT_NONE) act_fwd_row(v, e.act);
-        if (e.drop_post) dropout_row(v, e, e.key_post, pr0);
+        if (e.drop_pre) dropout_row<L>(v, e, e.key_pre, pr_row);
+        if (e.act != ACT_NONE) act_fwd_row<COLS>(v, e.act);
+        if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
       }
     } else {
-      if (e.drop_post) dropout_row(v, e, e.key_post, pr0);
-      if (use_mask) act_bwd_mask_row(v, mbits[i], g4);
-      else if (e.act != ACT_NONE) act_bwd_row<BN>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
-      if (e.drop_pre) dropout_row(v, e, e.key_pre, pr0);
+      if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
+      if (use_mask) act_bwd_mask_row<L>(v, mbits[i], nlane);
+      else if (e.act != ACT_NONE) act_bwd_row<BN, L>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
+      if (e.drop_pre) dropout_row<L>(v, e, e.key_pre, pr_row);
     }
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
-      *reinterpret_cast<PZ_LDS u32x2_t*>(smem + cimg_off<BN>(ml, nl0 + 16 * j)) =
+    for (int j = 0; j < COLS; ++j)
+      *reinterpret_cast<PZ_LDS u32x2_t*>(smem + cimg_off<BN>(ml, nl0 + L::n_off(j))) =
           u32x2_t{pack_bf2(v[j][0], v[j][1]), pack_bf2(v[j][2], v[j][3])};
+    if (!FWD_ONLY && p.colsum != nullptr && m0 + ml < p.M) {
+#pragma unroll
+      for (int j = 0; j < COLS; ++j) cs[j] += v[j];
+    }
     __builtin_amdgcn_sched_barrier(0);  // keep rows apart: bounds the live temporaries
   });
-  if (p.colsum != nullptr) {
+  if (!FWD_ONLY && p.colsum != nullptr) {
 #pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-        if (m0 + ml0 + 16 * i < p.M) cs += acc[i][j];
-      const int n = n0 + nl0 + 16 * j;
+    for (int j = 0; j < COLS; ++j) {
+      const int n = n0 + nl0 + L::n_off(j);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = cs[r];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
-        if ((lane & 15) == 0 && n + r < p.N) atomicAdd(p.colsum + n + r, s);
+        float s = cs[j][r];
+#pragma unroll
+        for (int o = 1; o < L::RED; o <<= 1) s += __shfl_xor(s, o, 64);
+        if ((lane & (L::RED - 1)) == 0 && n + r < p.N) atomicAdd(p.colsum + n + r, s);
       }
     }
   }
   __syncthreads();
   uint16_t* __restrict__ Cp = static_cast<uint16_t*>(p.C);
+  const bool want8 = !bwd && p.out8 != nullptr;
+  const float qs = want8 ? *p.out8_qscale : 1.f;
+  float amax = 0.f;
 #pragma unroll
   for (int s = 0; s < PASSES; ++s) {
     const int r = s * ROWS_PER_PASS + my_row;
@@ -208,6 +258,20 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, f32x4_t (&acc)[BM / WM / 16][BN / WN
         }
         p.mask[static_cast<int64_t>(gm) * p.ldmask + gn / 8] = static_cast<uint8_t>(byte);
       }
+      if (want8) {  // e4m3 copy of the bf16 values + running |y| max
+        float x[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          x[2 * q] = bf2f(v[q] & 0xFFFFu);
+          x[2 * q + 1] = bf2f(v[q] >> 16);
+          amax = fmaxf(amax, fmaxf(fabsf(x[2 * q]), fabsf(x[2 * q + 1])));
+        }
+        *reinterpret_cast<u32x2_t*>(p.out8 + static_cast<int64_t>(gm) * p.ldout8 + gn) = to_e4m3x8(x, qs);
+      }
     }
+  }
+  if (want8 && p.amax != nullptr) {
+    amax = wave_max(amax);
+    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(amax));
   }
 }

@@ -141,7 +141,8 @@ int gemm_path(const GemmArgs& p) { return mfma_eligible(p) ? 1 : 0; }
 
 hipError_t gemm(const GemmArgs& p, hipStream_t s) {
   if (mfma_eligible(p)) return gemm_mfma(p, s);
-  if (p.mask != nullptr) return hipErrorInvalidValue;  // bitmask epilogues exist on the MFMA path only
+  // bitmask / e4m3 epilogues and e4m3 operands exist on the MFMA path only
+  if (p.mask != nullptr || p.out8 != nullptr || p.in_dtype == DT_FP8) return hipErrorInvalidValue;
   return gemm_generic(p, s);
 }
 

@@ -42,12 +42,12 @@ PZ_DEV int swz_kc(int row) { return (120 >> (2 * ((row >> 2) & 3))) & 3; }
 // M/N-contiguous slot [32][R]: chunk XOR so a half-wave's transposed reads hit 16 distinct slots
 PZ_DEV int swz_mn(int krow) { return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1; }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NS_ = 4>
 struct Cfg {
   // ring depth in 32-deep K slots. Measured on the step's GEMMs: 5 slots for 256x256 (160 KiB)
   // and 6 for 256x128 are 2-4% SLOWER than 4 (the DMA stream is throughput-, not latency-bound),
   // and 5 slots for 128x128 drop it to one workgroup per CU (-20%).
-  static constexpr int NS = 4;
+  static constexpr int NS = NS_;
   static constexpr int NW = WM * WN;
   static constexpr int NT = NW * 64;
   static constexpr int WTM = BM / WM;
@@ -83,14 +83,40 @@ PZ_DEV void glds16(const void* gsrc, uint32_t lds) {
       : "memory");
 }
 
+// Same DMA through the buffer (MUBUF) path: `rs` = raw buffer resource of the operand, `voff`
+// = per-lane byte offset. Out-of-range offsets (>= num_records) read zeros.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+PZ_DEV void blds16(i32x4_t rs, uint32_t voff, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(rs), "s"(lds)
+      : "memory");
+}
+
+PZ_DEV i32x4_t buf_rsrc(const void* base) {
+  const uint64_t b = reinterpret_cast<uint64_t>(base);
+  i32x4_t r;
+  r[0] = static_cast<int>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b)));
+  r[1] = static_cast<int>(__builtin_amdgcn_readfirstlane(static_cast<uint32_t>(b >> 32)));
+  r[2] = -1;           // num_records: whole 4 GiB window
+  r[3] = 0x00020000;   // gfx9 raw buffer
+  return r;
+}
+
 PZ_DEV uint32_t lds_addr(const PZ_LDS char* p) {
   return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
 }
 
 // K-contiguous operand rows [row0, row0+R) x k [k0, k0+32) -> slot [R][32]
-template <int R, int NW>
+template <int R, int NW, bool BUF = false>
 PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
-                     PZ_LDS char* tile, int wave, int lane) {
+                     PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
   constexpr int INSTR = R / (16 * NW);  // 16 rows of 64 B per 1-KiB instruction
 #pragma unroll
   for (int i = 0; i < INSTR; ++i) {
@@ -99,15 +125,19 @@ PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int r
     const int chunk = (lane & 3) ^ swz_kc(r);
     int gr = row0 + r;
     gr = gr < rows_valid ? gr : rows_valid - 1;
-    const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
-    glds16(src, lds_addr(tile + rbase * 64));
+    if constexpr (BUF) {
+      blds16(rs, static_cast<uint32_t>((static_cast<int64_t>(gr) * ld + k0 + chunk * 8) * 2), lds_addr(tile + rbase * 64));
+    } else {
+      const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
+      glds16(src, lds_addr(tile + rbase * 64));
+    }
   }
 }
 
 // M/N-contiguous operand: k rows [k0, k0+32) x cols [col0, col0+R) -> slot [32][R]
-template <int R, int NW>
+template <int R, int NW, bool BUF = false>
 PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int cols_valid, int k0,
-                     PZ_LDS char* tile, int wave, int lane) {
+                     PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
   constexpr int ROW_BYTES = R * 2;
   constexpr int CHUNKS = R / 8;
   constexpr int ROWS_PER = 1024 / ROW_BYTES;
@@ -119,14 +149,24 @@ PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int c
     const int chunk = (lane % CHUNKS) ^ swz_mn(kr);
     int gc = col0 + chunk * 8;
     gc = gc < cols_valid ? gc : cols_valid - 8;
-    const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
-    glds16(src, lds_addr(tile + kbase * ROW_BYTES));
+    if constexpr (BUF) {
+      blds16(rs, static_cast<uint32_t>((static_cast<int64_t>(k0 + kr) * ld + gc) * 2), lds_addr(tile + kbase * ROW_BYTES));
+    } else {
+      const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
+      glds16(src, lds_addr(tile + kbase * ROW_BYTES));
+    }
   }
 }
 
 PZ_DEV i16x8_t frag_kc(const PZ_LDS char* tile, int row, int chunk) {
   const int slot = chunk ^ swz_kc(row);
   return *reinterpret_cast<const PZ_LDS i16x8_t*>(tile + row * 64 + slot * 16);
+}
+
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+PZ_DEV i32x8_t cat_frag(i16x8_t lo, i16x8_t hi) {
+  const i32x4_t a = __builtin_bit_cast(i32x4_t, lo), b = __builtin_bit_cast(i32x4_t, hi);
+  return i32x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
 }
 
 template <int R>
@@ -231,7 +271,7 @@ PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
-  using C = Cfg<BM, BN, WM, WN>;
+  using C = Cfg<BM, BN, WM, WN, VAR == 5 ? 3 : 4>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
 
@@ -247,43 +287,72 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
   const uint16_t* __restrict__ B = static_cast<const uint16_t*>(p.B);
 
-  f32x4_t acc[C::TM][C::TN];
+  // VAR 8: e4m3 operands (both K-contiguous), v_mfma_scale_f32_32x32x64_f8f6f4 with unit block
+  // scales: a ring slot holds 64 K-bytes per row (the bf16 slot geometry), one MFMA K-step
+  constexpr bool F8 = VAR == 8;
+  static_assert(!F8 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "fp8: K-contiguous in, bf16 out");
+  constexpr int TM8 = C::WTM / 32, TN8 = C::WTN / 32;
+  struct Frags16 { i16x8_t a[C::TM]; i16x8_t b[C::TN]; };
+  struct Frags8 { i32x8_t a[TM8]; i32x8_t b[TN8]; };
+  using Frags = std::conditional_t<F8, Frags8, Frags16>;
+  using AccT = std::conditional_t<F8, f32x16_t[TM8][TN8], f32x4_t[C::TM][C::TN]>;
+  AccT acc;
+  if constexpr (F8) {
 #pragma unroll
-  for (int i = 0; i < C::TM; ++i)
+    for (int i = 0; i < TM8; ++i)
 #pragma unroll
-    for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-
-  auto stage = [&](int kt, int slot) {
-    PZ_LDS char* base = smem + slot * C::SLOT_BYTES;
-    const int k0 = kt * kBK;
-    if constexpr (A_KC) stage_kc<BM, C::NW>(A, p.lda, m0, p.M, k0, base, wave, lane);
-    else stage_mn<BM, C::NW>(A, p.lda, m0, p.M, k0, base, wave, lane);
-    if constexpr (B_KC) stage_kc<BN, C::NW>(B, p.ldb, n0, p.N, k0, base + C::A_BYTES, wave, lane);
-    else stage_mn<BN, C::NW>(B, p.ldb, n0, p.N, k0, base + C::A_BYTES, wave, lane);
-  };
-
-  auto mfma_step = [&](const i16x8_t (&af)[C::TM], const i16x8_t (&bfr)[C::TN]) {
-    __builtin_amdgcn_s_setprio(1);
+      for (int j = 0; j < TN8; ++j) acc[i][j] = f32x16_t{};
+  } else {
 #pragma unroll
     for (int i = 0; i < C::TM; ++i)
 #pragma unroll
-      for (int j = 0; j < C::TN; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, bfr[j]),
-                                                            __builtin_bit_cast(bf16x8_t, af[i]), acc[i][j], 0, 0, 0);
+      for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  }
+
+  auto mfma_step = [&](const Frags& f) {
+    __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
+#pragma unroll
+      for (int i = 0; i < TM8; ++i)
+#pragma unroll
+        for (int j = 0; j < TN8; ++j)  // cbsz/blgp 0 = e4m3; E8M0 block scales 127 = 1.0
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[j], f.a[i], acc[i][j], 0, 0, 0, 127, 0, 127);
+    } else {
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C::TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, f.b[j]),
+                                                              __builtin_bit_cast(bf16x8_t, f.a[i]), acc[i][j], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
-  auto read_frags = [&](int slot, i16x8_t (&af)[C::TM], i16x8_t (&bfr)[C::TN]) {
+  auto read_frags = [&](int slot, Frags& f) {
     const PZ_LDS char* ta = smem + slot * C::SLOT_BYTES;
     const PZ_LDS char* tb = ta + C::A_BYTES;
+    if constexpr (F8) {  // lane l: row l&31, K bytes [32*(l>>5), +32) = 16-B chunks 2h, 2h+1
+      const int h2 = 2 * (lane >> 5);
 #pragma unroll
-    for (int j = 0; j < C::TN; ++j) {
-      if constexpr (B_KC) bfr[j] = frag_kc(tb, wn * C::WTN + j * 16 + (lane & 15), lane >> 4);
-      else bfr[j] = frag_mn<BN>(tb, wn * C::WTN + j * 16, 8 * (lane >> 4), lane);
-    }
+      for (int j = 0; j < TN8; ++j) {
+        const int row = wn * C::WTN + j * 32 + (lane & 31);
+        f.b[j] = cat_frag(frag_kc(tb, row, h2), frag_kc(tb, row, h2 + 1));
+      }
 #pragma unroll
-    for (int i = 0; i < C::TM; ++i) {
-      if constexpr (A_KC) af[i] = frag_kc(ta, wm * C::WTM + i * 16 + (lane & 15), lane >> 4);
-      else af[i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, 8 * (lane >> 4), lane);
+      for (int i = 0; i < TM8; ++i) {
+        const int row = wm * C::WTM + i * 32 + (lane & 31);
+        f.a[i] = cat_frag(frag_kc(ta, row, h2), frag_kc(ta, row, h2 + 1));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < C::TN; ++j) {
+        if constexpr (B_KC) f.b[j] = frag_kc(tb, wn * C::WTN + j * 16 + (lane & 15), lane >> 4);
+        else f.b[j] = frag_mn<BN>(tb, wn * C::WTN + j * 16, 8 * (lane >> 4), lane);
+      }
+#pragma unroll
+      for (int i = 0; i < C::TM; ++i) {
+        if constexpr (A_KC) f.a[i] = frag_kc(ta, wm * C::WTM + i * 16 + (lane & 15), lane >> 4);
+        else f.a[i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, 8 * (lane >> 4), lane);
+      }
     }
   };
   auto barrier = [] {
@@ -292,18 +361,27 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  constexpr bool BUF = VAR == 6;
+  const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
+  // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
+  const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;
   auto stage_a = [&](int kt) {
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
-    if constexpr (A_KC) stage_kc<BM, C::NW>(A, p.lda, m0, p.M, kt * kBK, base, wave, lane);
-    else stage_mn<BM, C::NW>(A, p.lda, m0, p.M, kt * kBK, base, wave, lane);
+    if constexpr (A_KC) stage_kc<BM, C::NW, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
+    else stage_mn<BM, C::NW, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
   };
   auto stage_b = [&](int kt) {
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (B_KC) stage_kc<BN, C::NW>(B, p.ldb, n0, p.N, kt * kBK, base, wave, lane);
-    else stage_mn<BN, C::NW>(B, p.ldb, n0, p.N, kt * kBK, base, wave, lane);
+    if constexpr (B_KC) stage_kc<BN, C::NW, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
+    else stage_mn<BN, C::NW, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
+  };
+  auto stage = [&](int kt, int slot) {  // slot == kt % NS
+    (void)slot;
+    stage_a(kt);
+    stage_b(kt);
   };
 
-  const int nk = p.K / kBK;
+  const int nk = p.K / (F8 ? 2 * kBK : kBK);
   constexpr int NS = C::NS;
   // K-contiguous operands in the 8-wave schedule are staged in PAIRS of steps (t, t+1), the two
   // 64-B halves of every 128-B row line back to back: one L2 request per line instead of two.
@@ -365,21 +443,22 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
         if (VAR != 2 && t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
         wait_newer<C::G, NS - 2>(min(nk - 1, t + NS - 1) - (t + 1));  // step t+1 landed
       }
-      i16x8_t af[C::TM], bfr[C::TN];
+      Frags f;
       if constexpr (VAR == 3) {  // perf probe: no fragment reads
 #pragma unroll
-        for (int i = 0; i < C::TM; ++i) af[i] = i16x8_t{(short)i, 1, 2, 3, 4, 5, 6, (short)t};
+        for (int i = 0; i < C::TM; ++i) f.a[i] = i16x8_t{(short)i, 1, 2, 3, 4, 5, 6, (short)t};
 #pragma unroll
-        for (int j = 0; j < C::TN; ++j) bfr[j] = i16x8_t{(short)j, 1, 2, 3, 4, 5, 6, (short)t};
+        for (int j = 0; j < C::TN; ++j) f.b[j] = i16x8_t{(short)j, 1, 2, 3, 4, 5, 6, (short)t};
       } else {
-        read_frags(t % NS, af, bfr);
+        read_frags(t % NS, f);
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier();
-      if constexpr (VAR != 1) mfma_step(af, bfr);
-      else {  // perf probe: no MFMAs (keep the fragments live)
+      if constexpr (VAR != 1) {
+        mfma_step(f);
+      } else {  // perf probe: no MFMAs (keep the fragments live)
 #pragma unroll
-        for (int i = 0; i < C::TM; ++i) acc[i][0][0] += static_cast<float>(af[i][0] + bfr[i % C::TN][1]);
+        for (int i = 0; i < C::TM; ++i) acc[i][0][0] += static_cast<float>(f.a[i][0] + f.b[i % C::TN][1]);
       }
       barrier();
     }
@@ -391,9 +470,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
-    i16x8_t af[C::TM], bfr[C::TN];
-    read_frags(t % NS, af, bfr);
-    mfma_step(af, bfr);
+    Frags f;
+    read_frags(t % NS, f);
+    mfma_step(f);
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -402,8 +481,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   OutT* __restrict__ Cp = static_cast<OutT*>(p.C);
   const AuxT* __restrict__ aux = static_cast<const AuxT*>(p.aux);
   const int g4 = 4 * (lane >> 4);
-  if constexpr (std::is_same<OutT, uint16_t>::value) {
-    epilogue_lds<BM, BN, WM, WN>(p, acc, smem, m0, n0, wm, wn, lane);
+  if constexpr (F8) {
+    const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
+    epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+  } else if constexpr (std::is_same<OutT, uint16_t>::value) {
+    epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
   } else {
   static_for<C::TN>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
@@ -434,7 +516,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
-  using C = Cfg<BM, BN, WM, WN>;
+  using C = Cfg<BM, BN, WM, WN, VAR == 5 ? 3 : 4>;
   auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -469,6 +551,8 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     case 12: return launch_layout<256, 256, 2, 4, OutT, AuxT, 2>(p, s);
     case 13: return launch_layout<256, 256, 2, 4, OutT, AuxT, 3>(p, s);
     case 14: return launch_layout<256, 256, 2, 4, OutT, AuxT, 4>(p, s);
+    case 15: return launch_layout<256, 128, 4, 2, OutT, AuxT, 5>(p, s);
+    case 16: return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
     case 1: return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
     case 2: return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
     case 3: return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
@@ -479,9 +563,33 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
 }
 
+hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
+  const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  if (tiles >= 240) return launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
+  return launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
+}
+
 }  // namespace
 
+bool fp8_eligible(const GemmArgs& p) {
+  if (p.force_generic || p.in_dtype != DT_FP8 || p.out_dtype != DT_BF16) return false;
+  if (!p.a_kc || !p.b_kc || p.accumulate) return false;
+  if (p.M < 64 || p.N < 64 || p.K < 64 || p.K % 64 != 0) return false;
+  if (p.N % 8 != 0 || p.ldc % 8 != 0 || p.lda % 16 != 0 || p.ldb % 16 != 0) return false;
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al16(p.A) || !al16(p.B) || !al16(p.C)) return false;
+  if (p.idx_ld % 2 != 0) return false;
+  if (p.bias != nullptr && !al16(p.bias)) return false;
+  if (p.epi_mode == EPI_BWD) return false;  // fp8 is a forward-only operand format here
+  if (p.mask != nullptr && (p.ldmask % 8 != 0 || (reinterpret_cast<uintptr_t>(p.mask) & 7) != 0)) return false;
+  if (p.out8 != nullptr && (p.ldout8 % 8 != 0 || (reinterpret_cast<uintptr_t>(p.out8) & 7) != 0 ||
+                            p.out8_qscale == nullptr))
+    return false;
+  return true;
+}
+
 bool mfma_eligible(const GemmArgs& p) {
+  if (p.in_dtype == DT_FP8) return fp8_eligible(p);
   if (p.force_generic || p.in_dtype != DT_BF16) return false;
   if (p.out_dtype != DT_BF16 && p.out_dtype != DT_F32) return false;
   if (p.M < 64 || p.N < 64 || p.K < kBK || p.K % kBK != 0) return false;
@@ -495,6 +603,9 @@ bool mfma_eligible(const GemmArgs& p) {
   if (p.out_dtype == DT_F32 && p.epi_mode != EPI_STORE) return false;
   if (p.out_dtype == DT_BF16 && p.accumulate) return false;
   if (p.bias != nullptr && !al16(p.bias)) return false;
+  if (p.out8 != nullptr && (p.out_dtype != DT_BF16 || p.epi_mode == EPI_BWD || p.ldout8 % 8 != 0 ||
+                            (reinterpret_cast<uintptr_t>(p.out8) & 7) != 0 || p.out8_qscale == nullptr))
+    return false;
   if (p.mask != nullptr) {
     if (p.out_dtype != DT_BF16 || p.ldmask % 8 != 0 || (reinterpret_cast<uintptr_t>(p.mask) & 7) != 0) return false;
     if (p.epi_mode == EPI_BWD ? p.epi.act != ACT_RELU : p.epi_mode != EPI_FWD) return false;
@@ -508,6 +619,7 @@ bool mfma_eligible(const GemmArgs& p) {
 }
 
 hipError_t gemm_mfma(const GemmArgs& p, hipStream_t s) {
+  if (p.in_dtype == DT_FP8) return launch_fp8(p, s);
   if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);
   return launch_tiles<float, uint16_t>(p, s);
 }

@@ -173,4 +173,13 @@ hipError_t embedding_fwd(const void* table, int table_dtype, const void* idx, in
 hipError_t embedding_bwd(const void* dout, int dout_dtype, const void* idx, int idx_dtype, int64_t n_idx, int dim,
                          void* dtable, int dtable_dtype, hipStream_t s);
 
+// ------------------------------------------------------------------ fp8 quantisation
+// qs records are {q, s}: T8 = sat(T * q), T ~= T8 * s
+hipError_t amax_abs(const void* x, int dtype, int64_t n, float* amax, hipStream_t s);
+hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool reset, hipStream_t s);
+hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, const float* qs,
+                           hipStream_t s);
+hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
+                         const float* qs, float* amax, hipStream_t s);
+
 }  // namespace pz

@@ -45,6 +45,16 @@ struct GemmArgs {
   // the bytes of re-reading the stored bf16 activation. MFMA path only.
   uint8_t* mask;
   int64_t ldmask;
+  // fp8 (e4m3) operands: A/B hold e4m3 bytes; the products are dequantised by the device-side
+  // per-tensor factors *scale_a * *scale_b (nullptr = 1) on top of alpha
+  const float* scale_a;
+  const float* scale_b;
+  // EPI_FWD extra output: e4m3 copy of C, out8[m*ldout8 + n] = sat(C * *out8_qscale), and the
+  // running max |C| (atomicMax into *amax, which the caller zeroes) for delayed scaling
+  uint8_t* out8;
+  int64_t ldout8;
+  const float* out8_qscale;
+  float* amax;
 };
 
 // returns hipSuccess or an error; chooses the MFMA path when the shape allows

@@ -1,0 +1,148 @@
+// fp8 (OCP e4m3) quantisation kernels for the fp8 precision policy.
+//
+// Per-tensor scaling: a tensor T is stored as T8 = sat(T * q) with q = 448 / (amax * headroom)
+// and multiplied back by s = 1/q inside the GEMM epilogue. Weights use CURRENT scaling (their
+// amax is reduced right before the transpose-quantise that follows every optimizer step);
+// activations use DELAYED scaling: the producing GEMM epilogue records this step's amax and
+// scale_update() turns it into the (q, s) pair of the next step.
+//
+// Scale records are fp32 device arrays {q, s} so no host sync is ever needed.
+#include "pz_common.h"
+#include "pz_kernels.h"
+
+namespace pz {
+namespace {
+
+constexpr float kE4m3Max = 448.f;
+
+PZ_DEV uint8_t to_e4m3(float x) {
+  x = fminf(fmaxf(x, -kE4m3Max), kE4m3Max);
+  return static_cast<uint8_t>(__builtin_amdgcn_cvt_pk_fp8_f32(x, 0.f, 0, false) & 0xFF);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, int64_t n, float* amax) {
+  float m = 0.f;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < n; i += static_cast<int64_t>(gridDim.x) * 256)
+    m = fmaxf(m, fabsf(to_f(x[i])));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+}
+
+// amax -> {q, s}; optionally clears amax for the next accumulation window
+__global__ void scale_update_kernel(float* amax, float* qs, int n, float headroom, int reset) {
+  const int i = threadIdx.x + blockIdx.x * blockDim.x;
+  if (i >= n) return;
+  const float a = amax[i];
+  const float q = a > 0.f ? kE4m3Max / (a * headroom) : 1.f;
+  qs[2 * i] = q;
+  qs[2 * i + 1] = 1.f / q;
+  if (reset) amax[i] = 0.f;
+}
+
+// W [K][N] (fp32, row stride ldw) -> W8 [N][K] e4m3 (row stride ldo): 64x64 tiles through LDS;
+// the scale comes from the amax already reduced into qs[0] (q).
+__global__ void __launch_bounds__(256) quant_transpose_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
+                                                              uint8_t* __restrict__ out, int64_t ldo,
+                                                              const float* __restrict__ qs) {
+  __shared__ float tile[64][65];
+  const int k0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
+  const float q = qs[0];
+#pragma unroll
+  for (int r = ty; r < 64; r += 4) {
+    const int k = k0 + r, n = n0 + tx;
+    tile[r][tx] = (k < K && n < N) ? w[static_cast<int64_t>(k) * ldw + n] : 0.f;
+  }
+  __syncthreads();
+  // each thread writes 4 consecutive k of one output row n: 64 rows x 16 quads
+  const int n_local = threadIdx.x >> 2, kq = (threadIdx.x & 3) * 16;
+  const int n = n0 + n_local;
+  if (n >= N) return;
+#pragma unroll
+  for (int c = 0; c < 16; c += 4) {
+    const int k = k0 + kq + c;
+    if (k + 3 < K) {
+      uint32_t packed = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) packed |= static_cast<uint32_t>(to_e4m3(tile[kq + c + e][n_local] * q)) << (8 * e);
+      *reinterpret_cast<uint32_t*>(out + static_cast<int64_t>(n) * ldo + k) = packed;
+    } else {
+      for (int e = 0; e < 4 && k + e < K; ++e) out[static_cast<int64_t>(n) * ldo + k + e] = to_e4m3(tile[kq + c + e][n_local] * q);
+    }
+  }
+}
+
+// x [rows][cols] (bf16 or fp32, row stride ldx) -> x8 [rows][ldo] with quantisation factor qs[0]
+template <typename T>
+__global__ void __launch_bounds__(256) quantize_rows_kernel(const T* __restrict__ x, int64_t ldx, int rows, int cols,
+                                                            uint8_t* __restrict__ out, int64_t ldo,
+                                                            const float* __restrict__ qs, float* amax) {
+  const float q = qs[0];
+  float m = 0.f;
+  const int per_row = cols / 4;
+  const int64_t total = static_cast<int64_t>(rows) * per_row;
+  for (int64_t i = blockIdx.x * 256LL + threadIdx.x; i < total; i += static_cast<int64_t>(gridDim.x) * 256) {
+    const int r = static_cast<int>(i / per_row), c = static_cast<int>(i % per_row) * 4;
+    uint32_t packed = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float v = to_f(x[static_cast<int64_t>(r) * ldx + c + e]);
+      m = fmaxf(m, fabsf(v));
+      packed |= static_cast<uint32_t>(to_e4m3(v * q)) << (8 * e);
+    }
+    *reinterpret_cast<uint32_t*>(out + static_cast<int64_t>(r) * ldo + c) = packed;
+  }
+  if (amax != nullptr) {
+    m = wave_max(m);
+    if ((threadIdx.x & 63) == 0) atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+  }
+}
+
+int grid_for(int64_t work, int per_block = 256, int cap = 4096) {
+  const int64_t g = (work + per_block - 1) / per_block;
+  return static_cast<int>(g < 1 ? 1 : (g > cap ? cap : g));
+}
+
+}  // namespace
+
+hipError_t amax_abs(const void* x, int dtype, int64_t n, float* amax, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  const int g = grid_for(n);
+  if (dtype == DT_F32) hipLaunchKernelGGL(amax_kernel<float>, dim3(g), dim3(256), 0, s, static_cast<const float*>(x), n, amax);
+  else if (dtype == DT_BF16)
+    hipLaunchKernelGGL(amax_kernel<uint16_t>, dim3(g), dim3(256), 0, s, static_cast<const uint16_t*>(x), n, amax);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool reset, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scale_update_kernel, dim3((n + 63) / 64), dim3(64), 0, s, amax, qs, n, headroom, reset ? 1 : 0);
+  return hipGetLastError();
+}
+
+hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, const float* qs,
+                           hipStream_t s) {
+  if (K <= 0 || N <= 0) return hipSuccess;
+  hipLaunchKernelGGL(quant_transpose_kernel, dim3((N + 63) / 64, (K + 63) / 64), dim3(256), 0, s, w, ldw, K, N, out, ldo,
+                     qs);
+  return hipGetLastError();
+}
+
+hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
+                         const float* qs, float* amax, hipStream_t s) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (cols % 4 != 0) return hipErrorInvalidValue;
+  const int g = grid_for(static_cast<int64_t>(rows) * (cols / 4));
+  if (dtype == DT_BF16)
+    hipLaunchKernelGGL(quantize_rows_kernel<uint16_t>, dim3(g), dim3(256), 0, s, static_cast<const uint16_t*>(x), ldx,
+                       rows, cols, out, ldo, qs, amax);
+  else if (dtype == DT_F32)
+    hipLaunchKernelGGL(quantize_rows_kernel<float>, dim3(g), dim3(256), 0, s, static_cast<const float*>(x), ldx, rows,
+                       cols, out, ldo, qs, amax);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace pz

@@ -65,6 +65,9 @@ class Stage:
     seg_b: object = None
     layer: object = None
     buffers: dict = field(default_factory=dict)
+    index: int = 0                # position in the stage list
+    fp8: bool = False             # forward GEMM on e4m3 operands (fp8 policy)
+    w8_index: int = -1            # row of the fp8 weight scale table
 
     @property
     def has_epi(self) -> bool:
@@ -152,6 +155,8 @@ class FusedTrainer:
         self.compute = torch.bfloat16 if model.precision.name in ("bfloat16", "fp8") else torch.float32
         self.ctx = context or get_context()
         self.stages, self.head = compile_stages(model)
+        for i, st in enumerate(self.stages):
+            st.index = i
         self.grads = torch.zeros(self.store.numel + 64, device=self.dev, dtype=torch.float32)
         self.loss_slot = self.grads[self.store.numel:self.store.numel + 1]
         self.shadows: dict[int, torch.Tensor] = {}
@@ -166,6 +171,22 @@ class FusedTrainer:
             seg = next(s for s in self.store.segments if s.offset == sh_off)
             sh.copy_(self.store.view(seg))
         self.opt.init_stats()
+        # fp8 policy: e4m3 copies [out, in] of every GEMM weight + per-tensor {q, s} records
+        self.fp8 = model.precision.name == "fp8"
+        self.w8: dict[int, torch.Tensor] = {}
+        if self.fp8:
+            gemms = [st for st in self.stages if st.kind == "gemm"]
+            self.wqs = torch.ones(len(gemms), 2, device=self.dev)
+            self.wamax = torch.zeros(len(gemms), device=self.dev)
+            self.aqs = torch.ones(len(self.stages), 2, device=self.dev)     # activations (delayed)
+            self.aamax = torch.zeros(len(self.stages), device=self.dev)
+            self.xqs = torch.ones(2, device=self.dev)                       # first-layer input
+            self.xamax = torch.zeros(1, device=self.dev)
+            for k, st in enumerate(gemms):
+                st.w8_index = k
+                self.w8[st.seg_w.offset] = torch.empty(st.seg_w.shape[1], st.seg_w.shape[0], device=self.dev,
+                                                       dtype=torch.float8_e4m3fn)
+            self._refresh_fp8_weights()
         self._rows = None
         self._pending: list = []   # (epoch, ratio_row or None, event)
         self._drained = 0
@@ -256,10 +277,59 @@ class FusedTrainer:
         if pos != 1:
             raise UnsupportedModel(f"head input still has {pos} positions per sample")
         self._plan_relu_masks(rows_b)
+        self._plan_fp8(rows_b)
         # record-mode scratch: one buffer per layer output / grad, allocated lazily
 
     # ------------------------------------------------------------------------------------
     # epilogue specs
+    def _refresh_fp8_weights(self) -> None:
+        """Current-scaled e4m3 weight copies, transposed to [out, in] (K-contiguous GEMM operand)."""
+        ops = torch.ops.pz
+        for st in self.stages:
+            if st.kind != "gemm":
+                continue
+            k = st.w8_index
+            w = self.store.view(st.seg_w)
+            ops.amax_abs(w, self.wamax[k:k + 1])
+            ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
+            ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
+
+    def _plan_fp8(self, rows_b: int) -> None:
+        """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
+        for st in self.stages:
+            st.fp8 = False
+            st.buffers.pop("y8", None)
+        if not self.fp8:
+            return
+        self.x8 = None
+        for i, st in enumerate(self.stages):
+            if st.kind != "gemm":
+                continue
+            prev = self.stages[i - 1] if i > 0 else None
+            if prev is None:
+                x = self.x_in
+                if x.dtype != torch.bfloat16 or x.shape[1] % 64:
+                    continue
+                x8 = torch.empty(x.shape, device=self.dev, dtype=torch.float8_e4m3fn)
+            else:
+                # the producing GEMM writes the e4m3 copy from its epilogue: it must be on the MFMA path
+                if prev.kind != "gemm" or prev.buffers["y"].shape[1] % 64:
+                    continue
+                px = self.x8 if prev.fp8 and prev.index == 0 else (
+                    self.stages[prev.index - 1].buffers.get("y8") if prev.fp8 else
+                    (self.stages[prev.index - 1].buffers["y"] if prev.index > 0 else self.x_in))
+                pw = self.w8[prev.seg_w.offset] if prev.fp8 else self._w(prev)
+                if px is None or PF.gemm_path(px, True, pw, prev.fp8, prev.buffers["y"]) != "mfma":
+                    continue
+                x8 = torch.empty(prev.buffers["y"].shape, device=self.dev, dtype=torch.float8_e4m3fn)
+            if PF.gemm_path(x8, True, self.w8[st.seg_w.offset], True, st.buffers["y"]) != "mfma":
+                continue
+            st.fp8 = True
+            if prev is None:
+                self.x8 = x8
+            else:
+                prev.buffers["y8"] = x8
+
     def _plan_relu_masks(self, rows_b: int) -> None:
         """ReLU GEMM stages feeding a GEMM stage keep a 1-bit mask of ``y > 0`` next to ``y``: the
         next stage's dX GEMM reads it (8 B per 64 columns) instead of re-reading ``y`` (128 B)."""
@@ -329,12 +399,18 @@ class FusedTrainer:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
         rec = {} if record else None
+        if self.fp8 and not record and self.x8 is not None:  # current-scaled e4m3 input
+            ops.amax_abs(self.x_in, self.xamax)
+            ops.scale_update(self.xamax, self.xqs, 1.0, True)
+            ops.quantize_rows(self.x_in, self.x8, self.xqs, None)
         x = self.x_in
         prev = None
         for st in self.stages:
             x = self._forward_stage(st, x, batch, dropout, seed, rec)
             prev = st
         last = prev
+        if self.fp8 and not record:  # this step's activation amax -> next step's scales
+            ops.scale_update(self.aamax, self.aqs, 1.25, True)
 
         # ---------------- head
         g_pre = self._head(last, x, batch, dropout, seed, rec)
@@ -354,6 +430,8 @@ class FusedTrainer:
         if record:
             self._finish_record(rec, batch, l2)
         self.opt.step(self.grads, lr, l2, 1.0 / world)
+        if self.fp8:
+            self._refresh_fp8_weights()
         row = -1
         if want_ratios:
             row = self._ratio_rows
@@ -388,8 +466,20 @@ class FusedTrainer:
             ei, ef = self._epi(st, p, seed)
             if st.kind == "gemm":
                 bias = self.store.view(st.seg_b) if st.seg_b is not None else None
-                PF.gemm(x, True, self._w(st), False, y, bias=bias, mode=PF.EPI_FWD, epi=(ei, ef),
-                        mask=st.buffers.get("mask"))
+                kw = {}
+                if st.fp8:  # e4m3 x e4m3 with the per-tensor dequantisation factors
+                    i = st.index
+                    xa, sa = (self.x8, self.xqs[1:2]) if i == 0 else \
+                        (self.stages[i - 1].buffers["y8"], self.aqs[i - 1, 1:2])
+                    wa, wkc = self.w8[st.seg_w.offset], True
+                    kw.update(scale_a=sa, scale_b=self.wqs[st.w8_index, 1:2])
+                else:
+                    xa, wa, wkc = x, self._w(st), False
+                if "y8" in st.buffers:  # the next stage consumes an e4m3 copy (delayed scaling)
+                    kw.update(out8=st.buffers["y8"], out8_qscale=self.aqs[st.index, 0:1],
+                              amax=self.aamax[st.index:st.index + 1])
+                PF.gemm(xa, True, wa, wkc, y, bias=bias, mode=PF.EPI_FWD, epi=(ei, ef),
+                        mask=st.buffers.get("mask"), **kw)
             else:
                 self._bn_fwd(st, x, y, batch, ei, ef)
             return y

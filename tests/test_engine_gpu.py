@@ -159,3 +159,35 @@ def test_record_mode_matches_fused_cost():
     assert abs(fused - recorded) < 1e-5 * max(1, abs(fused))
     rec = tr.record()
     assert len(rec["activations"]) == len(gpu.layers)
+
+
+def test_fp8_training_tracks_bf16():
+    """fp8 policy: e4m3 forward GEMMs (current-scaled weights, delayed-scaled activations, e4m3
+    input) with bf16 backward; the loss curve follows the bf16 run of the same model + batches."""
+    sizes = [256, 512, 512, 128]
+    algos = ["relu", "relu", "softmax"]
+    n, S, steps = 4096, 1024, 12
+    g = torch.Generator().manual_seed(2)
+    inputs = torch.randn(n, sizes[0], generator=g)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    idx = torch.randint(0, n, (steps, S), generator=g)
+    curves = {}
+    for dtype in ("bfloat16", "fp8"):
+        torch.manual_seed(0)
+        model = NeuralNetworkModel("f8", sizes, "xavier", "random", algos, "adam", dtype=dtype, device="cuda")
+        tr = FusedTrainer(model)
+        tr.load_tensors(inputs, labels, seed=9)
+        tr.begin(steps)
+        for e in range(steps):
+            tr.step(e, 0.002, S, 0.1, 1e-4, want_ratios=False, record=False, indices=idx[e])
+        curves[dtype] = [c for _, c, _, _ in tr.drain()]
+        if dtype == "fp8":
+            assert [st.fp8 for st in tr.stages] == [True, True, True]
+            assert "y8" in tr.stages[0].buffers and "y8" in tr.stages[1].buffers
+            s_w = tr.wqs[:, 1].cpu()
+            assert torch.all(s_w > 0) and torch.all(torch.isfinite(s_w))
+    bf, f8 = curves["bfloat16"], curves["fp8"]
+    assert all(math.isfinite(c) for c in f8)
+    assert f8[-1] < f8[0] - 0.05  # it learns
+    for a, b in zip(bf, f8):
+        assert abs(a - b) < 0.05 * abs(a) + 0.02, (bf, f8)

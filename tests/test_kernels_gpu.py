@@ -143,6 +143,40 @@ def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
     assert (out_bit.double() - ref).abs().max().item() < 0.02 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (4096 + 64, 4096, 512), (256, 1024, 8192)])
+def test_gemm_fp8_forward(native_lib, M, N, K):
+    """e4m3 x e4m3 (v_mfma_scale_f32_32x32x64_f8f6f4) + dequant scales + fused stage epilogue +
+    e4m3 copy of the output + amax, against an fp32 reference on the same e4m3 values."""
+    f8 = torch.float8_e4m3fn
+    p, seed = 0.1, (3, 4)
+    x8 = (torch.randn(M, K, device=DEV) * 4).to(f8)
+    w8 = (torch.randn(N, K, device=DEV) * 2).to(f8)        # weights stored [out, in] (K-contiguous)
+    sa = torch.tensor([0.125], device=DEV)
+    sb = torch.tensor([1.0 / 64], device=DEV)
+    bias = torch.randn(N, device=DEV)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    y8 = torch.empty(M, N, device=DEV, dtype=f8)
+    qs = torch.tensor([8.0], device=DEV)
+    amax = torch.zeros(1, device=DEV)
+    mask = torch.empty(M, PF.relu_mask_cols(N), device=DEV, dtype=torch.uint8)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=p, seed=seed)
+    assert PF.gemm_path(x8, True, w8, True, y) == "mfma"
+    PF.gemm(x8, True, w8, True, y, bias=bias, mode=PF.EPI_FWD, epi=epi, scale_a=sa, scale_b=sb, out8=y8,
+            out8_qscale=qs, amax=amax, mask=mask)
+    h = (x8.double() @ w8.double().t()) * (0.125 / 64) + bias.double()
+    m1 = torch.from_numpy(keep_mask(M * N, *seed, 1, p).reshape(M, N)).to(DEV)
+    m2 = torch.from_numpy(keep_mask(M * N, *seed, 2, p).reshape(M, N)).to(DEV)
+    ref = torch.relu(h * m1 / (1 - p)) * m2 / (1 - p)
+    err = (y.double() - ref).abs().max().item()
+    assert err < 0.01 * ref.abs().max().item(), err
+    yf = y.float()
+    assert amax.item() == yf.abs().max().item()
+    exp8 = (yf * 8.0).clamp(-448, 448).to(f8)
+    assert (y8.view(torch.uint8) != exp8.view(torch.uint8)).float().mean().item() < 1e-4
+    bits = torch.stack([(mask[:, :N // 8].int() >> b) & 1 for b in range(8)], dim=2).reshape(M, N)
+    assert torch.equal(bits.bool(), yf > 0)
+
+
 def test_stage_kernels_match_torch(native_lib):
     x = torch.randn(1000, 33, device=DEV, dtype=torch.float64, requires_grad=True)
     for algo, fn in [("relu", torch.relu), ("sigmoid", torch.sigmoid), ("tanh", torch.tanh)]:
