@@ -270,8 +270,18 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       }
     }
   }
-  if (want8 && p.amax != nullptr) {
+  if (want8 && p.amax != nullptr) {  // one atomic per workgroup (same-address atomics serialise)
     amax = wave_max(amax);
-    if (lane == 0) atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(amax));
+    constexpr int NW = WM * WN;
+    __syncthreads();  // the LDS image has been read out
+    PZ_LDS float* part = (PZ_LDS float*)(smem);
+    if (lane == 0) part[threadIdx.x >> 6] = amax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float m = part[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) m = fmaxf(m, part[w]);
+      atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(m));
+    }
   }
 }

@@ -24,7 +24,10 @@ ELEMS_PER_BLOCK = 4096  # keep in sync with kOptElemsPerBlock (csrc/pz_kernels.h
 
 class FusedOptimizer:
     def __init__(self, store: ParamStore, params: list[torch.Tensor], torch_opt: torch.optim.Optimizer | None,
-                 shadows: dict[int, torch.Tensor]):
+                 shadows: dict[int, torch.Tensor] | list[dict[int, torch.Tensor]]):
+        # shadows: low-precision weight copies the update writes; a LIST of dicts = ping-pong sets
+        # selected per launch by `parity` (the trainer reads one set while the other is written)
+        shadow_sets = shadows if isinstance(shadows, list) else [shadows]
         self.store = store
         self.params = params
         self.torch_opt = torch_opt
@@ -47,10 +50,10 @@ class FusedOptimizer:
             starts.append(acc)
             acc += b
         self.total_blocks = acc
-        packed = torch.ops.pz.pack_segments(
+        self.segments_p = [torch.ops.pz.pack_segments(
             [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
-            [slot_of.get(id(s), -1) for s in segs], [shadows.get(s.offset) for s in segs])
-        self.segments = packed.to(dev)
+            [slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs]).to(dev) for sh in shadow_sets]
+        self.segments = self.segments_p[0]
         self.block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
         self.num_segments = len(segs)
         self.nslots = len(self.weight_slots)
@@ -59,6 +62,31 @@ class FusedOptimizer:
         # double-buffered per-slot stats: sum(dw), sum(dw^2), sum(w), sum(w^2)
         self.stats = [torch.zeros(max(1, self.nslots) * 4, device=dev, dtype=torch.float64) for _ in range(2)]
         self.cur = 0
+        self.shadow_sets = shadow_sets
+        self.slot_of = slot_of
+        self.groups: dict = {}
+
+    def define_groups(self, keys: list[int]) -> None:
+        """Split the update into launches: one per listed segment offset (a dense weight whose
+        gradient bucket is ready early in the backward) plus one for every other segment. Each
+        launch is the same fused kernel over its own packed segment table."""
+        dev = self.store.device
+        by_off = {s.offset: s for s in self.store.segments}
+        rest = sorted((s for s in self.store.segments if s.offset not in set(keys)), key=lambda s: s.offset)
+        for key, segs in [(k, [by_off[k]]) for k in keys] + [("rest", rest)]:
+            if not segs:
+                continue
+            blocks = [max(1, math.ceil(s.numel / ELEMS_PER_BLOCK)) for s in segs]
+            starts, acc = [], 0
+            for b in blocks:
+                starts.append(acc)
+                acc += b
+            block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
+            for parity, sh in enumerate(self.shadow_sets):
+                packed = torch.ops.pz.pack_segments(
+                    [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
+                    [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs]).to(dev)
+                self.groups[(key, parity)] = (packed, block_seg, len(segs), acc)
 
     # ------------------------------------------------------------------------------------
     def _adopt_state(self) -> None:
@@ -98,8 +126,18 @@ class FusedOptimizer:
         torch.ops.pz.segment_stats(self.store.flat, self.segments, self.block_seg, self.num_segments,
                                    self.total_blocks, prev)
 
-    def step(self, grads: torch.Tensor, lr: float, l2: float, grad_scale: float) -> None:
-        stats = self.stats[self.cur]
+    def step(self, grads: torch.Tensor, lr: float, l2: float, grad_scale: float, parity: int = 0) -> None:
+        self.begin_step(lr)
+        self._launch(grads, self.segments_p[parity], self.block_seg, self.num_segments, self.total_blocks, l2,
+                     grad_scale)
+
+    def step_group(self, key, grads: torch.Tensor, l2: float, grad_scale: float, parity: int = 0) -> None:
+        """Update one group (define_groups) with the hyper-parameters of the last begin_step()."""
+        g = self.groups.get((key, parity))
+        if g is not None:
+            self._launch(grads, *g, l2, grad_scale)
+
+    def begin_step(self, lr: float) -> None:
         if self.adam:
             group = self.torch_opt.param_groups[0]
             b1, b2 = group["betas"]
@@ -111,9 +149,13 @@ class FusedOptimizer:
         else:
             b1 = b2 = eps = 0.0
             bc1 = bc2s = 1.0
-        torch.ops.pz.optimizer_step(self.store.flat, grads, self.exp_avg, self.exp_avg_sq, self.segments,
-                                    self.block_seg, self.num_segments, self.total_blocks, self.adam, lr, b1, b2, eps,
-                                    bc1, bc2s, grad_scale, l2, stats)
+        self._hp = (lr, b1, b2, eps, bc1, bc2s)
+
+    def _launch(self, grads, segments, block_seg, nseg, nblocks, l2: float, grad_scale: float) -> None:
+        lr, b1, b2, eps, bc1, bc2s = self._hp
+        torch.ops.pz.optimizer_step(self.store.flat, grads, self.exp_avg, self.exp_avg_sq, segments, block_seg, nseg,
+                                    nblocks, self.adam, lr, b1, b2, eps, bc1, bc2s, grad_scale, l2,
+                                    self.stats[self.cur])
 
     def finalize(self, loss: torch.Tensor | None, world: int, l2: float, costs: torch.Tensor, epoch: int,
                  ratios: torch.Tensor, ratio_row: int) -> None:

@@ -30,6 +30,7 @@ follows a linear or batchnorm.
 from __future__ import annotations
 
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from datetime import datetime, timedelta
@@ -159,17 +160,21 @@ class FusedTrainer:
             st.index = i
         self.grads = torch.zeros(self.store.numel + 64, device=self.dev, dtype=torch.float32)
         self.loss_slot = self.grads[self.store.numel:self.store.numel + 1]
-        self.shadows: dict[int, torch.Tensor] = {}
+        # low-precision GEMM copies of the weights, PING-PONG: step t's GEMMs read set `parity`
+        # while its optimizer writes set 1-parity — so a weight can be updated as soon as its
+        # gradient is reduced, even while the dX GEMM of the same layer still reads it
+        self.shadow_sets: list[dict[int, torch.Tensor]] = [{}, {}]
+        self.parity = 0
         for st in self.stages:
             if st.kind == "gemm" and self.compute != torch.float32:
-                sh = torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute)
-                sh.copy_(self.store.view(st.seg_w))
-                self.shadows[st.seg_w.offset] = sh
-        self.opt = FusedOptimizer(self.store, model.params, model.optimizer, self.shadows)
+                for sset in self.shadow_sets:
+                    sset[st.seg_w.offset] = torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute)
+        self.opt = FusedOptimizer(self.store, model.params, model.optimizer, self.shadow_sets)
         self.ctx.broadcast_(self.store.flat)  # identical replicas (rank 0 wins)
-        for sh_off, sh in self.shadows.items():
-            seg = next(s for s in self.store.segments if s.offset == sh_off)
-            sh.copy_(self.store.view(seg))
+        for sset in self.shadow_sets:
+            for sh_off, sh in sset.items():
+                seg = next(s for s in self.store.segments if s.offset == sh_off)
+                sh.copy_(self.store.view(seg))
         self.opt.init_stats()
         # fp8 policy: e4m3 copies [out, in] of every GEMM weight + per-tensor {q, s} records
         self.fp8 = model.precision.name == "fp8"
@@ -187,6 +192,14 @@ class FusedTrainer:
                 self.w8[st.seg_w.offset] = torch.empty(st.seg_w.shape[1], st.seg_w.shape[0], device=self.dev,
                                                        dtype=torch.float8_e4m3fn)
             self._refresh_fp8_weights()
+        # Optimizer overlap: each GEMM weight is updated on a side stream as soon as its gradient
+        # bucket is complete (its dW GEMM on one GPU, its all-reduce under DP), while the rest of
+        # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
+        self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
+        self.opt_stream = torch.cuda.Stream(device=self.dev) if self.overlap else None
+        self.opt.define_groups([st.seg_w.offset for st in self.stages if st.kind == "gemm"])
+        self._opt_done = None
+        self._ov = None
         self._rows = None
         self._pending: list = []   # (epoch, ratio_row or None, event)
         self._drained = 0
@@ -282,10 +295,10 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------------------------
     # epilogue specs
-    def _refresh_fp8_weights(self) -> None:
+    def _refresh_fp8_weights(self, only: Stage | None = None) -> None:
         """Current-scaled e4m3 weight copies, transposed to [out, in] (K-contiguous GEMM operand)."""
         ops = torch.ops.pz
-        for st in self.stages:
+        for st in self.stages if only is None else [only]:
             if st.kind != "gemm":
                 continue
             k = st.w8_index
@@ -293,6 +306,18 @@ class FusedTrainer:
             ops.amax_abs(w, self.wamax[k:k + 1])
             ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
             ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
+
+    def _opt_async(self, key, handle, st: Stage | None) -> None:
+        """Queue the update of one optimizer group on the side stream behind its gradient."""
+        main, l2, scale = self._ov
+        ready = torch.cuda.Event()
+        ready.record(main)
+        with torch.cuda.stream(self.opt_stream):
+            self.opt_stream.wait_event(ready)
+            self.ctx.wait_one(handle)
+            self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
+            if self.fp8 and st is not None:
+                self._refresh_fp8_weights(st)
 
     def _plan_fp8(self, rows_b: int) -> None:
         """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
@@ -361,7 +386,7 @@ class FusedTrainer:
 
     def _w(self, st: Stage) -> torch.Tensor:
         """GEMM operand for the stage's weight: bf16 shadow or the fp32 master view, [in, out]."""
-        sh = self.shadows.get(st.seg_w.offset)
+        sh = self.shadow_sets[self.parity].get(st.seg_w.offset)
         return sh if sh is not None else self.store.view(st.seg_w)
 
     # ------------------------------------------------------------------------------------
@@ -382,6 +407,14 @@ class FusedTrainer:
             self._alloc_progress(epoch + 1)
         seed = self._seed(epoch)
         ops = torch.ops.pz
+        main = torch.cuda.current_stream(self.dev)
+        if self._opt_done is not None:  # the previous step's side-stream updates
+            main.wait_event(self._opt_done)
+            self._opt_done = None
+        overlap = self.overlap and not record
+        if overlap:
+            self.opt.begin_step(lr)
+            self._ov = (main, l2, 1.0 / world)
 
         # zero the accumulated-gradient region (+ loss slot)
         self.grads[self.store.accum_offset:].zero_()
@@ -426,10 +459,26 @@ class FusedTrainer:
 
         # ---------------- reduce + update
         handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:]))
+        if overlap:
+            self._opt_async("rest", handles[-1], None)
+            self._ov = None
+            row = -1
+            if want_ratios:
+                row = self._ratio_rows
+                self._ratio_rows += 1
+            with torch.cuda.stream(self.opt_stream):
+                self.opt.finalize(self.loss_slot, world, l2, self.costs, epoch, self.ratios, row)
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(self.opt_stream)
+            self._opt_done = ev
+            self.parity = 1 - self.parity
+            self._pending.append((epoch, row if want_ratios else None, ev))
+            return
         self.ctx.wait_all(handles)
         if record:
             self._finish_record(rec, batch, l2)
-        self.opt.step(self.grads, lr, l2, 1.0 / world)
+        self.opt.step(self.grads, lr, l2, 1.0 / world, 1 - self.parity)
+        self.parity = 1 - self.parity
         if self.fp8:
             self._refresh_fp8_weights()
         row = -1
@@ -580,6 +629,17 @@ class FusedTrainer:
         w_grad = self.store.view(st.seg_w, self.grads)
         PF.gemm(x_in, False, g, False, w_grad)
         handles.append(self.ctx.all_reduce_async(w_grad))
+        # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
+        # unless the GEMMs read the fp32 master itself (float32 policy)
+        early = st.seg_w.offset in self.shadow_sets[self.parity]
+        if self._ov is not None and early:
+            self._opt_async(st.seg_w.offset, handles[-1], st)
+        out = self._backward_dx(st, before, g, batch, p, seed, rec)
+        if self._ov is not None and not early:
+            self._opt_async(st.seg_w.offset, handles[-1], st)
+        return out
+
+    def _backward_dx(self, st: Stage, before: Stage | None, g, batch, p, seed, rec):
         if before is None:
             return None, True
         # dX = dZ · Wᵀ (+ previous stage's epilogue derivative and bias colsum when fusable)

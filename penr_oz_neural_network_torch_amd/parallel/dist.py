@@ -47,12 +47,18 @@ class DataParallelContext:
 
     def wait_all(self, handles) -> None:
         for h in handles:
-            if h is None:
-                continue
-            work, low, dst = h
-            work.wait()
-            if low is not None:
-                dst.copy_(low)
+            self.wait_one(h)
+
+    def wait_one(self, h) -> None:
+        """Make the CURRENT stream wait for one bucket (and unpack a reduced-precision bucket)."""
+        if h is None:
+            return
+        work, low, dst = h
+        work.wait()
+        if low is not None:
+            if dst.is_cuda:
+                low.record_stream(torch.cuda.current_stream(dst.device))
+            dst.copy_(low)
 
     def broadcast_(self, t: torch.Tensor, src: int = 0) -> None:
         if self.enabled:
