@@ -365,15 +365,18 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
   const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;
+  // (measured, not kept: DMA issued by waves 0-3 only, twice the instructions each: -2..4%)
+  constexpr int NWD = C::NW;
+  constexpr int GD = C::G;
   auto stage_a = [&](int kt) {
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
-    if constexpr (A_KC) stage_kc<BM, C::NW, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
-    else stage_mn<BM, C::NW, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
+    if constexpr (A_KC) stage_kc<BM, NWD, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
+    else stage_mn<BM, NWD, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
   };
   auto stage_b = [&](int kt) {
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (B_KC) stage_kc<BN, C::NW, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
-    else stage_mn<BN, C::NW, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
+    if constexpr (B_KC) stage_kc<BN, NWD, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
+    else stage_mn<BN, NWD, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
   };
   auto stage = [&](int kt, int slot) {  // slot == kt % NS
     (void)slot;
@@ -383,66 +386,32 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 
   const int nk = p.K / (F8 ? 2 * kBK : kBK);
   constexpr int NS = C::NS;
-  // K-contiguous operands in the 8-wave schedule are staged in PAIRS of steps (t, t+1), the two
-  // 64-B halves of every 128-B row line back to back: one L2 request per line instead of two.
-  constexpr bool PAIR = C::NW == 8 && NS == 4 && (A_KC || B_KC) && VAR != 4;
-  if constexpr (PAIR) {
-    for (int s = 0; s < (A_KC ? 2 : 3); ++s)
-      if (s < nk) stage_a(s);
-    for (int s = 0; s < (B_KC ? 2 : 3); ++s)
-      if (s < nk) stage_b(s);
-  } else {
+  // Measured, not kept: staging K-contiguous operands in PAIRS of steps so both 64-B halves of
+  // every 128-B line are requested back to back (halved L1->L2 requests, matched hipBLASLt's
+  // request count) ran 2-4% SLOWER than the plain ring with DEFER below.
+  constexpr bool DEFER = VAR != 4;  // group 0 waits for step t+1 at the END of M_t (+2..6%)
 #pragma unroll
-    for (int s = 0; s < NS - 1; ++s)
-      if (s < nk) stage(s, s);
-  }
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) stage(s, s);
 
   if constexpr (C::NW == 8) {
     // Ping-pong (8 waves = 2 per SIMD). Waves 0-3 and 4-7 sit on the same four SIMDs and run one
     // barrier interval apart: while one wave of a SIMD issues its MFMA block (setprio 1) its
     // partner issues the next step's LDS-DMA + fragment reads into the MFMA gaps. Per wave and
-    // step t: R_t = {stage t+NS-1, wait until step t+1 landed, read slot t, lgkmcnt(0)} |
-    // barrier | M_t = {MFMAs} | barrier. Hazards: slot t+1 is waited for by BOTH groups during
-    // R_t, at least one barrier before either group reads it in R_{t+1}; slot (t+NS-1)%NS =
-    // (t-1)%NS was last read in R_{t-1} and every wave retired those reads (lgkmcnt(0)) before
-    // the barrier that precedes R_t of either group.
-    //
-    // PAIR staging: even steps t stage K-contiguous operands for t+2 and t+3, M/N-contiguous
-    // ones stage t+3 every step (A before B, pair halves adjacent). In steady state (t+4 < nk)
-    // the instructions younger than the last one of step t+1 are: even t: 2G; odd t: whatever
-    // of steps t+2, t+3 was issued after it (per layout below). Tail steps drain to vmcnt(0).
+    // step t: R_t = {stage t+NS-1, [group 1: wait until step t+1 landed], read slot t,
+    // lgkmcnt(0)} | barrier | M_t = {MFMAs, [group 0: wait until step t+1 landed]} | barrier.
+    // Group 0 runs one interval AHEAD, so its wait can sit at the end of its MFMA block (one
+    // interval more of DMA latency hidden) and still precede the barrier that opens R_{t+1} for
+    // both groups. Hazards: slot t+1 is waited for by every wave before that barrier; slot
+    // (t+NS-1)%NS = (t-1)%NS was last read in R_{t-1} and every wave retired those reads
+    // (lgkmcnt(0)) before the barrier that precedes R_t of either group.
     const int grp = wave >> 2;
-    if constexpr (PAIR) wait_vm<0>();
-    else wait_newer<C::G, NS - 2>(min(nk, NS - 1) - 1);  // step 0 landed
+    wait_newer<GD, NS - 2>(min(nk, NS - 1) - 1);  // step 0 landed
     barrier();
     if (grp == 1) barrier();
-    constexpr int ODD_INFLIGHT = A_KC && B_KC ? C::GB : (A_KC ? C::GA + 2 * C::GB : C::GA + C::GB);
     for (int t = 0; t < nk; ++t) {
-      if constexpr (PAIR) {
-        if (VAR != 2) {
-          if (A_KC) {
-            if ((t & 1) == 0 && t + 2 < nk) stage_a(t + 2);
-            if ((t & 1) == 0 && t + 3 < nk) stage_a(t + 3);
-          } else if (t + 3 < nk) {
-            stage_a(t + 3);
-          }
-          if (B_KC) {
-            if ((t & 1) == 0 && t + 2 < nk) stage_b(t + 2);
-            if ((t & 1) == 0 && t + 3 < nk) stage_b(t + 3);
-          } else if (t + 3 < nk) {
-            stage_b(t + 3);
-          }
-        }
-        if (t + 4 < nk) {
-          if (t & 1) wait_vm<ODD_INFLIGHT>();
-          else wait_vm<2 * C::G>();
-        } else {
-          wait_vm<0>();
-        }
-      } else {
-        if (VAR != 2 && t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
-        wait_newer<C::G, NS - 2>(min(nk - 1, t + NS - 1) - (t + 1));  // step t+1 landed
-      }
+      if (VAR != 2 && t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
+      if (!DEFER || grp == 1) wait_newer<GD, NS - 2>(min(nk - 1, t + NS - 1) - (t + 1));  // step t+1 landed
       Frags f;
       if constexpr (VAR == 3) {  // perf probe: no fragment reads
 #pragma unroll
@@ -460,6 +429,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 #pragma unroll
         for (int i = 0; i < C::TM; ++i) acc[i][0][0] += static_cast<float>(f.a[i][0] + f.b[i % C::TN][1]);
       }
+      if (DEFER && grp == 0) wait_newer<GD, NS - 2>(min(nk - 1, t + NS - 1) - (t + 1));
       barrier();
     }
     if (grp == 0) barrier();
