@@ -120,34 +120,49 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
 }
 
 // bf16 fast path: every lane holds NCH chunks of 8 logits in registers (one read of the row),
-// 16-B loads / stores, dropout masks two hashes per 4 elements.
+// 16-B loads / stores, dropout masks two hashes per 4 elements. A wave's RPW rows are loaded up
+// front (memory-level parallelism), bias-gradient column partials stay in registers and are
+// reduced across the block's waves through LDS once (no LDS atomics: they made this 60 us).
 template <int NCH>
 __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
-  extern __shared__ float cs_lds[];
+  extern __shared__ float cs_lds[];  // [4][cols] wave partials (when colsum)
   __shared__ float red[4];
+  constexpr int RPW = kHeadRows / 4;
   const uint16_t* __restrict__ logits = static_cast<const uint16_t*>(a.logits);
   uint16_t* __restrict__ dh = static_cast<uint16_t*>(a.dh);
   uint16_t* __restrict__ probs = static_cast<uint16_t*>(a.probs);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const bool cs_on = a.colsum != nullptr && dh != nullptr;
-  if (cs_on) {
-    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = 0.f;
-    __syncthreads();
-  }
+  float cs[NCH][8];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) cs[j][e] = 0.f;
+  bool ok[NCH];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j) ok[j] = (lane + 64 * j) * 8 < a.cols;
+  const int row0 = blockIdx.x * kHeadRows + wave * RPW;
+  uint4 raw[RPW][NCH];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr)
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int row = row0 + rr;
+      raw[rr][j] = (row < a.rows && ok[j])
+                       ? *reinterpret_cast<const uint4*>(logits + static_cast<int64_t>(row) * a.ld + (lane + 64 * j) * 8)
+                       : make_uint4(0, 0, 0, 0);
+    }
   float loss_acc = 0.f;
-  for (int rr = 0; rr < kHeadRows / 4; ++rr) {
-    const int row = blockIdx.x * kHeadRows + wave * (kHeadRows / 4) + rr;
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = row0 + rr;
     if (row >= a.rows) break;
     const uint16_t* lr = logits + static_cast<int64_t>(row) * a.ld;
     float v[NCH][8];
-    bool ok[NCH];
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
-      const int c0 = (lane + 64 * j) * 8;
-      ok[j] = c0 < a.cols;
-      uint4 u = ok[j] ? *reinterpret_cast<const uint4*>(lr + c0) : make_uint4(0, 0, 0, 0);
-      const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+      const uint32_t w[4] = {raw[rr][j].x, raw[rr][j].y, raw[rr][j].z, raw[rr][j].w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) { v[j][2 * e] = bf2f(w[e] & 0xFFFF); v[j][2 * e + 1] = bf2f(w[e] >> 16); }
     }
@@ -191,9 +206,8 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
           epi_bwd4(g + 4, zero4, idx + 4, a.epi);
           *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + c0) =
               make_uint4(pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7]));
-          if (cs_on)
 #pragma unroll
-            for (int e = 0; e < 8; ++e) atomicAdd(&cs_lds[c0 + e], g[e]);
+          for (int e = 0; e < 8; ++e) cs[j][e] += g[e];
         }
       }
     } else if (dh != nullptr) {
@@ -205,7 +219,19 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
     }
   }
   if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red);
-  if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
+  if (cs_on) {
+    float* mine = cs_lds + wave * a.cols;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+      if (ok[j])
+#pragma unroll
+        for (int e = 0; e < 8; ++e) mine[(lane + 64 * j) * 8 + e] = cs[j][e];
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.cols; c += 256) {
+      const float t = cs_lds[c] + cs_lds[a.cols + c] + cs_lds[2 * a.cols + c] + cs_lds[3 * a.cols + c];
+      if (t != 0.f) atomicAdd(a.colsum + c, t);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -383,9 +409,10 @@ hipError_t xent_head(const XentArgs& in, hipStream_t s) {
                    (a.probs == nullptr || a.ld_probs % 8 == 0) && a.idx_ld % 2 == 0 &&
                    (reinterpret_cast<uintptr_t>(a.logits) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dh) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(a.probs) & 15) == 0;
-  if (vec && a.cols <= 512) hipLaunchKernelGGL(xent_head_bf16_kernel<1>, grid, dim3(256), lds, s, a);
-  else if (vec && a.cols <= 1024) hipLaunchKernelGGL(xent_head_bf16_kernel<2>, grid, dim3(256), lds, s, a);
-  else if (vec && a.cols <= 2048) hipLaunchKernelGGL(xent_head_bf16_kernel<4>, grid, dim3(256), lds, s, a);
+  const size_t lds4 = 4 * lds;  // the bf16 kernel keeps one partial row per wave
+  if (vec && a.cols <= 512) hipLaunchKernelGGL(xent_head_bf16_kernel<1>, grid, dim3(256), lds4, s, a);
+  else if (vec && a.cols <= 1024) hipLaunchKernelGGL(xent_head_bf16_kernel<2>, grid, dim3(256), lds4, s, a);
+  else if (vec && a.cols <= 2048) hipLaunchKernelGGL(xent_head_bf16_kernel<4>, grid, dim3(256), lds4, s, a);
   else {
     PZ_DISPATCH_FLOAT(a.dtype, T, {
       using F = typename MathOf<T>::type;

@@ -197,7 +197,11 @@ class FusedTrainer:
         # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
         self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
         self.opt_stream = torch.cuda.Stream(device=self.dev) if self.overlap else None
-        self.opt.define_groups([st.seg_w.offset for st in self.stages if st.kind == "gemm"])
+        # one launch per GEMM weight except the first layer's, which comes last anyway and
+        # shares the final launch with the small accumulated parameters (biases, BN, embedding)
+        gemm_w = [st.seg_w.offset for st in self.stages if st.kind == "gemm"]
+        self._early_keys = set(gemm_w[1:])
+        self.opt.define_groups(gemm_w[1:])
         self._opt_done = None
         self._ov = None
         self._rows = None
@@ -307,17 +311,19 @@ class FusedTrainer:
             ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
             ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
 
-    def _opt_async(self, key, handle, st: Stage | None) -> None:
-        """Queue the update of one optimizer group on the side stream behind its gradient."""
+    def _opt_async(self, key, handles: list, stages: list[Stage]) -> None:
+        """Queue the update of one optimizer group on the side stream behind its gradient(s)."""
         main, l2, scale = self._ov
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             self.opt_stream.wait_event(ready)
-            self.ctx.wait_one(handle)
+            for h in handles:
+                self.ctx.wait_one(h)
             self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
-            if self.fp8 and st is not None:
-                self._refresh_fp8_weights(st)
+            if self.fp8:
+                for st in stages:
+                    self._refresh_fp8_weights(st)
 
     def _plan_fp8(self, rows_b: int) -> None:
         """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
@@ -415,6 +421,7 @@ class FusedTrainer:
         if overlap:
             self.opt.begin_step(lr)
             self._ov = (main, l2, 1.0 / world)
+            self._late_stages, self._late_handles = [], []
 
         # zero the accumulated-gradient region (+ loss slot)
         self.grads[self.store.accum_offset:].zero_()
@@ -460,7 +467,8 @@ class FusedTrainer:
         # ---------------- reduce + update
         handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:]))
         if overlap:
-            self._opt_async("rest", handles[-1], None)
+            late = list(self._late_handles)
+            self._opt_async("rest", late + [handles[-1]], self._late_stages)
             self._ov = None
             row = -1
             if want_ratios:
@@ -631,12 +639,16 @@ class FusedTrainer:
         handles.append(self.ctx.all_reduce_async(w_grad))
         # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
         # unless the GEMMs read the fp32 master itself (float32 policy)
+        own = st.seg_w.offset in self._early_keys
         early = st.seg_w.offset in self.shadow_sets[self.parity]
-        if self._ov is not None and early:
-            self._opt_async(st.seg_w.offset, handles[-1], st)
+        if self._ov is not None and not own:  # updated by the final launch
+            self._late_stages.append(st)
+            self._late_handles.append(handles[-1])
+        if self._ov is not None and own and early:
+            self._opt_async(st.seg_w.offset, [handles[-1]], [st])
         out = self._backward_dx(st, before, g, batch, p, seed, rec)
-        if self._ov is not None and not early:
-            self._opt_async(st.seg_w.offset, handles[-1], st)
+        if self._ov is not None and own and not early:
+            self._opt_async(st.seg_w.offset, [handles[-1]], [st])
         return out
 
     def _backward_dx(self, st: Stage, before: Stage | None, g, batch, p, seed, rec):
