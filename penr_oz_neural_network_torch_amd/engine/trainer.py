@@ -44,6 +44,15 @@ from .optim import FusedOptimizer
 
 ROW_PAD = 64  # batch rows padded to the GEMM K-tile so dW = XᵀdZ stays on the MFMA path
 
+# Tracing / debugging: PZ_TRACE=1 brackets every step phase in a roctx range
+# (visible with `rocprofv3 --marker-trace`); PZ_DEBUG_SYNC=1 synchronises after every phase so an
+# asynchronous kernel fault surfaces at the phase that caused it (combine with the runtime's
+# AMD_SERIALIZE_KERNEL=3 for per-kernel attribution).
+_TRACE = os.environ.get("PZ_TRACE", "0") == "1"
+_DEBUG_SYNC = os.environ.get("PZ_DEBUG_SYNC", "0") == "1"
+
+
+
 
 def _round_up(n: int, a: int) -> int:
     return (n + a - 1) // a * a
@@ -428,6 +437,7 @@ class FusedTrainer:
         self.grads[self.store.accum_offset:].zero_()
 
         # ---------------- sample + input
+        self._phase("pz.sample")
         gseed = ((self.base_seed[0] + epoch * 0x632BE5AB) & 0xFFFFFFFF,
                  (self.base_seed[1] ^ (self.ctx.rank * 0x27D4EB2F + epoch)) & 0xFFFFFFFF)
         idx = None
@@ -440,6 +450,7 @@ class FusedTrainer:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
         rec = {} if record else None
+        self._phase("pz.forward")
         if self.fp8 and not record and self.x8 is not None:  # current-scaled e4m3 input
             ops.amax_abs(self.x_in, self.xamax)
             ops.scale_update(self.xamax, self.xqs, 1.0, True)
@@ -454,9 +465,11 @@ class FusedTrainer:
             ops.scale_update(self.aamax, self.aqs, 1.25, True)
 
         # ---------------- head
+        self._phase("pz.head")
         g_pre = self._head(last, x, batch, dropout, seed, rec)
 
         # ---------------- backward
+        self._phase("pz.backward")
         handles = []
         g = last.buffers["g"]
         for si in range(len(self.stages) - 1, -1, -1):
@@ -466,6 +479,7 @@ class FusedTrainer:
             g, g_pre = self._backward_stage(st, before, x_in, g, g_pre, batch, dropout, seed, rec, handles)
 
         # ---------------- reduce + update
+        self._phase("pz.update")
         handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:]))
         if overlap:
             late = list(self._late_handles)
@@ -482,6 +496,7 @@ class FusedTrainer:
             self._opt_done = ev
             self.parity = 1 - self.parity
             self._pending.append((epoch, row if want_ratios else None, ev))
+            self._phase(None)
             return
         self.ctx.wait_all(handles)
         if record:
@@ -498,6 +513,20 @@ class FusedTrainer:
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         self._pending.append((epoch, row if want_ratios else None, ev))
+        self._phase(None)
+
+    _in_phase = False
+
+    def _phase(self, name: str | None) -> None:
+        """End the current step phase and start `name` (None: end only)."""
+        if _TRACE:
+            if self._in_phase:
+                torch.cuda.nvtx.range_pop()
+            if name is not None:
+                torch.cuda.nvtx.range_push(name)
+            self._in_phase = name is not None
+        if _DEBUG_SYNC:
+            torch.cuda.synchronize(self.dev)
 
     # ------------------------------------------------------------------------------------
     def _forward_stage(self, st: Stage, x, batch, p, seed, rec):

@@ -19,6 +19,7 @@ batchnorm, embeddings) and the loss scalar.
 from __future__ import annotations
 
 import os
+from datetime import timedelta
 from dataclasses import dataclass
 
 import torch
@@ -92,7 +93,12 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        dist.init_process_group(backend=backend)
+            # failure detection: a rank that dies or a collective that hangs must abort the job
+            # (RCCL async error handling + the collective watchdog timeout) instead of hanging the
+            # node; the REST layer then persists status "Failed" 
+            os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        timeout = timedelta(seconds=float(os.environ.get("PZ_DIST_TIMEOUT_S", "600")))
+        dist.init_process_group(backend=backend, timeout=timeout)
     comm = os.environ.get("PZ_GRAD_COMM_DTYPE")
     comm_dtype = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": None, None: None}.get(comm)
     if dist.is_initialized():

@@ -26,6 +26,7 @@ import json
 import logging
 import os
 import tempfile
+import threading
 
 import torch
 
@@ -165,6 +166,62 @@ def save(model_id: str, skeleton: dict, optimizer_state: dict | None) -> None:
         opath = optimizer_path(model_id)
         _atomic_torch_save(_to_cpu(optimizer_state), opath)
         log.info(f"Optimizer saved successfully: {opath}")
+
+
+# --------------------------------------------------------------------------------------------
+# background writes (periodic checkpoints of long trainings)
+# --------------------------------------------------------------------------------------------
+_inflight: dict[str, threading.Thread] = {}
+_inflight_lock = threading.Lock()
+
+
+def snapshot(skeleton, optimizer_state: dict | None):
+    """Host copy of a checkpoint: parameter tensors (TensorRef leaves, possibly on the GPU) and
+    the optimizer state move to CPU now; lists / dicts are copied so training can go on."""
+    def copy(obj):
+        if isinstance(obj, TensorRef):
+            return TensorRef(obj.tensor.detach().to("cpu", copy=True))
+        if isinstance(obj, dict):
+            return {k: copy(v) for k, v in obj.items()}
+        if isinstance(obj, list):
+            return [copy(v) for v in obj]
+        return obj
+    opt = _to_cpu(optimizer_state) if optimizer_state is not None else None
+    if opt is not None:  # _to_cpu keeps host tensors shared: clone what training may update
+        opt = {k: ({i: {n: (t.clone() if isinstance(t, torch.Tensor) else t) for n, t in st.items()}
+                    for i, st in v.items()} if k == "state" else v) for k, v in opt.items()}
+    return copy(skeleton), opt
+
+
+def pending(model_id: str) -> bool:
+    with _inflight_lock:
+        t = _inflight.get(model_id)
+        return t is not None and t.is_alive()
+
+
+def wait_pending(model_id: str) -> None:
+    with _inflight_lock:
+        t = _inflight.get(model_id)
+    if t is not None:
+        t.join()
+
+
+def save_async(model_id: str, skeleton: dict, optimizer_state: dict | None) -> threading.Thread:
+    """Write a :func:`snapshot` on a background thread (JSON rendering of a large model takes
+    seconds; the training loop keeps running). One writer per model at a time."""
+    wait_pending(model_id)
+
+    def work():
+        try:
+            save(model_id, skeleton, optimizer_state)
+        except Exception:  # pragma: no cover - logged, the next checkpoint retries
+            log.exception(f"background checkpoint of model {model_id} failed")
+
+    t = threading.Thread(target=work, name=f"ckpt-{model_id}", daemon=True)
+    with _inflight_lock:
+        _inflight[model_id] = t
+    t.start()
+    return t
 
 
 def load(model_id: str) -> tuple[dict, dict | None]:

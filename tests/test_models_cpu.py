@@ -152,3 +152,28 @@ def test_batchnorm_eval_uses_running_stats():
 def test_relu_layer_gain_constants():
     assert ReluLayer.weight_gain == math.sqrt(2.0)
     assert TanhLayer.weight_gain == 5.0 / 3.0
+
+
+def test_background_checkpoint_matches_synchronous(models_tmpdir):
+    torch.manual_seed(5)
+    m = NeuralNetworkModel("bg", [6, 12, 3], activation_algos=["relu", "softmax"], optimizer_algo="adam")
+    data = [([float((i + j) % 4) for j in range(6)], [i % 3]) for i in range(m.training_buffer_size)]
+    m.train(data, epochs=2, batch_size=16)
+    m.serialize()
+    with open(ckpt.model_path("bg")) as f:
+        sync_text = f.read()
+    sync_opt = torch.load(ckpt.optimizer_path("bg"), weights_only=True)
+    assert m.serialize_background()
+    snap_params = [p.clone() for p in m.params]
+    with torch.no_grad():  # training continues while the snapshot is being written
+        for p in m.params:
+            p.add_(1.0)
+    ckpt.wait_pending("bg")
+    with open(ckpt.model_path("bg")) as f:
+        assert f.read() == sync_text
+    bg_opt = torch.load(ckpt.optimizer_path("bg"), weights_only=True)
+    for k, st in sync_opt["state"].items():
+        assert torch.equal(st["exp_avg"], bg_opt["state"][k]["exp_avg"])
+    loaded = NeuralNetworkModel.deserialize("bg")
+    for a, b in zip(loaded.params, snap_params):
+        assert torch.equal(a, b)
