@@ -5,6 +5,9 @@
 // allocator, RCCL collectives issued through torch.distributed, and hipGraph capture.
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
+#include <map>
+#include <mutex>
+
 #include <torch/library.h>
 
 #include <cstring>
@@ -124,6 +127,22 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   return p;
 }
 
+// per-tile split-K tickets: one zeroed device ring per GPU, handed out in chunks (the kernel's
+// last arriver resets its tiles' counters, so a chunk is clean again when its launch retires)
+int* split_counters(int tiles, const c10::Device& dev) {
+  static std::mutex mu;
+  static std::map<int, std::pair<at::Tensor, int64_t>> rings;
+  constexpr int64_t kCap = 1 << 16;
+  std::lock_guard<std::mutex> lock(mu);
+  auto& ring = rings[dev.index()];
+  if (!ring.first.defined()) ring.first = at::zeros({kCap}, at::TensorOptions().dtype(at::kInt).device(dev));
+  TORCH_CHECK(tiles <= kCap, "pz::gemm: too many split-K tiles");
+  if (ring.second + tiles > kCap) ring.second = 0;
+  int* ptr = ring.first.data_ptr<int>() + ring.second;
+  ring.second += tiles;
+  return ptr;
+}
+
 const float* f32_scalar_ptr(const optional<Tensor>& t, const char* what) {
   if (!t.has_value() || !t->defined()) return nullptr;
   TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() >= 1, "pz::gemm: ", what, " must be an fp32 device scalar");
@@ -156,6 +175,14 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
   }
   TORCH_CHECK((p.out8 == nullptr && p.in_dtype != pz::DT_FP8) || pz::gemm_path(p) == 1,
               "pz::gemm: fp8 operands / outputs need an MFMA-eligible shape");
+  at::Tensor ws;  // split-K slabs: from the caching allocator, stream-ordered reuse is safe
+  const int64_t ws_floats = pz::gemm_split_ws_floats(p);
+  if (ws_floats > 0) {
+    ws = at::empty({ws_floats}, A.options().dtype(at::kFloat));
+    p.split_k = pz::gemm_split(p);
+    p.ws = ws.data_ptr<float>();
+    p.counters = split_counters(static_cast<int>(((M + 255) / 256) * ((N + 255) / 256)), A.device());
+  }
   TORCH_CHECK(p.mask == nullptr || pz::gemm_path(p) == 1, "pz::gemm: a mask epilogue needs an MFMA-eligible shape");
   PZ_HIP_CHECK(pz::gemm(p, cur_stream(A)));
 }

@@ -253,10 +253,16 @@ PZ_DEV f32x4_t epi_apply(const GemmArgs& p, f32x4_t a, f32x4_t bias4, int m, int
   return f32x4_t{v[0], v[1], v[2], v[3]};
 }
 
-PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+// XCD-aware bijective remap of the launch order (consecutive ids share an XCD's L2), then
+// tile = id / split, slice = id % split (a tile's K slices stay on one XCD), then grouped
+// tile order for L2 reuse.
+PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int split, int& tm, int& tn, int& tile, int& slice) {
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  tile = wgid / split;
+  slice = wgid - tile * split;
+  wgid = tile;
   constexpr int GROUP = 8;
   const int per_group = GROUP * tiles_n;
   const int g = wgid / per_group;
@@ -277,8 +283,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 
   const int tiles_m = (p.M + BM - 1) / BM;
   const int tiles_n = (p.N + BN - 1) / BN;
-  int tm, tn;
-  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, tm, tn);
+  const int split = p.split_k > 1 ? p.split_k : 1;
+  int tm, tn, tile_id, slice;
+  tile_coords(tiles_m * tiles_n * split, tiles_m, tiles_n, split, tm, tn, tile_id, slice);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -361,6 +368,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     __builtin_amdgcn_sched_barrier(0);
   };
 
+  const int nk = p.K / (F8 ? 2 * kBK : kBK) / split;  // K steps of this slice
+  const int kt0 = slice * nk;
   constexpr bool BUF = VAR == 6;
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
@@ -370,13 +379,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   constexpr int GD = C::G;
   auto stage_a = [&](int kt) {
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
-    if constexpr (A_KC) stage_kc<BM, NWD, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
-    else stage_mn<BM, NWD, BUF>(A, lda, m0, p.M, kt * kBK, base, wave, lane, rs_a);
+    if constexpr (A_KC) stage_kc<BM, NWD, BUF>(A, lda, m0, p.M, (kt0 + kt) * kBK, base, wave, lane, rs_a);
+    else stage_mn<BM, NWD, BUF>(A, lda, m0, p.M, (kt0 + kt) * kBK, base, wave, lane, rs_a);
   };
   auto stage_b = [&](int kt) {
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (B_KC) stage_kc<BN, NWD, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
-    else stage_mn<BN, NWD, BUF>(B, ldb, n0, p.N, kt * kBK, base, wave, lane, rs_b);
+    if constexpr (B_KC) stage_kc<BN, NWD, BUF>(B, ldb, n0, p.N, (kt0 + kt) * kBK, base, wave, lane, rs_b);
+    else stage_mn<BN, NWD, BUF>(B, ldb, n0, p.N, (kt0 + kt) * kBK, base, wave, lane, rs_b);
   };
   auto stage = [&](int kt, int slot) {  // slot == kt % NS
     (void)slot;
@@ -384,7 +393,6 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     stage_b(kt);
   };
 
-  const int nk = p.K / (F8 ? 2 * kBK : kBK);
   constexpr int NS = C::NS;
   // Measured, not kept: staging K-contiguous operands in PAIRS of steps so both 64-B halves of
   // every 128-B line are requested back to back (halved L1->L2 requests, matched hipBLASLt's
@@ -445,6 +453,56 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     mfma_step(f);
   }
 
+  // ---------------------------------------------------------------- split-K reduction
+  // (guide "In-launch split-K reduction": plain slab stores, vmcnt(0), barrier, ONE agent-scope
+  // release + relaxed ticket; the last arriver acquires, sums the other slabs, runs the epilogue)
+  if (split > 1) {
+    constexpr int CH = F8 ? TM8 * TN8 * 4 : C::TM * C::TN;  // f32x4 chunks per lane
+    const int tid = threadIdx.x;
+    auto get_chunk = [&](auto cc) -> f32x4_t {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (F8) {
+        constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
+        return f32x4_t{acc[i][j][q], acc[i][j][q + 1], acc[i][j][q + 2], acc[i][j][q + 3]};
+      } else {
+        return acc[c / C::TN][c % C::TN];
+      }
+    };
+    auto add_chunk = [&](auto cc, f32x4_t v) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (F8) {
+        constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
+        acc[i][j][q] += v[0]; acc[i][j][q + 1] += v[1]; acc[i][j][q + 2] += v[2]; acc[i][j][q + 3] += v[3];
+      } else {
+        acc[c / C::TN][c % C::TN] += v;
+      }
+    };
+    f32x4_t* mine = reinterpret_cast<f32x4_t*>(p.ws + static_cast<int64_t>(tile_id * split + slice) * (BM * BN));
+    static_for<CH>([&](auto cc) { mine[decltype(cc)::value * C::NT + tid] = get_chunk(cc); });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    PZ_LDS int* flag = (PZ_LDS int*)(smem);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int prev = __hip_atomic_fetch_add(p.counters + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = prev == split - 1;
+    }
+    __syncthreads();
+    if (*flag == 0) return;  // block-uniform: another slice finishes this tile
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      p.counters[tile_id] = 0;  // ready for the next launch
+    }
+    __syncthreads();
+    for (int sl = 0; sl < split; ++sl) {
+      if (sl == slice) continue;
+      const f32x4_t* other = reinterpret_cast<const f32x4_t*>(p.ws + static_cast<int64_t>(tile_id * split + sl) * (BM * BN));
+      static_for<CH>([&](auto cc) { add_chunk(cc, other[decltype(cc)::value * C::NT + tid]); });
+    }
+  }
+
   // ---------------------------------------------------------------- epilogue
   // static_for (not #pragma unroll): the acc array must only ever be indexed by compile-time
   // constants or it is demoted to scratch (guide §5.4 rule 20)
@@ -495,7 +553,7 @@ hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const int nwg = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN) * (p.split_k > 1 ? p.split_k : 1);
   hipLaunchKernelGGL(kern, dim3(nwg), dim3(C::NT), C::LDS_BYTES, s, p);
   return hipGetLastError();
 }
@@ -516,6 +574,7 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     const char* e = getenv("PZ_GEMM_TILE");
     return e ? atoi(e) : 0;
   }();
+  if (p.split_k > 1) return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);  // slabs sized for 256x256
   switch (forced) {
     case 11: return launch_layout<256, 256, 2, 4, OutT, AuxT, 1>(p, s);
     case 12: return launch_layout<256, 256, 2, 4, OutT, AuxT, 2>(p, s);
@@ -535,7 +594,7 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
 
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  if (tiles >= 240) return launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
+  if (tiles >= 240 || p.split_k > 1) return launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
   return launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
 }
 
@@ -588,7 +647,31 @@ bool mfma_eligible(const GemmArgs& p) {
   return true;
 }
 
+int gemm_split(const GemmArgs& p) {
+  static const int mode = [] {  // PZ_SPLITK=0 disables split-K (experiments)
+    const char* e = getenv("PZ_SPLITK");
+    return e ? atoi(e) : 1;
+  }();
+  static const bool forced_tile = getenv("PZ_GEMM_TILE") != nullptr;
+  // fp8 skinny shapes run better as 128x128 tiles (measured: split-K 256x256 -4%)
+  if (mode == 0 || forced_tile || p.in_dtype == DT_FP8 || !mfma_eligible(p)) return 1;
+  const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  constexpr int kFill = 240;
+  if (tiles >= kFill) return 1;
+  const int nk = p.K / (p.in_dtype == DT_FP8 ? 64 : kBK);
+  for (int sp : {2, 4, 8})
+    if (tiles * sp >= kFill && nk % sp == 0 && nk / sp >= 16) return sp;
+  return 1;
+}
+
+int64_t gemm_split_ws_floats(const GemmArgs& p) {
+  const int sp = gemm_split(p);
+  if (sp <= 1) return 0;
+  return static_cast<int64_t>((p.M + 255) / 256) * ((p.N + 255) / 256) * sp * 256 * 256;
+}
+
 hipError_t gemm_mfma(const GemmArgs& p, hipStream_t s) {
+  if (p.split_k > 1 && (p.ws == nullptr || p.counters == nullptr)) return hipErrorInvalidValue;
   if (p.in_dtype == DT_FP8) return launch_fp8(p, s);
   if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);
   return launch_tiles<float, uint16_t>(p, s);

@@ -55,7 +55,17 @@ struct GemmArgs {
   int64_t ldout8;
   const float* out8_qscale;
   float* amax;
+  // split-K (set by the launcher, gemm_split()): K is cut into split_k slices computed by
+  // separate workgroups; every slice stores its fp32 partial tile into ws, and the LAST slice to
+  // arrive at a tile (per-tile counter) sums the others and runs the epilogue
+  int split_k;
+  float* ws;       // [tiles * split_k][BM * BN] fp32
+  int* counters;   // [tiles], zero; reset by the last arriver
 };
+
+// split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().
+int gemm_split(const GemmArgs& args);
+int64_t gemm_split_ws_floats(const GemmArgs& args);
 
 // returns hipSuccess or an error; chooses the MFMA path when the shape allows
 hipError_t gemm(const GemmArgs& args, hipStream_t stream);
