@@ -193,6 +193,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 #pragma unroll
   for (int j = 0; j < COLS; ++j) cs[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const uint64_t col0 = static_cast<uint64_t>(n0 + nl0);
+  const float bwd_scale = (e.drop_post ? e.scale : 1.f) * (e.drop_pre ? e.scale : 1.f);
   static_for<ROWS>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
     const int ml = ml0 + L::MSTEP * i;
@@ -207,10 +208,15 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
         if (e.act != ACT_NONE) act_fwd_row<COLS>(v, e.act);
         if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
       }
+    } else if (use_mask) {
+      // ReLU stage: y > 0  <=>  kept by drop_post AND kept by drop_pre AND z > 0, so the whole
+      // derivative chain is one bit times the dropout scales — no hashes in the backward
+      act_bwd_mask_row<L>(v, mbits[i], nlane);
+#pragma unroll
+      for (int j = 0; j < COLS; ++j) v[j] *= bwd_scale;
     } else {
       if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
-      if (use_mask) act_bwd_mask_row<L>(v, mbits[i], nlane);
-      else if (e.act != ACT_NONE) act_bwd_row<BN, L>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
+      if (e.act != ACT_NONE) act_bwd_row<BN, L>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
       if (e.drop_pre) dropout_row<L>(v, e, e.key_pre, pr_row);
     }
 #pragma unroll

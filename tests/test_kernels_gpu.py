@@ -115,7 +115,7 @@ def test_gemm_backward_epilogue_and_colsum(native_lib, act):
 
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (8192 + 64, 1024 + 64, 256), (256, 4096, 64)])
 def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
-    """EPI_FWD writes bit(y > 0); EPI_BWD reading those bits == EPI_BWD reading y (bit-identical)."""
+    """EPI_FWD writes bit(y > 0); EPI_BWD reading those bits == EPI_BWD reading y."""
     p, seed = 0.2, (5, 11)
     x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     w = (torch.randn(K, N, device=DEV) / 8).to(torch.bfloat16)
@@ -135,8 +135,9 @@ def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
     cs_bit = torch.zeros(N, device=DEV)
     PF.gemm(gz, True, wt, True, out_aux, aux=y, colsum=cs_aux, mode=PF.EPI_BWD, epi=epi)
     PF.gemm(gz, True, wt, True, out_bit, colsum=cs_bit, mode=PF.EPI_BWD, epi=epi, mask=mask)
-    assert torch.equal(out_aux, out_bit)
-    torch.testing.assert_close(cs_aux, cs_bit, rtol=1e-5, atol=1e-3)
+    # the bit path folds both dropout scales into one multiply: equal up to one bf16 rounding
+    torch.testing.assert_close(out_bit.float(), out_aux.float(), rtol=8e-3, atol=1e-6)
+    torch.testing.assert_close(cs_aux, cs_bit, rtol=1e-4, atol=1e-3)
     ref = (gz.double() @ wt.double().t()) * (y.double() > 0)
     m1 = torch.from_numpy(keep_mask(M * N, *seed, 3, p).reshape(M, N)).to(DEV)
     ref = ref * m1 / (1 - p) * (torch.from_numpy(keep_mask(M * N, *seed, 4, p).reshape(M, N)).to(DEV) / (1 - p))
