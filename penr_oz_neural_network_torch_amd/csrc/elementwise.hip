@@ -360,6 +360,48 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(GatherArgs a) {
   }
 }
 
+// vectorised bf16-output gather (fp32 or bf16 table): one wave per row, 8 elements (one 16-B
+// store) per lane-iteration; the sampled index is hashed once per row by lane 0
+template <typename Tin>
+__global__ void __launch_bounds__(256) gather_rows_vec_kernel(GatherArgs a) {
+  const Tin* __restrict__ src = static_cast<const Tin*>(a.data);
+  uint16_t* __restrict__ dst = static_cast<uint16_t*>(a.out);
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= a.rows) return;
+  int64_t pick = 0;
+  const bool valid = row < a.rows_valid;
+  if (valid) {
+    if (a.indices != nullptr) {
+      pick = a.indices[row];
+    } else {
+      const uint32_t h = mix32(mix32(static_cast<uint32_t>(row) ^ a.seed_lo) ^ a.seed_hi);
+      pick = static_cast<int64_t>((static_cast<uint64_t>(h) * static_cast<uint64_t>(a.n_data)) >> 32);
+    }
+    if (lane == 0) {
+      if (a.picked != nullptr) a.picked[row] = pick;
+      if (a.labels_out != nullptr) a.labels_out[row] = a.labels_in[pick];
+    }
+  } else if (lane == 0 && a.labels_out != nullptr) {
+    a.labels_out[row] = 0;
+  }
+  const Tin* s = src + pick * a.ld_data;
+  uint16_t* d = dst + static_cast<int64_t>(row) * a.ld_out;
+  for (int c = lane * 8; c < a.cols; c += 64 * 8) {
+    uint4 o = make_uint4(0, 0, 0, 0);
+    if (valid) {
+      if constexpr (sizeof(Tin) == 4) {
+        const float4 x0 = *reinterpret_cast<const float4*>(s + c);
+        const float4 x1 = *reinterpret_cast<const float4*>(s + c + 4);
+        o = make_uint4(pack_bf2(x0.x, x0.y), pack_bf2(x0.z, x0.w), pack_bf2(x1.x, x1.y), pack_bf2(x1.z, x1.w));
+      } else {
+        o = *reinterpret_cast<const uint4*>(s + c);
+      }
+    }
+    *reinterpret_cast<uint4*>(d + c) = o;
+  }
+}
+
 }  // namespace
 
 #define PZ_DISPATCH_FLOAT(dt, T, ...)                       \
@@ -480,6 +522,16 @@ hipError_t colsum(const void* x, int dtype, float* out, int rows, int cols, hipS
 
 hipError_t gather_rows(const GatherArgs& a, hipStream_t s) {
   if (a.rows <= 0) return hipSuccess;
+  const bool vec = a.out_dtype == DT_BF16 && (a.data_dtype == DT_F32 || a.data_dtype == DT_BF16) && a.cols % 8 == 0 &&
+                   a.ld_data % 8 == 0 && a.ld_out % 8 == 0 && (reinterpret_cast<uintptr_t>(a.data) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+  if (vec) {
+    if (a.data_dtype == DT_F32)
+      hipLaunchKernelGGL(gather_rows_vec_kernel<float>, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
+    else
+      hipLaunchKernelGGL(gather_rows_vec_kernel<uint16_t>, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   PZ_DISPATCH_FLOAT(a.data_dtype, Tin, PZ_DISPATCH_FLOAT(a.out_dtype, Tout, {
     hipLaunchKernelGGL((gather_rows_kernel<Tin, Tout>), dim3(a.rows), dim3(256), 0, s, a);
   }));

@@ -236,7 +236,7 @@ class FusedTrainer:
         else:
             x = torch.tensor(inputs, dtype=torch.float32).reshape(len(inputs), -1)
             self.block = 1
-        self.data = x.to(self.dev).contiguous()
+        self.data = self._table(x)
         if self.head == "softmax":
             self.labels = torch.tensor([int(t[0]) for t in targets], dtype=torch.int64, device=self.dev)
             self.targets = None
@@ -247,13 +247,20 @@ class FusedTrainer:
         self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
         self._rows = None
 
+    def _table(self, x: torch.Tensor) -> torch.Tensor:
+        """Device-resident dataset. Dense inputs are kept in the GEMM operand dtype (the gather
+        would round them to it anyway): half the bytes per sampled row for bf16 models."""
+        if self.stages[0].kind != "embed" and self.compute == torch.bfloat16:
+            return x.to(device=self.dev, dtype=torch.bfloat16).contiguous()
+        return x.to(self.dev).contiguous()
+
     def load_tensors(self, inputs: torch.Tensor, targets: torch.Tensor, seed: int | None = None) -> None:
         """Fast path for benchmarks / programmatic use: a dataset already held as tensors.
 
         ``inputs``: ``[N, in]`` (or ``[N, T]`` token ids); ``targets``: ``[N]`` class labels for a
         softmax head, ``[N, out]`` regression targets otherwise.
         """
-        self.data = inputs.to(device=self.dev, dtype=torch.float32).contiguous()
+        self.data = self._table(inputs.to(dtype=torch.float32))
         self.block = self.data.shape[1] if self.stages[0].kind == "embed" else 1
         if self.head == "softmax":
             self.labels = targets.reshape(-1).to(device=self.dev, dtype=torch.int64).contiguous()
