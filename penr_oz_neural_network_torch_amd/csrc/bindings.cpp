@@ -322,9 +322,11 @@ void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t
 
 // ------------------------------------------------------------------------------- optimizer
 Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::IntArrayRef is_weight,
-                        at::IntArrayRef stat_slot, at::ArrayRef<optional<Tensor>> shadows) {
+                        at::IntArrayRef stat_slot, at::ArrayRef<optional<Tensor>> shadows,
+                        at::ArrayRef<optional<Tensor>> grads16) {
   const size_t n = offsets.size();
-  TORCH_CHECK(numels.size() == n && is_weight.size() == n && stat_slot.size() == n && shadows.size() == n,
+  TORCH_CHECK(numels.size() == n && is_weight.size() == n && stat_slot.size() == n && shadows.size() == n &&
+                  (grads16.empty() || grads16.size() == n),
               "pz::pack_segments: length mismatch");
   Tensor out = at::empty({static_cast<int64_t>(n * sizeof(pz::OptSegment))}, at::TensorOptions().dtype(at::kByte));
   auto* segs = reinterpret_cast<pz::OptSegment*>(out.data_ptr<uint8_t>());
@@ -339,6 +341,12 @@ Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::Int
       TORCH_CHECK(sh->is_contiguous() && sh->numel() == numels[i], "pz::pack_segments: shadow shape");
       s.shadow = sh->data_ptr();
       s.shadow_dtype = dt_of(*sh);
+    }
+    if (!grads16.empty() && grads16[i].has_value() && grads16[i]->defined()) {
+      const Tensor& g = *grads16[i];
+      TORCH_CHECK(g.is_contiguous() && g.numel() == numels[i] && g.scalar_type() == at::kBFloat16,
+                  "pz::pack_segments: bf16 gradient shape");
+      s.grad16 = reinterpret_cast<const uint16_t*>(g.data_ptr());
     }
     std::memcpy(segs + i, &s, sizeof(s));
   }
@@ -576,7 +584,8 @@ TORCH_LIBRARY(pz, m) {
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()");
   m.def("gather_rows(Tensor data, Tensor? indices, int seed_lo, int seed_hi, Tensor(a!) out, int rows_valid, "
         "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked) -> ()");
-  m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows) -> Tensor");
+  m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows, "
+        "Tensor?[] grads16) -> Tensor");
   m.def("optimizer_step(Tensor(a!) params, Tensor grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
         "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
         "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats) -> ()");

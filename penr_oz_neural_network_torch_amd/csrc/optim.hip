@@ -61,7 +61,8 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(const OptArgs a) {
     if (li >= seg.numel) break;
     const int64_t gi = seg.offset + li;
     const float p0 = a.params[gi];
-    const float g = a.grads[gi] * a.grad_scale + l2x2 * p0;
+    const float graw = seg.grad16 != nullptr ? bf2f(seg.grad16[li]) : a.grads[gi];
+    const float g = graw * a.grad_scale + l2x2 * p0;
     float p1;
     if constexpr (ADAM) {
       float m = a.exp_avg[gi];

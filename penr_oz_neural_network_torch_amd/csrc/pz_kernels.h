@@ -76,6 +76,8 @@ struct OptSegment {
   int stat_slot;        // index into stats (4 doubles per slot), -1 = none
   void* shadow;         // optional low-precision copy written after the update
   int shadow_dtype;
+  const uint16_t* grad16;  // optional bf16 gradient of this segment (data parallel: the GEMM
+                           // writes it and RCCL reduces it in bf16); replaces grads[offset..]
 };
 
 struct OptArgs {

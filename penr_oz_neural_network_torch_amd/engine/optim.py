@@ -24,10 +24,14 @@ ELEMS_PER_BLOCK = 4096  # keep in sync with kOptElemsPerBlock (csrc/pz_kernels.h
 
 class FusedOptimizer:
     def __init__(self, store: ParamStore, params: list[torch.Tensor], torch_opt: torch.optim.Optimizer | None,
-                 shadows: dict[int, torch.Tensor] | list[dict[int, torch.Tensor]]):
+                 shadows: dict[int, torch.Tensor] | list[dict[int, torch.Tensor]],
+                 grads16: dict[int, torch.Tensor] | None = None):
         # shadows: low-precision weight copies the update writes; a LIST of dicts = ping-pong sets
         # selected per launch by `parity` (the trainer reads one set while the other is written)
+        # grads16: segment offset -> bf16 gradient view that replaces the fp32 gradient of that
+        # segment (data parallel: dense weight gradients are produced and all-reduced in bf16)
         shadow_sets = shadows if isinstance(shadows, list) else [shadows]
+        self.grads16 = grads16 or {}
         self.store = store
         self.params = params
         self.torch_opt = torch_opt
@@ -52,7 +56,8 @@ class FusedOptimizer:
         self.total_blocks = acc
         self.segments_p = [torch.ops.pz.pack_segments(
             [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
-            [slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs]).to(dev) for sh in shadow_sets]
+            [slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
+            [self.grads16.get(s.offset) for s in segs]).to(dev) for sh in shadow_sets]
         self.segments = self.segments_p[0]
         self.block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
         self.num_segments = len(segs)
@@ -85,7 +90,8 @@ class FusedOptimizer:
             for parity, sh in enumerate(self.shadow_sets):
                 packed = torch.ops.pz.pack_segments(
                     [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
-                    [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs]).to(dev)
+                    [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
+                    [self.grads16.get(s.offset) for s in segs]).to(dev)
                 self.groups[(key, parity)] = (packed, block_seg, len(segs), acc)
 
     # ------------------------------------------------------------------------------------

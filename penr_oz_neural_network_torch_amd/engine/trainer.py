@@ -10,7 +10,7 @@ HIP kernels with nothing on the host between epochs:
     per stage:  GEMM(+bias+dropout+act+dropout epilogue) | batchnorm(+epilogue) | flatten(+dropout)
     head:       xent_head / mse_head  (loss + dZ of the last stage + its bias-grad colsum)
     per stage, reversed:
-                dW GEMM  (XᵀdZ, fp32 straight into the flat grad buffer)
+                dW GEMM  (XᵀdZ straight into the flat grad buffer: fp32; bf16 under data parallel)
                 -> async RCCL all-reduce of that bucket (data parallel)
                 dX GEMM  (dZ Wᵀ with the previous stage's epilogue derivative + bias colsum fused)
                 | batchnorm_bwd | embedding_bwd
@@ -178,7 +178,18 @@ class FusedTrainer:
             if st.kind == "gemm" and self.compute != torch.float32:
                 for sset in self.shadow_sets:
                     sset[st.seg_w.offset] = torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute)
-        self.opt = FusedOptimizer(self.store, model.params, model.optimizer, self.shadow_sets)
+        # Data parallel: dense weight gradients are written by the dW GEMMs straight in bf16 and
+        # all-reduced in bf16 (half the xGMI bytes of fp32 — rings over xGMI are per-link bound,
+        # SURVEY §5.8); the fused optimizer reads them back as fp32. Biases, BN, embeddings and
+        # the loss stay in the exact fp32 bucket. PZ_GRAD_COMM_DTYPE=fp32 keeps fp32 gradients.
+        self.grads16: dict[int, torch.Tensor] = {}
+        policy = os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower()
+        if self.ctx.world_size > 1 and self.compute == torch.bfloat16 and policy in ("bf16", "bfloat16"):
+            buf16 = torch.zeros(max(1, self.store.accum_offset), device=self.dev, dtype=torch.bfloat16)
+            for st in self.stages:
+                if st.kind == "gemm":
+                    self.grads16[st.seg_w.offset] = self.store.view(st.seg_w, buf16)
+        self.opt = FusedOptimizer(self.store, model.params, model.optimizer, self.shadow_sets, self.grads16)
         self.ctx.broadcast_(self.store.flat)  # identical replicas (rank 0 wins)
         for sset in self.shadow_sets:
             for sh_off, sh in sset.items():
@@ -407,6 +418,11 @@ class FusedTrainer:
                            drop_pre=st.drop_pre if "pre" in parts else -1,
                            drop_post=st.drop_post if "post" in parts else -1, p=p, seed=seed)
 
+    def _w_grad(self, seg) -> torch.Tensor:
+        """Gradient buffer of a weight segment: the bf16 DP view or the fp32 flat gradient."""
+        g16 = self.grads16.get(seg.offset)
+        return g16 if g16 is not None else self.store.view(seg, self.grads)
+
     def _w(self, st: Stage) -> torch.Tensor:
         """GEMM operand for the stage's weight: bf16 shadow or the fp32 master view, [in, out]."""
         sh = self.shadow_sets[self.parity].get(st.seg_w.offset)
@@ -487,7 +503,7 @@ class FusedTrainer:
 
         # ---------------- reduce + update
         self._phase("pz.update")
-        handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:]))
+        handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:], exact=True))
         if overlap:
             late = list(self._late_handles)
             self._opt_async("rest", late + [handles[-1]], self._late_stages)
@@ -671,7 +687,7 @@ class FusedTrainer:
                 rec[("grad", before.layers[-1])] = dx[:batch * st.pos_in]
             return dx, False
         # GEMM stage: dW = x_inᵀ · dZ
-        w_grad = self.store.view(st.seg_w, self.grads)
+        w_grad = self._w_grad(st.seg_w)
         PF.gemm(x_in, False, g, False, w_grad)
         handles.append(self.ctx.all_reduce_async(w_grad))
         # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
@@ -754,7 +770,7 @@ class FusedTrainer:
             if seg is None:
                 wgrads.append(None)
                 continue
-            gview = self.store.view(seg, self.grads) / world
+            gview = self._w_grad(seg).float() / world
             wgrads.append(gview + (2.0 * l2) * self.store.view(seg))
         self._record = {"activations": acts, "act_grads": grads, "weight_grads": wgrads}
 

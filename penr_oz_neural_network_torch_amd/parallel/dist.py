@@ -37,10 +37,12 @@ class DataParallelContext:
     def enabled(self) -> bool:
         return self.world_size > 1
 
-    def all_reduce_async(self, t: torch.Tensor):
+    def all_reduce_async(self, t: torch.Tensor, exact: bool = False):
+        """Start a SUM all-reduce of ``t`` in place. ``exact``: never through ``comm_dtype``
+        (buckets that carry the loss or small accumulated parameters)."""
         if not self.enabled or t.numel() == 0:
             return None
-        if self.comm_dtype is not None and t.dtype != self.comm_dtype:
+        if not exact and self.comm_dtype is not None and t.dtype != self.comm_dtype:
             low = t.to(self.comm_dtype)
             work = dist.all_reduce(low, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
             return (work, low, t)

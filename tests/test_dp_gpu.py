@@ -34,19 +34,22 @@ def _data():
     return x, y, idx
 
 
-def _build(optimizer):
+def _build(optimizer, comm):
     from penr_oz_neural_network_torch_amd.models import NeuralNetworkModel
     torch.manual_seed(0)
-    return NeuralNetworkModel("dp", SIZES, "xavier", "random", ALGOS, optimizer, dtype="float32", device="cuda:0")
+    dtype = "float32" if comm == "fp32" else "bfloat16"  # bf16 gradient buckets need a bf16-compute model
+    return NeuralNetworkModel("dp", SIZES, "xavier", "random", ALGOS, optimizer, dtype=dtype, device="cuda:0")
 
 
-def _rank_main(rank, world, port, optimizer, out_path):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+def _rank_main(rank, world, port, optimizer, comm, out_path):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      PZ_GRAD_COMM_DTYPE=comm)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
-    model = _build(optimizer)
+    model = _build(optimizer, comm)
     tr = FusedTrainer(model, DataParallelContext(rank, world))
+    assert bool(tr.grads16) == (comm == "bf16")
     x, y, idx = _data()
     tr.load_tensors(x, y, seed=3)
     tr.begin(2)
@@ -59,14 +62,17 @@ def _rank_main(rank, world, port, optimizer, out_path):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
 @pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
-def test_two_rank_step_equals_single_rank(tmp_path, optimizer):
+def test_two_rank_step_equals_single_rank(tmp_path, optimizer, comm):
+    """fp32 gradient buckets reproduce the single-rank step to fp32 rounding; bf16 buckets (the
+    default under DP for bf16 models: dW GEMMs write bf16, RCCL reduces bf16) to bf16 rounding."""
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_rank_main, args=(2, _free_port(), optimizer, out), nprocs=2, start_method="spawn")
+    mp.start_processes(_rank_main, args=(2, _free_port(), optimizer, comm, out), nprocs=2, start_method="spawn")
     dp = torch.load(out, weights_only=True)
 
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
-    model = _build(optimizer)
+    model = _build(optimizer, comm)
     tr = FusedTrainer(model)
     x, y, idx = _data()
     tr.load_tensors(x, y, seed=3)
@@ -74,11 +80,12 @@ def test_two_rank_step_equals_single_rank(tmp_path, optimizer):
     for e in range(2):
         tr.step(e, 0.01, 2 * B, 0.0, 1e-3, want_ratios=True, record=False, indices=idx)
     costs = [c for _, c, _, _ in tr.drain()]
+    ctol = 1e-5 if comm == "fp32" else 2e-3
     for a, b in zip(dp["costs"], costs):
-        assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (dp["costs"], costs)
+        assert abs(a - b) < ctol * max(1.0, abs(b)), (dp["costs"], costs)
     d = (dp["flat"] - model._param_store.flat.cpu()).abs()
     if optimizer == "adam":  # sign-noise flips of ~lr on near-zero gradients are legitimate
-        assert (d > 1e-3).double().mean().item() < 1e-3
-        assert d.mean().item() < 1e-5
+        assert (d > 1e-3).double().mean().item() < (1e-3 if comm == "fp32" else 2e-2)
+        assert d.mean().item() < (1e-5 if comm == "fp32" else 2e-4)
     else:
-        assert d.max().item() < 1e-6, d.max().item()
+        assert d.max().item() < (1e-6 if comm == "fp32" else 1e-4), d.max().item()
