@@ -88,10 +88,12 @@ def main(argv=None) -> int:
     labels = torch.randint(0, cfg["sizes"][-1], (n_data,), generator=g)
     trainer.load_tensors(inputs, labels, seed=7 + rank)
     total = args.warmup + args.steps
-    trainer.begin(total)
-    every = max(1, total // 100)
     global_batch = batch * world
     lr0, decay = 1e-3, 0.999
+    # the schedule lets the trainer tabulate per-epoch hyper-parameters and replay captured
+    # hipGraphs of the step (single GPU); steps are launched eagerly under data parallelism
+    trainer.begin(total, lr_schedule=lambda e: lr0 * decay ** e)
+    every = max(1, total // 100)
 
     def run(epoch: int) -> None:
         trainer.step(epoch, lr0 * decay ** epoch, global_batch, args.dropout, args.l2,

@@ -67,6 +67,7 @@ __global__ void bn_finalize_kernel(const double* partial, int n, int cols, P* ru
 
 template <typename T, typename P>
 __global__ void __launch_bounds__(256) bn_normalize_kernel(BnArgs a) {
+  a.epi = epi_resolve(a.epi);
   const T* __restrict__ x = static_cast<const T*>(a.x);
   T* __restrict__ y = static_cast<T*>(a.y);
   const P* gain = static_cast<const P*>(a.gain);
@@ -88,6 +89,7 @@ __global__ void __launch_bounds__(256) bn_normalize_kernel(BnArgs a) {
 // backward reductions: sum(dyn), sum(dyn * xhat) with dyn = epi_bwd(g, y)
 template <typename T>
 __global__ void __launch_bounds__(256) bn_bwd_sums_kernel(BnBwdArgs a) {
+  a.epi = epi_resolve(a.epi);
   const T* __restrict__ g = static_cast<const T*>(a.g);
   const T* __restrict__ y = static_cast<const T*>(a.y);
   const T* __restrict__ x = static_cast<const T*>(a.x);
@@ -125,6 +127,7 @@ __global__ void bn_param_grads_kernel(const double* partial, int cols, P* dgain,
 
 template <typename T, typename P>
 __global__ void __launch_bounds__(256) bn_dx_kernel(BnBwdArgs a) {
+  a.epi = epi_resolve(a.epi);
   const T* __restrict__ g = static_cast<const T*>(a.g);
   const T* __restrict__ y = static_cast<const T*>(a.y);
   const T* __restrict__ x = static_cast<const T*>(a.x);

@@ -49,6 +49,13 @@ T* ptr_or_null(const optional<Tensor>& t) {
   return t.has_value() && t->defined() ? static_cast<T*>(t->data_ptr()) : nullptr;
 }
 
+// device epoch counter of graph-replayed steps: one int32 on the GPU
+const int* epoch_counter(const optional<Tensor>& t) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kInt && t->numel() >= 1, "pz: epoch counter must be a GPU int32");
+  return t->data_ptr<int>();
+}
+
 pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
   pz::EpiSpec e{};
   e.act = pz::ACT_NONE;
@@ -63,6 +70,9 @@ pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
     e.thresh16 = static_cast<uint32_t>(ei[5]);
     e.drop_all = static_cast<int>(ei[6]);
   }
+  // [7]: device address of an int32 epoch counter (graph-captured steps), 0 = keys are final.
+  // Internal API: the trainer passes counter.data_ptr() of a tensor it owns for the graph's life.
+  if (ei.size() >= 8 && ei[7] != 0) e.epoch_ptr = reinterpret_cast<const int*>(static_cast<uintptr_t>(ei[7]));
   if (ef.size() >= 2) {
     e.scale = static_cast<float>(ef[0]);
     e.inv_scale = static_cast<float>(ef[1]);
@@ -296,7 +306,8 @@ void colsum_op(const Tensor& x, const Tensor& out) {
 
 void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t seed_lo, int64_t seed_hi,
                     const Tensor& out, int64_t rows_valid, const optional<Tensor>& labels_in,
-                    const optional<Tensor>& labels_out, const optional<Tensor>& picked) {
+                    const optional<Tensor>& labels_out, const optional<Tensor>& picked,
+                    const optional<Tensor>& epoch) {
   check_dev(data, "data");
   TORCH_CHECK(data.dim() == 2 && out.dim() == 2 && data.stride(1) == 1 && out.stride(1) == 1, "pz::gather_rows: 2-D");
   TORCH_CHECK(out.size(1) == data.size(1), "pz::gather_rows: width mismatch");
@@ -317,6 +328,7 @@ void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t
   a.labels_in = ptr_or_null<const int64_t>(labels_in);
   a.labels_out = ptr_or_null<int64_t>(labels_out);
   a.picked = ptr_or_null<int64_t>(picked);
+  a.epoch_ptr = epoch_counter(epoch);
   PZ_HIP_CHECK(pz::gather_rows(a, cur_stream(data)));
 }
 
@@ -357,7 +369,7 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
                        const optional<Tensor>& exp_avg_sq, const Tensor& segments, const Tensor& block_seg,
                        int64_t num_segments, int64_t total_blocks, bool adam, double lr, double beta1, double beta2,
                        double eps, double bias_c1, double bias_c2_sqrt, double grad_scale, double l2,
-                       const optional<Tensor>& stats) {
+                       const optional<Tensor>& stats, const optional<Tensor>& hp, const optional<Tensor>& epoch) {
   check_dev(params, "params");
   TORCH_CHECK(params.scalar_type() == at::kFloat && grads.scalar_type() == at::kFloat, "pz::optimizer_step: fp32 master");
   pz::OptArgs a{};
@@ -380,6 +392,12 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
   a.grad_scale = static_cast<float>(grad_scale);
   a.l2_lambda = static_cast<float>(l2);
   a.stats = ptr_or_null<double>(stats);
+  if (hp.has_value() && hp->defined()) {
+    TORCH_CHECK(hp->scalar_type() == at::kFloat && hp->is_contiguous() && hp->is_cuda(), "pz::optimizer_step: hp table");
+    TORCH_CHECK(epoch.has_value(), "pz::optimizer_step: an hp table needs the epoch counter");
+    a.hp = hp->data_ptr<float>();
+    a.epoch_ptr = epoch_counter(epoch);
+  }
   PZ_HIP_CHECK(pz::optimizer_step(a, cur_stream(params)));
 }
 
@@ -536,10 +554,13 @@ void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, cons
 
 void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tensor& stats_prev, const Tensor& stats_cur,
                       const Tensor& slot_numel, int64_t nslots, double l2, const Tensor& costs, int64_t epoch,
-                      const Tensor& ratios, int64_t ratio_row) {
+                      const Tensor& ratios, int64_t ratio_row, const optional<Tensor>& epoch_ctr, int64_t every) {
   check_dev(costs, "costs");
-  TORCH_CHECK(epoch >= 0 && epoch < costs.numel(), "pz::step_finalize: epoch out of range");
+  const bool dev_epoch = epoch < 0;  // read from the counter (graph-replayed step)
+  TORCH_CHECK(!dev_epoch || epoch_ctr.has_value(), "pz::step_finalize: epoch < 0 needs the epoch counter");
+  TORCH_CHECK(dev_epoch || epoch < costs.numel(), "pz::step_finalize: epoch out of range");
   TORCH_CHECK(ratio_row < 0 || (ratio_row + 1) * nslots <= ratios.numel(), "pz::step_finalize: ratio row out of range");
+  TORCH_CHECK(ratio_row != -2 || every >= 1, "pz::step_finalize: ratio rule needs every >= 1");
   pz::FinalizeArgs a{};
   a.loss = ptr_or_null<const float>(loss);
   a.loss_div = static_cast<float>(loss_div);
@@ -552,6 +573,10 @@ void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tenso
   a.epoch = static_cast<int>(epoch);
   a.ratios = ratios.data_ptr<float>();
   a.ratio_row = static_cast<int>(ratio_row);
+  a.every = static_cast<int>(every);
+  a.n_costs = static_cast<int>(costs.numel());
+  a.n_ratio_rows = static_cast<int>(ratios.numel() / (nslots > 0 ? nslots : 1));
+  a.epoch_ptr = const_cast<int*>(epoch_counter(epoch_ctr));
   PZ_HIP_CHECK(pz::step_finalize(a, cur_stream(costs)));
 }
 
@@ -583,12 +608,13 @@ TORCH_LIBRARY(pz, m) {
   m.def("softmax_bwd(Tensor g, Tensor y, Tensor(a!) dx) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()");
   m.def("gather_rows(Tensor data, Tensor? indices, int seed_lo, int seed_hi, Tensor(a!) out, int rows_valid, "
-        "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked) -> ()");
+        "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked, Tensor? epoch=None) -> ()");
   m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows, "
         "Tensor?[] grads16) -> Tensor");
   m.def("optimizer_step(Tensor(a!) params, Tensor grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
         "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
-        "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats) -> ()");
+        "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats, Tensor? hp=None, "
+        "Tensor? epoch=None) -> ()");
   m.def("segment_stats(Tensor params, Tensor segments, Tensor block_seg, int num_segments, int total_blocks, "
         "Tensor(a!) stats) -> ()");
   m.def("tensor_moments(Tensor x, int row_len, int rule, float thr, Tensor(a!) out) -> ()");
@@ -602,7 +628,8 @@ TORCH_LIBRARY(pz, m) {
   m.def("embedding_fwd(Tensor table, Tensor idx, Tensor(a!) out) -> ()");
   m.def("embedding_bwd(Tensor dout, Tensor idx, Tensor(a!) dtable) -> ()");
   m.def("step_finalize(Tensor? loss, float loss_div, Tensor(a!) stats_prev, Tensor stats_cur, Tensor slot_numel, "
-        "int nslots, float l2, Tensor(b!) costs, int epoch, Tensor(c!) ratios, int ratio_row) -> ()");
+        "int nslots, float l2, Tensor(b!) costs, int epoch, Tensor(c!) ratios, int ratio_row, "
+        "Tensor(d!)? epoch_ctr=None, int every=1) -> ()");
   m.def("amax_abs(Tensor x, Tensor(a!) amax) -> ()");
   m.def("scale_update(Tensor(a!) amax, Tensor(b!) qs, float headroom, bool reset) -> ()");
   m.def("quant_transpose(Tensor w, Tensor(a!) out, Tensor qs) -> ()");

@@ -25,6 +25,7 @@ template <> PZ_DEV void std_<uint16_t>(uint16_t* p, int64_t i, double v) { p[i] 
 template <typename Tin, typename Tout, typename F>
 __global__ void __launch_bounds__(256) stage_fwd_kernel(const Tin* __restrict__ x, Tout* __restrict__ y,
                                                         int64_t n, EpiSpec e) {
+  e = epi_resolve(e);
   for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
     const F v = static_cast<F>(ldd<Tin>(x, i));
     std_<Tout>(y, i, static_cast<double>(epi_fwd<F>(v, static_cast<uint64_t>(i), e)));
@@ -35,6 +36,7 @@ __global__ void __launch_bounds__(256) stage_fwd_kernel(const Tin* __restrict__ 
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) stage_bwd_kernel(const T* __restrict__ g, const T* __restrict__ y,
                                                         T* __restrict__ dx, int64_t n, EpiSpec e) {
+  e = epi_resolve(e);
   for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
     const F gv = static_cast<F>(ldd<T>(g, i));
     const F yv = static_cast<F>(ldd<T>(y, i));
@@ -70,6 +72,7 @@ PZ_DEV void block_colsum_flush(float* colsum, const float* cs, int cols) {
 
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
+  a.epi = epi_resolve(a.epi);
   extern __shared__ float cs_lds[];  // [cols] when a.colsum (LDS column partials)
   __shared__ float red[4];
   const T* __restrict__ logits = static_cast<const T*>(a.logits);
@@ -125,6 +128,7 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
 // reduced across the block's waves through LDS once (no LDS atomics: they made this 60 us).
 template <int NCH>
 __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
+  a.epi = epi_resolve(a.epi);
   extern __shared__ float cs_lds[];  // [4][cols] wave partials (when colsum)
   __shared__ float red[4];
   constexpr int RPW = kHeadRows / 4;
@@ -239,6 +243,7 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
 // ---------------------------------------------------------------------------------------------
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) mse_head_kernel(MseArgs a) {
+  a.epi = epi_resolve(a.epi);
   extern __shared__ float cs_lds[];
   __shared__ float red[4];
   const T* __restrict__ y = static_cast<const T*>(a.y);
@@ -334,6 +339,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, fl
 // ---------------------------------------------------------------------------------------------
 template <typename Tin, typename Tout>
 __global__ void __launch_bounds__(256) gather_rows_kernel(GatherArgs a) {
+  if (a.epoch_ptr != nullptr) gather_seed(a.seed_lo, a.seed_hi, static_cast<uint32_t>(*a.epoch_ptr));
   const Tin* __restrict__ src = static_cast<const Tin*>(a.data);
   Tout* __restrict__ dst = static_cast<Tout*>(a.out);
   const int row = blockIdx.x;
@@ -364,6 +370,7 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(GatherArgs a) {
 // store) per lane-iteration; the sampled index is hashed once per row by lane 0
 template <typename Tin>
 __global__ void __launch_bounds__(256) gather_rows_vec_kernel(GatherArgs a) {
+  if (a.epoch_ptr != nullptr) gather_seed(a.seed_lo, a.seed_hi, static_cast<uint32_t>(*a.epoch_ptr));
   const Tin* __restrict__ src = static_cast<const Tin*>(a.data);
   uint16_t* __restrict__ dst = static_cast<uint16_t*>(a.out);
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);

@@ -144,7 +144,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   const int tid = threadIdx.x;
   const int my_row = tid / CHUNKS_PER_ROW, my_chunk = tid % CHUNKS_PER_ROW;
   const bool bwd = !FWD_ONLY && p.epi_mode == EPI_BWD;  // FWD_ONLY: no colsum / backward code
-  const EpiSpec& e = p.epi;
+  const EpiSpec e = epi_resolve(p.epi);  // graph-replayed steps: epoch from the device counter
   const int ml0 = wm * WTM + L::m_lane(lane);  // + MSTEP*i
   const int nlane = L::n_lane(lane);
   const int nl0 = wn * WTN + nlane;            // + n_off(j)

@@ -26,6 +26,7 @@ constexpr int GK = 16;
 
 template <typename T, typename Acc, typename OutT, typename AuxT>
 __global__ void __launch_bounds__(256) gemm_generic_kernel(const GemmArgs p) {
+  const EpiSpec epi = epi_resolve(p.epi);
   __shared__ Acc As[GK][GT + 1];
   __shared__ Acc Bs[GK][GT + 1];
   const T* __restrict__ A = static_cast<const T*>(p.A);
@@ -86,10 +87,10 @@ __global__ void __launch_bounds__(256) gemm_generic_kernel(const GemmArgs p) {
       const uint64_t idx = static_cast<uint64_t>(m) * static_cast<uint64_t>(p.idx_ld) + n;
       if (p.epi_mode == EPI_BWD) {
         const Acc y = ld<AuxT, Acc>(aux, int64_t(m) * p.ldaux + n);
-        v = epi_bwd<Acc>(v, y, idx, p.epi);
+        v = epi_bwd<Acc>(v, y, idx, epi);
       } else {
         if (p.bias != nullptr) v += static_cast<Acc>(p.bias[n]);
-        if (p.epi_mode == EPI_FWD) v = epi_fwd<Acc>(v, idx, p.epi);
+        if (p.epi_mode == EPI_FWD) v = epi_fwd<Acc>(v, idx, epi);
       }
       const int64_t off = int64_t(m) * p.ldc + n;
       if (p.accumulate) v += ld<OutT, Acc>(Cp, off);

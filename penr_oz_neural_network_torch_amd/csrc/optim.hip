@@ -46,7 +46,13 @@ PZ_DEV void block_reduce_add(double v[4], double* dst) {
 }
 
 template <bool ADAM>
-__global__ void __launch_bounds__(kThreads) optimizer_kernel(const OptArgs a) {
+__global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
+  if (a.hp != nullptr) {
+    const float* h = a.hp + 4 * static_cast<int64_t>(*a.epoch_ptr);
+    a.lr = h[0];
+    a.bias_c1 = h[1];
+    a.bias_c2_sqrt = h[2];
+  }
   const int seg_id = find_segment(a.block_seg, a.num_segments, blockIdx.x);
   const OptSegment seg = a.segments[seg_id];
   const int64_t local0 = (static_cast<int64_t>(blockIdx.x) - a.block_seg[seg_id]) * kOptElemsPerBlock;
@@ -114,8 +120,12 @@ PZ_DEV double std_from_sums(double s, double ss, double n) {
 
 // cost[e] = loss / world + l2 * sum_w ||w||^2 (weights in use during the step)
 // ratios[row][slot] = std(w_new - w_old) / (std(w_new) + 1e-8)       (progress points only)
-__global__ void step_finalize_kernel(const FinalizeArgs a) {
+__global__ void step_finalize_kernel(FinalizeArgs a) {
   __shared__ double l2sum;
+  if (a.epoch < 0) a.epoch = *a.epoch_ptr;
+  if (a.ratio_row == -2) a.ratio_row = a.epoch % a.every == 0 ? a.epoch / a.every : -1;
+  if (a.ratio_row >= a.n_ratio_rows) a.ratio_row = -1;
+  __syncthreads();  // every thread has read the counter before thread 0 advances it below
   if (threadIdx.x == 0) l2sum = 0.0;
   __syncthreads();
   for (int k = threadIdx.x; k < a.nslots; k += blockDim.x) {
@@ -131,7 +141,8 @@ __global__ void step_finalize_kernel(const FinalizeArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const double loss = a.loss != nullptr ? static_cast<double>(*a.loss) / a.loss_div : 0.0;
-    a.costs[a.epoch] = static_cast<float>(loss + static_cast<double>(a.l2) * l2sum);
+    if (a.epoch < a.n_costs) a.costs[a.epoch] = static_cast<float>(loss + static_cast<double>(a.l2) * l2sum);
+    if (a.epoch_ptr != nullptr) *a.epoch_ptr = a.epoch + 1;
   }
   __syncthreads();
   // the previous stats buffer becomes the next step's accumulation target

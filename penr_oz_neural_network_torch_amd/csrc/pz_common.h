@@ -56,6 +56,13 @@ PZ_DEV uint32_t mix32(uint32_t x) {  // "lowbias32" integer finaliser
   x ^= x >> 16;
   return x;
 }
+// per-epoch key of a (seed, layer) key; mirrored on the host by ops/functional.py: epoch_key
+PZ_DEV uint32_t epoch_key(uint32_t key, uint32_t epoch) { return mix32(key ^ mix32(epoch * 0x9E3779B1u + 0x7F4A7C15u)); }
+// per-epoch minibatch seeds; mirrored on the host by engine/trainer.py: FusedTrainer._gather_seed
+PZ_DEV void gather_seed(uint32_t& lo, uint32_t& hi, uint32_t epoch) {
+  lo += epoch * 0x632BE5ABu;
+  hi ^= epoch;
+}
 // 32 random bits shared by the element pair (2j, 2j+1); each element uses 16 of them
 PZ_DEV uint32_t pair_bits(uint32_t pair, uint32_t key) { return mix32(pair ^ key); }
 PZ_DEV bool keep_elem(uint64_t idx, uint32_t key, uint32_t thresh16) {
@@ -90,6 +97,17 @@ PZ_DEV F act_grad_from_out(F a, int act) {
     case ACT_TANH: return F(1) - a * a;
     default: return F(1);
   }
+}
+
+// make a (possibly graph-replayed) spec concrete: mix the device epoch counter into the keys
+PZ_DEV EpiSpec epi_resolve(EpiSpec e) {
+  if (e.epoch_ptr != nullptr) {
+    const uint32_t ep = static_cast<uint32_t>(*e.epoch_ptr);
+    e.key_pre = epoch_key(e.key_pre, ep);
+    e.key_post = epoch_key(e.key_post, ep);
+    e.epoch_ptr = nullptr;
+  }
+  return e;
 }
 
 PZ_DEV bool epi_keep(const EpiSpec& e, uint32_t key, uint64_t idx) {

@@ -56,7 +56,9 @@ struct GatherArgs {
   const int64_t* labels_in;  // optional [n_data]
   int64_t* labels_out;       // optional [rows]
   int64_t* picked;           // optional [rows]: chosen data index per row
+  const int* epoch_ptr;      // graph-replayed steps: seeds += epoch (gather_seed), read on device
 };
+
 
 hipError_t stage_fwd(const void* x, int x_dtype, void* y, int y_dtype, int64_t n, const EpiSpec& e, hipStream_t s);
 hipError_t stage_bwd(const void* g, const void* y, void* dx, int dtype, int64_t n, const EpiSpec& e, hipStream_t s);
@@ -96,6 +98,10 @@ struct OptArgs {
   float grad_scale;            // e.g. 1 / world_size
   float l2_lambda;             // grad += 2*l2*w for weight segments
   double* stats;               // per slot: sum(dw), sum(dw^2), sum(w), sum(w^2)  (accumulated)
+  // graph-replayed steps: {lr, bias_c1, bias_c2_sqrt, -} of epoch *epoch_ptr from this table
+  // (filled on the host for the whole run, so eager and replayed steps use identical values)
+  const float* hp;
+  const int* epoch_ptr;
 };
 
 constexpr int kOptElemsPerBlock = 4096;
@@ -115,7 +121,11 @@ struct FinalizeArgs {
   float* costs;             // costs[epoch]
   int epoch;
   float* ratios;            // [rows][nslots]
-  int ratio_row;            // -1: no progress point this epoch
+  int ratio_row;            // -1: no progress point this epoch; -2: epoch % every == 0 ? epoch / every : -1
+  int every;
+  int n_costs;              // costs[] length (device-read epochs are bounds-checked)
+  int n_ratio_rows;
+  int* epoch_ptr;           // device epoch counter: read when epoch < 0, always advanced to epoch + 1
 };
 hipError_t step_finalize(const FinalizeArgs& a, hipStream_t s);
 

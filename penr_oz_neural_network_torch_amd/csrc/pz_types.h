@@ -22,6 +22,10 @@ struct EpiSpec {
   float scale;        // 1 / (1 - p)
   float inv_scale;    // (1 - p)
   int drop_all;       // p >= 1: every element is dropped
+  // Graph-replayed steps: keys above are per (seed, layer) only and the kernel mixes in the
+  // epoch read from this device counter (epoch_key). nullptr: the keys are final (eager steps
+  // mix the epoch on the host with the same function, so both paths draw identical masks).
+  const int* epoch_ptr;
 };
 
 }  // namespace pz

@@ -70,6 +70,9 @@ class FusedOptimizer:
         self.shadow_sets = shadow_sets
         self.slot_of = slot_of
         self.groups: dict = {}
+        # (hp table, epoch counter) while a hipGraph is being captured: the kernels then read the
+        # epoch's lr / bias corrections from the table instead of the baked-in scalars
+        self.graph_tables = None
 
     def define_groups(self, keys: list[int]) -> None:
         """Split the update into launches: one per listed segment offset (a dense weight whose
@@ -159,13 +162,16 @@ class FusedOptimizer:
 
     def _launch(self, grads, segments, block_seg, nseg, nblocks, l2: float, grad_scale: float) -> None:
         lr, b1, b2, eps, bc1, bc2s = self._hp
+        hp, ctr = self.graph_tables or (None, None)
         torch.ops.pz.optimizer_step(self.store.flat, grads, self.exp_avg, self.exp_avg_sq, segments, block_seg, nseg,
                                     nblocks, self.adam, lr, b1, b2, eps, bc1, bc2s, grad_scale, l2,
-                                    self.stats[self.cur])
+                                    self.stats[self.cur], hp, ctr)
 
     def finalize(self, loss: torch.Tensor | None, world: int, l2: float, costs: torch.Tensor, epoch: int,
-                 ratios: torch.Tensor, ratio_row: int) -> None:
+                 ratios: torch.Tensor, ratio_row: int, epoch_ctr: torch.Tensor | None = None, every: int = 1) -> None:
+        """cost[epoch] and the update-ratio row; ``epoch=-1`` / ``ratio_row=-2``: taken from the
+        device ``epoch_ctr`` (graph-replayed step), which is advanced to epoch + 1 either way."""
         prev = self.stats[1 - self.cur]
         torch.ops.pz.step_finalize(loss, float(world), prev, self.stats[self.cur], self.slot_numel, self.nslots, l2,
-                                   costs, epoch, ratios, ratio_row)
+                                   costs, epoch, ratios, ratio_row, epoch_ctr, every)
         self.cur = 1 - self.cur

@@ -43,6 +43,12 @@ from ..parallel.dist import DataParallelContext, get_context
 from .optim import FusedOptimizer
 
 ROW_PAD = 64  # batch rows padded to the GEMM K-tile so dW = XᵀdZ stays on the MFMA path
+_M32 = 0xFFFFFFFF
+# Steps below this are launch-bound (measured on MI355X: [4,8,2] at batch 32 runs 0.093 ms/step
+# replayed vs 0.172 eager; [256,1024,1024,64] at batch 1024 (8 GFLOP) is already GPU-bound and
+# replays 5 % slower, as does the 1.2 TFLOP bench step: ROCm executes the captured side-stream
+# branch with less overlap than eager streams)
+GRAPH_MAX_FLOP = 4e9
 
 # Tracing / debugging: PZ_TRACE=1 brackets every step phase in a roctx range
 # (visible with `rocprofv3 --marker-trace`); PZ_DEBUG_SYNC=1 synchronises after every phase so an
@@ -226,6 +232,19 @@ class FusedTrainer:
         self._opt_done = None
         self._ov = None
         self._rows = None
+        # hipGraph replay of whole steps (single GPU) when a step is launch-bound: PZ_GRAPHS=auto
+        # (default: steps under GRAPH_MAX_FLOP), 1 (always), 0 (never)
+        mode = os.environ.get("PZ_GRAPHS", "auto")
+        self.use_graphs = mode != "0"
+        self._graphs_forced = mode == "1"
+        self._dense_params = sum(st.seg_w.numel for st in self.stages if st.kind == "gemm")
+        self.epoch_ctr = torch.zeros(1, device=self.dev, dtype=torch.int32)
+        self._ctr_epoch = 0
+        self._plan = None
+        self._graphs: dict = {}
+        self._warm: set = set()
+        self._graph_pool = None
+        self._last_event = None
         self._pending: list = []   # (epoch, ratio_row or None, event)
         self._drained = 0
         self._record = None
@@ -257,6 +276,7 @@ class FusedTrainer:
         seed = torch.randint(0, 2 ** 62, (1,)).item()
         self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
         self._rows = None
+        self._invalidate_graphs()
 
     def _table(self, x: torch.Tensor) -> torch.Tensor:
         """Device-resident dataset. Dense inputs are kept in the GEMM operand dtype (the gather
@@ -282,12 +302,14 @@ class FusedTrainer:
         seed = torch.randint(0, 2 ** 62, (1,)).item() if seed is None else seed
         self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
         self._rows = None
+        self._invalidate_graphs()
 
     def _ensure_buffers(self, batch: int) -> None:
         rows_b = _round_up(batch, ROW_PAD)
         if self._rows == (batch, rows_b):
             return
         self._rows = (batch, rows_b)
+        self._invalidate_graphs()  # captured steps point at the old buffers
         dev, cd = self.dev, self.compute
         pos = self.block
         self.x_in = torch.empty(rows_b, self.data.shape[1], device=dev, dtype=torch.float32 if
@@ -408,15 +430,28 @@ class FusedTrainer:
                                              device=self.dev, dtype=torch.uint8)
 
     # ------------------------------------------------------------------------------------
-    def _seed(self, epoch: int) -> tuple[int, int]:
-        lo = (self.base_seed[0] ^ (epoch * 0x9E3779B1)) & 0xFFFFFFFF
-        hi = (self.base_seed[1] + epoch * 0x85EBCA6B + self.ctx.rank * 0xC2B2AE35) & 0xFFFFFFFF
+    def _keys(self, epoch: int | None) -> tuple:
+        """Dropout key context of one step: ``(seed_lo, seed_hi, epoch, epoch_ptr)``. Eager steps
+        mix the epoch into the keys on the host; graph-captured steps (``epoch=None``) pass the
+        device epoch counter and the kernels mix it in with the same function."""
+        lo = self.base_seed[0] & _M32
+        hi = (self.base_seed[1] + self.ctx.rank * 0xC2B2AE35) & _M32
+        return (lo, hi, epoch, 0) if epoch is not None else (lo, hi, None, self.epoch_ctr.data_ptr())
+
+    def _gather_seed(self, epoch: int | None) -> tuple[int, int]:
+        """Minibatch sampler seeds (host mirror of the kernels' ``gather_seed``)."""
+        lo = self.base_seed[0] & _M32
+        hi = (self.base_seed[1] ^ (self.ctx.rank * 0x27D4EB2F)) & _M32
+        if epoch is not None:
+            lo = (lo + epoch * 0x632BE5AB) & _M32
+            hi ^= epoch & _M32
         return lo, hi
 
-    def _epi(self, st: Stage, p: float, seed, parts=("pre", "act", "post")):
+    def _epi(self, st: Stage, p: float, keys, parts=("pre", "act", "post")):
         return PF.epi_spec(act=st.act if "act" in parts else PF.ACT_NONE,
                            drop_pre=st.drop_pre if "pre" in parts else -1,
-                           drop_post=st.drop_post if "post" in parts else -1, p=p, seed=seed)
+                           drop_post=st.drop_post if "post" in parts else -1, p=p, seed=keys[:2], epoch=keys[2],
+                           epoch_ptr=keys[3])
 
     def _w_grad(self, seg) -> torch.Tensor:
         """Gradient buffer of a weight segment: the bf16 DP view or the fp32 flat gradient."""
@@ -431,20 +466,117 @@ class FusedTrainer:
     # ------------------------------------------------------------------------------------
     # one epoch
     # ------------------------------------------------------------------------------------
-    def begin(self, epochs: int) -> None:
-        """Size the device-side progress arrays for a ``train()`` call of ``epochs`` epochs."""
+    def begin(self, epochs: int, lr_schedule=None) -> None:
+        """Size the device-side progress arrays for a ``train()`` call of ``epochs`` epochs.
+
+        ``lr_schedule(epoch) -> lr`` (the learning rate :meth:`step` will be called with) enables
+        hipGraph replay: the per-epoch optimizer hyper-parameters are tabulated on the device
+        once, so a captured step needs nothing from the host but a replay."""
         self._alloc_progress(epochs)
+        self._invalidate_graphs()
+        self._plan = None
+        if lr_schedule is None or not self._graphs_possible():
+            return
+        every = max(1, epochs // 100)
+        t0 = self.opt.step_count
+        lrs = [float(lr_schedule(e)) for e in range(epochs)]
+        rows = []
+        for e, lr in enumerate(lrs):
+            if self.opt.adam:
+                b1, b2 = self.opt.torch_opt.param_groups[0]["betas"]
+                t = t0 + e + 1
+                rows.append((lr, 1.0 - b1 ** t, math.sqrt(1.0 - b2 ** t), 0.0))
+            else:
+                rows.append((lr, 1.0, 1.0, 0.0))
+        self._plan = {"epochs": epochs, "every": every, "t0": t0, "lrs": lrs,
+                      "hp": torch.tensor(rows or [(0.0, 1.0, 1.0, 0.0)], dtype=torch.float32, device=self.dev)}
+
+    def _graphs_possible(self) -> bool:
+        # single GPU only (collectives are not captured); no per-phase host syncs (PZ_DEBUG_SYNC)
+        return self.use_graphs and self.overlap and self.ctx.world_size == 1 and not _DEBUG_SYNC
+
+    def _launch_bound(self, batch: int) -> bool:
+        """Replay pays where the host's ~0.17 ms of per-step launches exceeds the GPU time."""
+        return self._graphs_forced or 6.0 * self._dense_params * batch < GRAPH_MAX_FLOP
+
+    def _invalidate_graphs(self) -> None:
+        self._graphs = {}
+        self._warm = set()
 
     def step(self, epoch: int, lr: float, sample_size: int, dropout: float, l2: float, want_ratios: bool,
              record: bool, indices: torch.Tensor | None = None) -> None:
         """One training epoch. ``indices`` (int64, this rank's ``batch`` rows) overrides the
-        on-device sampler — used by the data-parallel equivalence tests."""
+        on-device sampler — used by the data-parallel equivalence tests.
+
+        After :meth:`begin` with an ``lr_schedule``, plain (non-record) steps are captured once per
+        weight-shadow parity into a hipGraph and replayed: the epoch-dependent values (dropout
+        keys, sampler seeds, optimizer hyper-parameters, cost slot, ratio row) are then read from
+        the device epoch counter, which every step advances in ``step_finalize``."""
         world = self.ctx.world_size
         batch = max(1, sample_size // world) if world > 1 else sample_size
         self._ensure_buffers(batch)
         if not hasattr(self, "costs") or epoch >= self.costs.numel():
             self._alloc_progress(epoch + 1)
-        seed = self._seed(epoch)
+            self._invalidate_graphs()
+            self._plan = None
+        plan = self._plan
+        row = None
+        if want_ratios:
+            if plan is not None:
+                row = epoch // plan["every"]
+            else:
+                row = self._ratio_rows
+                self._ratio_rows += 1
+        graphable = (plan is not None and not record and indices is None and self._launch_bound(batch)
+                     and epoch < plan["epochs"]
+                     and want_ratios == (epoch % plan["every"] == 0) and lr == plan["lrs"][epoch]
+                     and self.opt.step_count == plan["t0"] + epoch)
+        gkey = (self.parity, batch, float(dropout), float(l2))
+        if graphable and gkey in self._warm:
+            self._replay(gkey, epoch, lr, batch, dropout, l2, row)
+        else:
+            self._run(epoch, lr, batch, dropout, l2, -1 if row is None else row, record, indices)
+            self._pending.append((epoch, row, self._last_event))
+            if graphable:
+                self._warm.add(gkey)
+        self._ctr_epoch = epoch + 1
+
+    def _replay(self, gkey, epoch: int, lr: float, batch: int, dropout: float, l2: float, row) -> None:
+        main = torch.cuda.current_stream(self.dev)
+        if self._opt_done is not None:
+            main.wait_event(self._opt_done)
+            self._opt_done = None
+        if self._ctr_epoch != epoch:
+            self.epoch_ctr.fill_(epoch)
+        parity = self.parity
+        graph = self._graphs.get(gkey)
+        if graph is not None:
+            self.opt.cur = 1 - self.opt.cur  # what the captured finalize did when it was recorded
+        else:
+            graph = torch.cuda.CUDAGraph()
+            self.opt.graph_tables = (self._plan["hp"], self.epoch_ctr)
+            try:
+                with torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
+                    self._run(None, lr, batch, dropout, l2, -2, False, None)
+            finally:
+                self.opt.graph_tables = None
+            self._graph_pool = graph.pool()
+            self._graphs[gkey] = graph
+            self.parity = parity  # capture does not execute: the replay below runs this epoch
+        self.opt.begin_step(lr)  # host bookkeeping only (step counter, param_group lr)
+        graph.replay()
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record(main)
+        self.parity = 1 - parity
+        self._pending.append((epoch, row, ev))
+
+    def _run(self, epoch: int | None, lr: float, batch: int, dropout: float, l2: float, row: int, record: bool,
+             indices: torch.Tensor | None) -> None:
+        """Enqueue one step. ``epoch=None``: hipGraph capture (epoch-dependent values from the
+        device counter / tables; the side stream joins the capture stream at the end)."""
+        world = self.ctx.world_size
+        capture = epoch is None
+        keys = self._keys(epoch)
         ops = torch.ops.pz
         main = torch.cuda.current_stream(self.dev)
         if self._opt_done is not None:  # the previous step's side-stream updates
@@ -452,7 +584,8 @@ class FusedTrainer:
             self._opt_done = None
         overlap = self.overlap and not record
         if overlap:
-            self.opt.begin_step(lr)
+            if not capture:
+                self.opt.begin_step(lr)
             self._ov = (main, l2, 1.0 / world)
             self._late_stages, self._late_handles = [], []
 
@@ -461,14 +594,14 @@ class FusedTrainer:
 
         # ---------------- sample + input
         self._phase("pz.sample")
-        gseed = ((self.base_seed[0] + epoch * 0x632BE5AB) & 0xFFFFFFFF,
-                 (self.base_seed[1] ^ (self.ctx.rank * 0x27D4EB2F + epoch)) & 0xFFFFFFFF)
+        gseed = self._gather_seed(epoch)
         idx = None
         if indices is not None:
             idx = indices.to(device=self.dev, dtype=torch.int64).contiguous()
             if idx.numel() < batch:
                 raise ValueError(f"need {batch} indices, got {idx.numel()}")
-        ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked)
+        ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
+                        self.epoch_ctr if capture else None)
         if self.tgt is not None:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
@@ -481,7 +614,7 @@ class FusedTrainer:
         x = self.x_in
         prev = None
         for st in self.stages:
-            x = self._forward_stage(st, x, batch, dropout, seed, rec)
+            x = self._forward_stage(st, x, batch, dropout, keys, rec)
             prev = st
         last = prev
         if self.fp8 and not record:  # this step's activation amax -> next step's scales
@@ -489,7 +622,7 @@ class FusedTrainer:
 
         # ---------------- head
         self._phase("pz.head")
-        g_pre = self._head(last, x, batch, dropout, seed, rec)
+        g_pre = self._head(last, x, batch, dropout, keys, rec)
 
         # ---------------- backward
         self._phase("pz.backward")
@@ -499,26 +632,27 @@ class FusedTrainer:
             st = self.stages[si]
             before = self.stages[si - 1] if si > 0 else None
             x_in = before.buffers["y"] if before is not None else self.x_in
-            g, g_pre = self._backward_stage(st, before, x_in, g, g_pre, batch, dropout, seed, rec, handles)
+            g, g_pre = self._backward_stage(st, before, x_in, g, g_pre, batch, dropout, keys, rec, handles)
 
         # ---------------- reduce + update
         self._phase("pz.update")
         handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:], exact=True))
+        fin = dict(epoch_ctr=self.epoch_ctr, every=self._plan["every"] if self._plan else 1)
         if overlap:
             late = list(self._late_handles)
             self._opt_async("rest", late + [handles[-1]], self._late_stages)
             self._ov = None
-            row = -1
-            if want_ratios:
-                row = self._ratio_rows
-                self._ratio_rows += 1
             with torch.cuda.stream(self.opt_stream):
-                self.opt.finalize(self.loss_slot, world, l2, self.costs, epoch, self.ratios, row)
-                ev = torch.cuda.Event(enable_timing=True)
+                self.opt.finalize(self.loss_slot, world, l2, self.costs, -1 if capture else epoch, self.ratios, row,
+                                  **fin)
+                ev = torch.cuda.Event(enable_timing=not capture)
                 ev.record(self.opt_stream)
-            self._opt_done = ev
+            if capture:  # join the side stream into the capture stream
+                main.wait_event(ev)
+            else:
+                self._opt_done = ev
+                self._last_event = ev
             self.parity = 1 - self.parity
-            self._pending.append((epoch, row if want_ratios else None, ev))
             self._phase(None)
             return
         self.ctx.wait_all(handles)
@@ -528,14 +662,10 @@ class FusedTrainer:
         self.parity = 1 - self.parity
         if self.fp8:
             self._refresh_fp8_weights()
-        row = -1
-        if want_ratios:
-            row = self._ratio_rows
-            self._ratio_rows += 1
-        self.opt.finalize(self.loss_slot, world, l2, self.costs, epoch, self.ratios, row)
+        self.opt.finalize(self.loss_slot, world, l2, self.costs, epoch, self.ratios, row, **fin)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        self._pending.append((epoch, row if want_ratios else None, ev))
+        self._last_event = ev
         self._phase(None)
 
     _in_phase = False
@@ -552,7 +682,7 @@ class FusedTrainer:
             torch.cuda.synchronize(self.dev)
 
     # ------------------------------------------------------------------------------------
-    def _forward_stage(self, st: Stage, x, batch, p, seed, rec):
+    def _forward_stage(self, st: Stage, x, batch, p, keys, rec):
         ops = torch.ops.pz
         y = st.buffers["y"]
         rows_valid = batch * st.pos_out
@@ -565,7 +695,7 @@ class FusedTrainer:
         if st.kind == "flatten":
             src = x.view(y.shape)
             if st.drop_pre >= 0:
-                ei, ef = self._epi(st, p, seed)
+                ei, ef = self._epi(st, p, keys)
                 ops.stage_fwd(src, y, ei, ef)
             else:
                 y.copy_(src)
@@ -573,7 +703,7 @@ class FusedTrainer:
                 rec[st.first] = y[:rows_valid]
             return y
         if rec is None:
-            ei, ef = self._epi(st, p, seed)
+            ei, ef = self._epi(st, p, keys)
             if st.kind == "gemm":
                 bias = self.store.view(st.seg_b) if st.seg_b is not None else None
                 kw = {}
@@ -602,10 +732,10 @@ class FusedTrainer:
         else:
             self._bn_fwd(st, x, z, batch, *none)
         out_first = self._scratch(("o", st.first), y)
-        ops.stage_fwd(z, out_first, *self._epi(st, p, seed, parts=("pre",)))
+        ops.stage_fwd(z, out_first, *self._epi(st, p, keys, parts=("pre",)))
         rec[st.first] = out_first[:rows_valid]
         if st.act_layer >= 0:
-            ops.stage_fwd(out_first, y, *self._epi(st, p, seed, parts=("act", "post")))
+            ops.stage_fwd(out_first, y, *self._epi(st, p, keys, parts=("act", "post")))
             rec[st.act_layer] = y[:rows_valid]
         else:
             y.copy_(out_first)
@@ -629,14 +759,14 @@ class FusedTrainer:
         return t
 
     # ------------------------------------------------------------------------------------
-    def _head(self, last: Stage, y, batch, p, seed, rec) -> bool:
+    def _head(self, last: Stage, y, batch, p, keys, rec) -> bool:
         """Loss + gradient of the last stage. Returns True when the gradient is wrt the
         producing op (epilogue derivative already applied), False when wrt the stage output."""
         ops = torch.ops.pz
         g = last.buffers["g"]
         fuse = rec is None and last.kind == "gemm"
         bias_grad = self.store.view(last.seg_b, self.grads) if (last.seg_b is not None and last.kind == "gemm") else None
-        ei, ef = self._epi(last, p, seed) if fuse else PF.epi_spec()
+        ei, ef = self._epi(last, p, keys) if fuse else PF.epi_spec()
         n = self.model.layers
         if self.head == "softmax":
             probs = self._scratch(("probs",), y) if rec is not None else None
@@ -653,7 +783,7 @@ class FusedTrainer:
                 rec[("grad", len(n) - 1)] = g[:batch]
         return fuse
 
-    def _backward_stage(self, st: Stage, before: Stage | None, x_in, g, g_pre: bool, batch, p, seed, rec, handles):
+    def _backward_stage(self, st: Stage, before: Stage | None, x_in, g, g_pre: bool, batch, p, keys, rec, handles):
         """Consume the gradient of stage `st`; return (gradient for `before`, is_pre flag)."""
         ops = torch.ops.pz
         rows_valid = batch * st.pos_out
@@ -663,7 +793,7 @@ class FusedTrainer:
             return None, True
         # bring g to the producing op (dZ)
         if not g_pre:
-            g = self._apply_epi_bwd(st, g, batch, p, seed, rec)
+            g = self._apply_epi_bwd(st, g, batch, p, keys, rec)
             if st.kind == "gemm" and st.seg_b is not None:
                 ops.colsum(g[:rows_valid], self.store.view(st.seg_b, self.grads))
         if st.kind == "flatten":
@@ -699,19 +829,19 @@ class FusedTrainer:
             self._late_handles.append(handles[-1])
         if self._ov is not None and own and early:
             self._opt_async(st.seg_w.offset, [handles[-1]], [st])
-        out = self._backward_dx(st, before, g, batch, p, seed, rec)
+        out = self._backward_dx(st, before, g, batch, p, keys, rec)
         if self._ov is not None and own and not early:
             self._opt_async(st.seg_w.offset, [handles[-1]], [st])
         return out
 
-    def _backward_dx(self, st: Stage, before: Stage | None, g, batch, p, seed, rec):
+    def _backward_dx(self, st: Stage, before: Stage | None, g, batch, p, keys, rec):
         if before is None:
             return None, True
         # dX = dZ · Wᵀ (+ previous stage's epilogue derivative and bias colsum when fusable)
         dx = before.buffers["g"]
         fuse_prev = rec is None and before.kind in ("gemm", "bn", "flatten") and before.has_epi
         if fuse_prev:
-            ei, ef = self._epi(before, p, seed)
+            ei, ef = self._epi(before, p, keys)
             colsum = self.store.view(before.seg_b, self.grads) if (before.kind == "gemm" and before.seg_b is not None) \
                 else None
             mask = before.buffers.get("mask")
@@ -729,25 +859,25 @@ class FusedTrainer:
             return dx, True
         return dx, False
 
-    def _apply_epi_bwd(self, st: Stage, g, batch, p, seed, rec):
+    def _apply_epi_bwd(self, st: Stage, g, batch, p, keys, rec):
         """dY (wrt stage output) -> dZ (wrt producing op); record mode keeps the per-layer grads."""
         ops = torch.ops.pz
         if not st.has_epi:
             return g
         if rec is None:
             dz = self._scratch(("dz", st.first), g)
-            ops.stage_bwd(g, st.buffers["y"], dz, *self._epi(st, p, seed))
+            ops.stage_bwd(g, st.buffers["y"], dz, *self._epi(st, p, keys))
             return dz
         # record: y_act = stage output; out_first = output of the first layer of the stage
         out_first = self._scratch(("o", st.first), g)
         if st.act_layer >= 0:
             g_first = self._scratch(("go", st.first), g)
-            ops.stage_bwd(g, st.buffers["y"], g_first, *self._epi(st, p, seed, parts=("act", "post")))
+            ops.stage_bwd(g, st.buffers["y"], g_first, *self._epi(st, p, keys, parts=("act", "post")))
             rec[("grad", st.first)] = g_first[:batch * st.pos_out]
         else:
             g_first = g
         dz = self._scratch(("dz", st.first), g)
-        ops.stage_bwd(g_first, out_first, dz, *self._epi(st, p, seed, parts=("pre",)))
+        ops.stage_bwd(g_first, out_first, dz, *self._epi(st, p, keys, parts=("pre",)))
         return dz
 
     # ------------------------------------------------------------------------------------

@@ -382,7 +382,7 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         """Same schedule as :meth:`_train_autograd`, enqueued on the GPU without host syncs;
         costs / ratios / timestamps come back in :meth:`FusedTrainer.drain`."""
         trainer.load_data(data)
-        trainer.begin(epochs)
+        trainer.begin(epochs, lr_schedule=lambda e: learning_rate * decay_rate ** e)
         every = max(1, epochs // MAX_PROGRESS_POINTS)
         last_saved = time.time()
         for epoch in range(epochs):

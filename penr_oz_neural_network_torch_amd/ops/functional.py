@@ -49,13 +49,23 @@ def layer_key(seed: tuple[int, int], lid: int) -> int:
     return mix32((seed[0] & _M32) ^ mix32((seed[1] + 0x9E3779B9 * (lid + 1)) & _M32))
 
 
+def epoch_key(key: int, epoch: int) -> int:
+    """Per-epoch variant of a (seed, layer) key — the kernels' ``epoch_key`` (pz_common.h)."""
+    return mix32((key & _M32) ^ mix32((epoch * 0x9E3779B1 + 0x7F4A7C15) & _M32))
+
+
 def epi_spec(act: int = ACT_NONE, drop_pre: int = -1, drop_post: int = -1, p: float = 0.0,
-             seed: tuple[int, int] = (0, 0)) -> tuple[list[int], list[float]]:
+             seed: tuple[int, int] = (0, 0), epoch: int | None = None,
+             epoch_ptr: int = 0) -> tuple[list[int], list[float]]:
     """Pack a stage epilogue ``drop_post(act(drop_pre(x)))`` for the kernels.
 
     ``drop_pre`` / ``drop_post`` are the reference layer indices whose dropout is applied (-1 =
     none). Dropout keeps an element iff its 16-bit counter-hash draw is ``>= round(p * 65536)``;
     kept elements are scaled by ``1/(1-p)`` like ``torch.nn.functional.dropout``.
+
+    Training steps vary the masks per epoch: eagerly launched steps pass ``epoch`` (mixed in
+    here), graph-replayed steps pass ``epoch_ptr`` = the device address of the trainer's int32
+    epoch counter, and the kernels mix ``*epoch_ptr`` in with the same function.
     """
     if p <= 0.0:
         drop_pre = drop_post = -1
@@ -65,7 +75,11 @@ def epi_spec(act: int = ACT_NONE, drop_pre: int = -1, drop_post: int = -1, p: fl
     inv_scale = 1.0 - p
     kpre = layer_key(seed, drop_pre) if drop_pre >= 0 else 0
     kpost = layer_key(seed, drop_post) if drop_post >= 0 else 0
-    return [act, int(drop_pre >= 0), int(drop_post >= 0), kpre, kpost, thresh, drop_all], [scale, inv_scale]
+    if epoch is not None:
+        kpre = epoch_key(kpre, epoch) if drop_pre >= 0 else 0
+        kpost = epoch_key(kpost, epoch) if drop_post >= 0 else 0
+    return ([act, int(drop_pre >= 0), int(drop_post >= 0), kpre, kpost, thresh, drop_all, int(epoch_ptr)],
+            [scale, inv_scale])
 
 
 def new_seed() -> tuple[int, int]:

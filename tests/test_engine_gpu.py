@@ -191,3 +191,45 @@ def test_fp8_training_tracks_bf16():
     assert f8[-1] < f8[0] - 0.05  # it learns
     for a, b in zip(bf, f8):
         assert abs(a - b) < 0.05 * abs(a) + 0.02, (bf, f8)
+
+
+@pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
+def test_graph_replay_matches_eager_steps(optimizer):
+    """hipGraph-replayed steps (epoch-dependent dropout keys, sampler seeds and optimizer
+    hyper-parameters read from the device epoch counter / tables) reproduce eager launches."""
+    sizes = [256, 512, 256, 128]
+    algos = ["relu", "tanh", "softmax"]
+    n, S, epochs = 2048, 512, 9
+    g = torch.Generator().manual_seed(4)
+    inputs = torch.randn(n, sizes[0], generator=g)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    runs = {}
+    for graphs in (False, True):
+        gpu, _ = _pair(sizes, algos, optimizer, "bfloat16")
+        tr = FusedTrainer(gpu)
+        tr.use_graphs = graphs
+        tr.load_tensors(inputs, labels, seed=11)
+        sched = lambda e: 0.01 * 0.9 ** e  # noqa: E731
+        tr.begin(epochs, lr_schedule=sched)
+        every = max(1, epochs // 100)
+        for e in range(epochs):
+            tr.step(e, 0.01 * 0.9 ** e, S, 0.2, 1e-3, want_ratios=e % every == 0, record=e == epochs - 1)
+        out = tr.drain()
+        assert bool(tr._graphs) == graphs  # the graph run really replayed captured steps
+        runs[graphs] = ([c for _, c, _, _ in out], [r for _, _, r, _ in out], gpu._param_store.flat.clone(),
+                        gpu.optimizer.state_dict() if gpu.optimizer is not None else None)
+    # same masks, seeds and hyper-parameters; only the float-atomic bias-gradient sums may round
+    # in a different order (as between two eager runs)
+    (c0, r0, p0, s0), (c1, r1, p1, s1) = runs[False], runs[True]
+    assert all(math.isfinite(c) for c in c1)
+    for a, b in zip(c0, c1):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(a)), (c0, c1)
+    for a, b in zip(r0, r1):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert all(abs(x - y) < 1e-3 * abs(x) + 1e-7 for x, y in zip(a, b)), (a, b)
+    d = (p0 - p1).abs()
+    assert (d > 1e-3).double().mean().item() < 1e-3 and d.mean().item() < 1e-5
+    if s0 is not None:
+        for k in s0["state"]:
+            assert float(s0["state"][k]["step"]) == float(s1["state"][k]["step"]) == epochs

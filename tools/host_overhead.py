@@ -30,15 +30,16 @@ def main():
     y = torch.randint(0, sizes[-1], (2 * batch,))
     tr.load_tensors(x, y, seed=1)
     n = 60
-    tr.begin(n + 10)
+    tr.begin(n + 20, lr_schedule=lambda e: 1e-3)  # enables hipGraph replay (PZ_GRAPHS=0: eager)
+    every = max(1, (n + 20) // 100)
     for e in range(10):
-        tr.step(e, 1e-3, batch, 0.2, 1e-3, want_ratios=False, record=False)
+        tr.step(e, 1e-3, batch, 0.2, 1e-3, want_ratios=e % every == 0, record=False)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     enq = []
     for e in range(10, 10 + n):
         a = time.perf_counter()
-        tr.step(e, 1e-3, batch, 0.2, 1e-3, want_ratios=False, record=False)
+        tr.step(e, 1e-3, batch, 0.2, 1e-3, want_ratios=e % every == 0, record=False)
         enq.append(time.perf_counter() - a)
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / n
@@ -46,8 +47,8 @@ def main():
           f"{sorted(enq)[n // 2] * 1e3:.3f} ms/step")
     pr = cProfile.Profile()
     pr.enable()
-    for e in range(10):
-        tr.step(e, 1e-3, batch, 0.2, 1e-3, want_ratios=False, record=False)
+    for e in range(10 + n, 20 + n):
+        tr.step(e, 1e-3, batch, 0.2, 1e-3, want_ratios=e % every == 0, record=False)
     pr.disable()
     torch.cuda.synchronize()
     s = io.StringIO()
