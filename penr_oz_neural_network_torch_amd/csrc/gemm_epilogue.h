@@ -229,18 +229,15 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     }
     __builtin_amdgcn_sched_barrier(0);  // keep rows apart: bounds the live temporaries
   });
+  // column sums: reduce across the lanes now, issue the atomics after the tile is stored — the
+  // barrier below would otherwise wait (vmcnt(0)) for every contended atomic to come back
   if (!FWD_ONLY && p.colsum != nullptr) {
 #pragma unroll
-    for (int j = 0; j < COLS; ++j) {
-      const int n = n0 + nl0 + L::n_off(j);
+    for (int j = 0; j < COLS; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float s = cs[j][r];
+      for (int r = 0; r < 4; ++r)
 #pragma unroll
-        for (int o = 1; o < L::RED; o <<= 1) s += __shfl_xor(s, o, 64);
-        if ((lane & (L::RED - 1)) == 0 && n + r < p.N) atomicAdd(p.colsum + n + r, s);
-      }
-    }
+        for (int o = 1; o < L::RED; o <<= 1) cs[j][r] += __shfl_xor(cs[j][r], o, 64);
   }
   __syncthreads();
   uint16_t* __restrict__ Cp = static_cast<uint16_t*>(p.C);
@@ -252,17 +249,17 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     const int r = s * ROWS_PER_PASS + my_row;
     const int gm = m0 + r, gn = n0 + my_chunk * 8;
     const u32x4_t v = *reinterpret_cast<const PZ_LDS u32x4_t*>(smem + cimg_off<BN>(r, my_chunk * 8));
-    if (gm < p.M && gn < p.N) {
+    const bool in_range = gm < p.M && gn < p.N;
+    uint32_t byte = 0;  // ReLU bitmask of this 8-column chunk: bit b = element gn+b > 0
+    if (in_range) {
       *reinterpret_cast<u32x4_t*>(Cp + static_cast<int64_t>(gm) * p.ldc + gn) = v;
-      if (!bwd && use_mask) {  // bit b = element gn+b > 0 (bf16: sign clear, magnitude nonzero)
-        uint32_t byte = 0;
+      if (!bwd && use_mask) {  // bf16 > 0: sign clear, magnitude nonzero
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const uint32_t lo = v[q] & 0xFFFFu, hi = v[q] >> 16;
           byte |= ((lo - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q);
           byte |= ((hi - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q + 1);
         }
-        p.mask[static_cast<int64_t>(gm) * p.ldmask + gn / 8] = static_cast<uint8_t>(byte);
       }
       if (want8) {  // e4m3 copy of the bf16 values + running |y| max
         float x[8];
@@ -274,6 +271,12 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
         }
         *reinterpret_cast<u32x2_t*>(p.out8 + static_cast<int64_t>(gm) * p.ldout8 + gn) = to_e4m3x8(x, qs);
       }
+    }
+    if (!bwd && use_mask) {  // 4 neighbouring chunks of a row -> one 4-byte store (not 4 byte stores)
+      const uint32_t b1 = __shfl_down(byte, 1, 64), b2 = __shfl_down(byte, 2, 64), b3 = __shfl_down(byte, 3, 64);
+      if (in_range && (my_chunk & 3) == 0)
+        *reinterpret_cast<uint32_t*>(p.mask + static_cast<int64_t>(gm) * p.ldmask + gn / 8) =
+            byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
     }
   }
   if (want8 && p.amax != nullptr) {  // one atomic per workgroup (same-address atomics serialise)
@@ -288,6 +291,15 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 #pragma unroll
       for (int w = 1; w < NW; ++w) m = fmaxf(m, part[w]);
       atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(m));
+    }
+  }
+  if (!FWD_ONLY && p.colsum != nullptr) {  // fire-and-forget: nothing waits for them in this kernel
+#pragma unroll
+    for (int j = 0; j < COLS; ++j) {
+      const int n = n0 + nl0 + L::n_off(j);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if ((lane & (L::RED - 1)) == 0 && n + r < p.N) atomicAdd(p.colsum + n + r, cs[j][r]);
     }
   }
 }

@@ -530,7 +530,7 @@ class FusedTrainer:
         graphable = (plan is not None and not record and indices is None and self._launch_bound(batch)
                      and epoch < plan["epochs"]
                      and want_ratios == (epoch % plan["every"] == 0) and lr == plan["lrs"][epoch]
-                     and self.opt.step_count == plan["t0"] + epoch)
+                     and (not self.opt.adam or self.opt.step_count == plan["t0"] + epoch))
         gkey = (self.parity, batch, float(dropout), float(l2))
         if graphable and gkey in self._warm:
             self._replay(gkey, epoch, lr, batch, dropout, l2, row)

@@ -41,6 +41,12 @@ def main():
         ("fwdL2_relu", B, 4096, 4096, True, False, torch.bfloat16, "fwd_relu"),
         ("fwdL2_drop1", B, 4096, 4096, True, False, torch.bfloat16, "fwd_nodrop"),
         ("dXL3_nodrop", B, 4096, 1024, True, True, torch.bfloat16, "bwd_nodrop"),
+        # the trainer's actual epilogues: ReLU bitmask written by the forward, read by dX
+        ("fwdL1_mask", B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask"),
+        ("fwdL2_mask", B, 4096, 4096, True, False, torch.bfloat16, "fwd_mask"),
+        ("dXL3_mask", B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask"),
+        ("dXL3_mask_nocs", B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask_nocs"),
+        ("dXL2_mask", B, 4096, 4096, True, True, torch.bfloat16, "bwd_mask"),
         # e4m3 forward GEMMs (run when named): mlp8192 layers and the mlp4 middle layer
         ("f8_8k_L1", B, 8192, 1024, True, True, "fp8", "fwd"),
         ("f8_8k_L2", B, 1024, 8192, True, True, "fp8", "fwd_nodrop"),
@@ -63,6 +69,7 @@ def main():
         aux = torch.randn(M, N, device=dev).to(torch.bfloat16)
         colsum = torch.zeros(N, device=dev)
         epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=0.2, seed=(1, 2))
+        mask = torch.randint(0, 256, (M, PF.relu_mask_cols(N)), device=dev, dtype=torch.uint8)
         if mode == "fwd":
             fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=epi)
         elif mode == "fwd_nodrop":
@@ -75,6 +82,12 @@ def main():
         elif mode == "bwd_nodrop":
             fused = lambda: PF.gemm(a, akc, b, bkc, c, aux=aux, colsum=colsum, mode=PF.EPI_BWD,
                                     epi=PF.epi_spec(act=PF.ACT_RELU))
+        elif mode == "fwd_mask":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=epi, mask=mask)
+        elif mode == "bwd_mask":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, colsum=colsum, mode=PF.EPI_BWD, epi=epi, mask=mask)
+        elif mode == "bwd_mask_nocs":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, mode=PF.EPI_BWD, epi=epi, mask=mask)
         elif mode == "bwd":
             fused = lambda: PF.gemm(a, akc, b, bkc, c, aux=aux, colsum=colsum, mode=PF.EPI_BWD, epi=epi)
         else:
