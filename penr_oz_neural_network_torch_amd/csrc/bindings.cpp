@@ -10,7 +10,9 @@
 
 #include <torch/library.h>
 
+#include <cstdio>
 #include <cstring>
+#include <tuple>
 #include <vector>
 
 #include "json_format.h"
@@ -590,6 +592,35 @@ std::string format_json_array_op(const Tensor& t, int64_t level) {
 
 std::string repr_double_op(double x) { return pz::repr_double(x); }
 
+// checkpoint reader (N9): -> (skeleton JSON text, float64 values, int64 [ndim, dims...] records)
+std::tuple<std::string, Tensor, Tensor> scan_json_arrays_op(const std::string& path, const std::string& key) {
+  std::string text;
+  {
+    FILE* f = std::fopen(path.c_str(), "rb");
+    TORCH_CHECK(f != nullptr, "pz::scan_json_arrays: cannot open ", path);
+    std::fseek(f, 0, SEEK_END);
+    const long n = std::ftell(f);
+    std::fseek(f, 0, SEEK_SET);
+    text.resize(n > 0 ? static_cast<size_t>(n) : 0);
+    const size_t got = n > 0 ? std::fread(&text[0], 1, static_cast<size_t>(n), f) : 0;
+    std::fclose(f);
+    TORCH_CHECK(got == text.size(), "pz::scan_json_arrays: short read of ", path);
+  }
+  std::string skeleton;
+  std::vector<double> values;
+  std::vector<int64_t> shapes;
+  try {
+    pz::scan_json_arrays(text, key, skeleton, values, shapes);
+  } catch (const std::exception& e) {
+    TORCH_CHECK(false, e.what());
+  }
+  Tensor v = at::empty({static_cast<int64_t>(values.size())}, at::TensorOptions().dtype(at::kDouble));
+  if (!values.empty()) std::memcpy(v.data_ptr<double>(), values.data(), values.size() * sizeof(double));
+  Tensor s = at::empty({static_cast<int64_t>(shapes.size())}, at::TensorOptions().dtype(at::kLong));
+  if (!shapes.empty()) std::memcpy(s.data_ptr<int64_t>(), shapes.data(), shapes.size() * sizeof(int64_t));
+  return {std::move(skeleton), v, s};
+}
+
 }  // namespace
 
 TORCH_LIBRARY(pz, m) {
@@ -636,6 +667,7 @@ TORCH_LIBRARY(pz, m) {
   m.def("quantize_rows(Tensor x, Tensor(a!) out, Tensor qs, Tensor(b!)? amax) -> ()");
   m.def("format_json_array(Tensor t, int level) -> str");
   m.def("repr_double(float x) -> str");
+  m.def("scan_json_arrays(str path, str key) -> (str, Tensor, Tensor)");
 }
 
 TORCH_LIBRARY_IMPL(pz, CUDA, m) {
@@ -671,4 +703,5 @@ TORCH_LIBRARY_IMPL(pz, CPU, m) {
 TORCH_LIBRARY_IMPL(pz, CompositeExplicitAutograd, m) {
   m.impl("pack_segments", TORCH_FN(pack_segments_op));
   m.impl("repr_double", TORCH_FN(repr_double_op));
+  m.impl("scan_json_arrays", TORCH_FN(scan_json_arrays_op));
 }

@@ -11,6 +11,8 @@
 #include <charconv>
 #include <cmath>
 #include <cstring>
+#include <stdexcept>
+#include <vector>
 
 namespace pz {
 namespace {
@@ -92,6 +94,161 @@ std::string repr_double(double x) {
   std::string s;
   append_repr(s, x);
   return s;
+}
+
+}  // namespace pz
+
+// ------------------------------------------------------------------------------------------
+// reader: lift the numeric arrays under one top-level key out of a JSON document
+// ------------------------------------------------------------------------------------------
+namespace pz {
+namespace {
+
+struct Scanner {
+  const char* p;
+  const char* end;
+  std::string& skel;
+  std::vector<double>& values;
+  std::vector<int64_t>& shapes;
+  int64_t next_id = 0;
+
+  void ws() {
+    while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p;
+  }
+  [[noreturn]] void fail(const char* what) {
+    throw std::runtime_error(std::string("pz::scan_json_arrays: ") + what);
+  }
+  // one JSON number (Python's json spelling incl. NaN / Infinity / -Infinity)
+  bool number(double& out) {
+    ws();
+    if (p >= end) return false;
+    if (end - p >= 3 && std::memcmp(p, "NaN", 3) == 0) { out = std::nan(""); p += 3; return true; }
+    if (end - p >= 8 && std::memcmp(p, "Infinity", 8) == 0) { out = HUGE_VAL; p += 8; return true; }
+    if (end - p >= 9 && std::memcmp(p, "-Infinity", 9) == 0) { out = -HUGE_VAL; p += 9; return true; }
+    if (!(*p == '-' || (*p >= '0' && *p <= '9'))) return false;
+    auto res = std::from_chars(p, end, out);  // correctly rounded, like Python's float()
+    if (res.ec != std::errc()) return false;
+    p = res.ptr;
+    return true;
+  }
+  // a rectangular nested array of numbers starting at '['; false (position restored) otherwise
+  bool numeric_array(std::vector<int64_t>& shape, int depth) {
+    const char* start = p;
+    const size_t nv = values.size();
+    ws();
+    if (p >= end || *p != '[') return false;
+    ++p;
+    ws();
+    int64_t count = 0;
+    std::vector<int64_t> inner;
+    bool nested = false;
+    if (p < end && *p == ']') {  // [] is a numeric (empty) row only inside an array
+      if (depth == 0) { p = start; return false; }
+      ++p;
+      shape.assign(1, 0);
+      return true;
+    }
+    while (true) {
+      ws();
+      if (p < end && *p == '[') {
+        std::vector<int64_t> sub;
+        if (!numeric_array(sub, depth + 1) || (count > 0 && (!nested || sub != inner))) {
+          p = start; values.resize(nv); return false;
+        }
+        nested = true;
+        inner = sub;
+      } else {
+        double v;
+        if (nested || !number(v)) { p = start; values.resize(nv); return false; }
+        values.push_back(v);
+      }
+      ++count;
+      ws();
+      if (p < end && *p == ',') { ++p; continue; }
+      if (p < end && *p == ']') { ++p; break; }
+      p = start; values.resize(nv); return false;
+    }
+    shape.assign(1, count);
+    if (nested) shape.insert(shape.end(), inner.begin(), inner.end());
+    return true;
+  }
+  // copy a string literal verbatim
+  void string_lit() {
+    const char* s = p++;
+    while (p < end && *p != '"') p += (*p == '\\') ? 2 : 1;
+    if (p >= end) fail("unterminated string");
+    ++p;
+    skel.append(s, p - s);
+  }
+  // copy / transform one value. Modes: COPY; IN_KEY (inside the target member: objects' "params"
+  // lists switch to PARAMS); PARAMS (a list of parameters: each element is lifted); LIFT (a
+  // numeric array becomes one "@@PZ_ARRAY_<k>@@" placeholder)
+  enum Mode { COPY, IN_KEY, PARAMS, LIFT };
+  void value(Mode mode) {
+    ws();
+    if (p >= end) fail("unexpected end");
+    if (*p == '"') { string_lit(); return; }
+    if (*p == '[') {
+      if (mode == LIFT) {
+        std::vector<int64_t> shape;
+        if (numeric_array(shape, 0)) {
+          shapes.push_back(static_cast<int64_t>(shape.size()));
+          shapes.insert(shapes.end(), shape.begin(), shape.end());
+          skel += "\"@@PZ_ARRAY_" + std::to_string(next_id++) + "@@\"";
+          return;
+        }
+      }
+      skel += *p++;
+      ws();
+      if (p < end && *p == ']') { skel += *p++; return; }
+      const Mode inner = mode == PARAMS ? LIFT : mode;
+      while (true) {
+        value(inner);
+        ws();
+        if (p < end && *p == ',') { skel += *p++; continue; }
+        if (p < end && *p == ']') { skel += *p++; return; }
+        fail("bad array");
+      }
+    }
+    if (*p == '{') { object(mode == COPY ? COPY : IN_KEY, false); return; }
+    const char* s = p;  // number / literal: copy the token
+    while (p < end && *p != ',' && *p != ']' && *p != '}' && *p != ' ' && *p != '\n' && *p != '\r' && *p != '\t') ++p;
+    skel.append(s, p - s);
+  }
+  void object(Mode mode, bool top) {
+    skel += *p++;  // '{'
+    ws();
+    if (p < end && *p == '}') { skel += *p++; return; }
+    while (true) {
+      ws();
+      if (p >= end || *p != '"') fail("expected a key");
+      const char* k0 = p + 1;
+      string_lit();
+      const std::string key(k0, p - 1 - k0);
+      ws();
+      if (p >= end || *p != ':') fail("expected ':'");
+      skel += *p++;
+      value(top && key == target ? IN_KEY : (mode == IN_KEY && key == "params") ? PARAMS : mode);
+      ws();
+      if (p < end && *p == ',') { skel += *p++; continue; }
+      if (p < end && *p == '}') { skel += *p++; return; }
+      fail("bad object");
+    }
+  }
+  std::string target;
+};
+
+}  // namespace
+
+void scan_json_arrays(const std::string& text, const std::string& key, std::string& skeleton,
+                      std::vector<double>& values, std::vector<int64_t>& shapes) {
+  skeleton.clear();
+  skeleton.reserve(4096);
+  Scanner sc{text.data(), text.data() + text.size(), skeleton, values, shapes};
+  sc.target = key;
+  sc.ws();
+  if (sc.p >= sc.end || *sc.p != '{') throw std::runtime_error("pz::scan_json_arrays: top level must be an object");
+  sc.object(Scanner::COPY, true);
 }
 
 }  // namespace pz

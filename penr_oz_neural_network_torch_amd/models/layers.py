@@ -32,6 +32,13 @@ def _pf():
     return PF
 
 
+def _f64(values) -> Tensor:
+    """Checkpoint values -> fp64 tensor: nested lists (reference loader) or tensors (native reader)."""
+    if isinstance(values, Tensor):
+        return values.detach().to(dtype=torch.float64, device=_CPU, copy=True)
+    return torch.tensor(values, dtype=torch.float64)
+
+
 def _randn_fp64(*shape: int) -> Tensor:
     """Initial values drawn exactly like the reference: fp32 ``randn`` widened to fp64
     (``neural_net_model.py:65,104,108``), so a seeded model equals the reference's bit for bit."""
@@ -64,9 +71,9 @@ class Layer:
     def state_dict(self, new_state: dict):
         values = new_state["params"]
         if values:
-            self.weights = torch.tensor(values[0], dtype=torch.float64)
+            self.weights = _f64(values[0])
         if len(values) > 1:
-            self.bias = torch.tensor(values[1], dtype=torch.float64)
+            self.bias = _f64(values[1])
 
     def checkpoint_state(self, ref) -> dict:
         """``state_dict`` with parameter tensors wrapped by ``ref`` (rendered natively later)."""
@@ -173,10 +180,10 @@ class BatchNormLayer(Layer):
     def state_dict(self, new_state: dict):
         values = new_state["params"]
         if values:
-            self.gain = torch.tensor(values[0], dtype=torch.float64)
+            self.gain = _f64(values[0])
             self.variance = torch.ones_like(self.gain, dtype=torch.float64)
         if len(values) > 1:
-            self.bias = torch.tensor(values[1], dtype=torch.float64)
+            self.bias = _f64(values[1])
             self.mean = torch.zeros_like(self.bias, dtype=torch.float64)
         self.eps = new_state["eps"]
         self.momentum = new_state["momentum"]

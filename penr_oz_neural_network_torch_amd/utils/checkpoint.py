@@ -224,10 +224,48 @@ def save_async(model_id: str, skeleton: dict, optimizer_state: dict | None) -> t
     return t
 
 
+_ARRAY_TAG = "@@PZ_ARRAY_"
+
+
+def _read_native(path: str) -> dict:
+    """Parse a checkpoint with the native reader: layer parameters come back as float64 tensors
+    (parsed straight into one buffer, correctly rounded like ``float()``), everything else as
+    ``json.loads`` of the small remaining skeleton would give it."""
+    skeleton, values, shapes = torch.ops.pz.scan_json_arrays(path, "layers")
+    data = json.loads(skeleton)
+    arrays, off, i = [], 0, 0
+    rec = shapes.tolist()
+    while i < len(rec):
+        nd = rec[i]
+        dims = rec[i + 1:i + 1 + nd]
+        n = 1
+        for d in dims:
+            n *= d
+        arrays.append(values[off:off + n].view(dims))
+        off += n
+        i += 1 + nd
+    for layer in data.get("layers", []):
+        if isinstance(layer, dict) and isinstance(layer.get("params"), list):
+            layer["params"] = [arrays[int(v[len(_ARRAY_TAG):-2])] if isinstance(v, str) and v.startswith(_ARRAY_TAG)
+                               else v for v in layer["params"]]
+    return data
+
+
+def read_model_data(path: str) -> dict:
+    """Model JSON -> dict. Parameter arrays are float64 tensors on the native path (N9 reader;
+    ~0.36 µs/param for the reference's ``json.load`` + ``torch.tensor(list)``), lists otherwise."""
+    if not os.path.exists(path):
+        raise FileNotFoundError(2, "No such file or directory", path)
+    from ..ops import native
+    if native.has_host_ops() and os.environ.get("PZ_NATIVE_JSON", "1") != "0":
+        return _read_native(path)
+    with open(path, "r", encoding="utf-8") as f:
+        return json.load(f)
+
+
 def load(model_id: str) -> tuple[dict, dict | None]:
     """Return ``(model_data, optimizer_state_or_None)``; missing model → ``FileNotFoundError``."""
-    with open(model_path(model_id), "r", encoding="utf-8") as f:
-        data = json.load(f)
+    data = read_model_data(model_path(model_id))
     opath = optimizer_path(model_id)
     opt_state = torch.load(opath, weights_only=True, map_location="cpu") if os.path.exists(opath) else None
     return data, opt_state

@@ -177,3 +177,42 @@ def test_background_checkpoint_matches_synchronous(models_tmpdir):
     loaded = NeuralNetworkModel.deserialize("bg")
     for a, b in zip(loaded.params, snap_params):
         assert torch.equal(a, b)
+
+
+def test_native_checkpoint_reader_matches_json_load(models_tmpdir, monkeypatch):
+    """N9 reader: layer parameters parsed natively into tensors equal json.load + torch.tensor
+    bit for bit (incl. NaN / inf / -0.0 / subnormals); every other field is untouched."""
+    from penr_oz_neural_network_torch_amd.ops import native
+    if not native.has_host_ops():
+        pytest.skip("native library not built")
+    torch.manual_seed(9)
+    m = NeuralNetworkModel("rd", [27, 10, 30, 16, 27], "he", "",
+                           ["embedding", "linear", "batchnorm", "tanh", "linear", "softmax"])
+    with torch.no_grad():
+        w = m.layers[2].weights
+        w[0, :4] = torch.tensor([float("nan"), float("inf"), -0.0, 5e-324], dtype=torch.float64)
+    m.training_data_buffer = [([1.0, 2.0, 3.0], [4]), ([0.5, -1.0, 2.0], [1])]
+    m.stats = {"layers": [{"histogram": {"x": [1.0, 2.0], "y": [0.5, 0.25]}}]}
+    m.serialize()
+    path = ckpt.model_path("rd")
+    fast = ckpt.read_model_data(path)
+    with open(path) as f:
+        slow = json.load(f)
+    assert [type(p) for l in fast["layers"] for p in l.get("params", [])] == \
+        [torch.Tensor] * sum(len(l.get("params", [])) for l in slow["layers"])
+    for lf, ls in zip(fast["layers"], slow["layers"]):
+        assert {k: v for k, v in lf.items() if k != "params"} == {k: v for k, v in ls.items() if k != "params"}
+        for a, b in zip(lf.get("params", []), ls.get("params", [])):
+            ref = torch.tensor(b, dtype=torch.float64)
+            assert a.shape == ref.shape
+            assert torch.equal(a.view(torch.int64), ref.view(torch.int64))  # bitwise, NaN included
+    for k in slow:
+        if k != "layers":
+            assert fast[k] == slow[k]
+    loaded = NeuralNetworkModel.deserialize("rd")
+    for a, b in zip(loaded.params, m.params):
+        assert torch.equal(a.view(torch.int64), b.detach().view(torch.int64))
+    monkeypatch.setenv("PZ_NATIVE_JSON", "0")
+    again = NeuralNetworkModel.deserialize("rd")
+    for a, b in zip(again.params, loaded.params):
+        assert torch.equal(a.view(torch.int64), b.view(torch.int64))
