@@ -228,6 +228,7 @@ class FusedTrainer:
         gemm_w = [st.seg_w.offset for st in self.stages if st.kind == "gemm"]
         self._early_keys = set(gemm_w[1:])
         self._after_dx = os.environ.get("PZ_OPT_AFTER_DX", "1") == "1"  # measured 0.6% faster on one GPU
+        self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "2")))  # first-layer dW under DP
         self.opt.define_groups(gemm_w[1:])
         self._opt_done = None
         self._ov = None
@@ -818,20 +819,31 @@ class FusedTrainer:
             return dx, False
         # GEMM stage: dW = x_inᵀ · dZ
         w_grad = self._w_grad(st.seg_w)
-        PF.gemm(x_in, False, g, False, w_grad)
-        handles.append(self.ctx.all_reduce_async(w_grad))
+        # Data parallel: the first layer's gradient is the last bucket of the backward and nothing
+        # is left to hide its all-reduce behind, so its dW GEMM runs in row chunks and chunk c's
+        # all-reduce travels while chunk c+1 is computed (only the last chunk's is exposed)
+        chunks = self._dw_chunks if (before is None and self.ctx.world_size > 1) else 1
+        if chunks < 2 or w_grad.shape[0] % (8 * chunks):
+            chunks = 1
+        mine = []
+        rows = w_grad.shape[0] // chunks
+        for c in range(chunks):
+            sl = slice(c * rows, (c + 1) * rows)
+            PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False, w_grad[sl] if chunks > 1 else w_grad)
+            mine.append(self.ctx.all_reduce_async(w_grad[sl] if chunks > 1 else w_grad))
+        handles.extend(mine)
         # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
         # unless the GEMMs read the fp32 master itself (float32 policy)
         own = st.seg_w.offset in self._early_keys
         early = st.seg_w.offset in self.shadow_sets[self.parity] and not self._after_dx
         if self._ov is not None and not own:  # updated by the final launch
             self._late_stages.append(st)
-            self._late_handles.append(handles[-1])
+            self._late_handles.extend(mine)
         if self._ov is not None and own and early:
-            self._opt_async(st.seg_w.offset, [handles[-1]], [st])
+            self._opt_async(st.seg_w.offset, mine, [st])
         out = self._backward_dx(st, before, g, batch, p, keys, rec)
         if self._ov is not None and own and not early:
-            self._opt_async(st.seg_w.offset, [handles[-1]], [st])
+            self._opt_async(st.seg_w.offset, mine, [st])
         return out
 
     def _backward_dx(self, st: Stage, before: Stage | None, g, batch, p, keys, rec):
@@ -912,6 +924,8 @@ class FusedTrainer:
         self._pending = []
         self._start_event = torch.cuda.Event(enable_timing=True)
         self._start_event.record()
+        self._last_ms = 0.0
+        self.step_ms = {}
         torch.cuda.synchronize(self.dev)
         self._start_wall = datetime.now()
 
@@ -923,11 +937,14 @@ class FusedTrainer:
         costs = self.costs.cpu().tolist()
         ratios = self.ratios.cpu().view(-1, max(1, self.opt.nslots)).tolist()
         out = []
+        self.step_ms = {}  # epoch -> GPU time since the previous step ended (ms), for telemetry
         for epoch, row, ev in self._pending:
             ms = self._start_event.elapsed_time(ev)
             when = (self._start_wall + timedelta(milliseconds=ms)).isoformat()
             r = ratios[row][:self.opt.nslots] if row is not None else None
             out.append((epoch, costs[epoch], r, when))
+            self.step_ms[epoch] = ms - self._last_ms
+            self._last_ms = ms
         self._pending = []
         self.opt.sync_torch_state()
         return out

@@ -303,15 +303,19 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         log.info(f"Model {self.model_id}: Done training for {epochs} epochs.")
         self.serialize()
 
-    def _progress_point(self, when: str, epoch: int, cost: float, ratios: list[float] | None) -> None:
+    def _progress_point(self, when: str, epoch: int, cost: float, ratios: list[float] | None,
+                        extra: dict | None = None) -> None:
         pending = list(ratios or [])
-        self.progress.append({
+        point = {
             "dt": when,
             "epoch": epoch + 1,
             "cost": cost,
             "weight_upd_ratio": [pending.pop(0) if layer.weights is not None and pending else None
                                  for layer in self.layers],
-        })
+        }
+        if extra:  # optional telemetry of GPU runs; the dashboard ignores unknown keys
+            point.update(extra)
+        self.progress.append(point)
 
     def _train_autograd(self, data, epochs, learning_rate, sample_size, decay_rate, dropout_rate, l2_lambda):
         """The reference epoch loop (``neural_net_model.py:457-522``). On the CPU it is the
@@ -368,10 +372,17 @@ class NeuralNetworkModel(MultiLayerPerceptron):
             log.info(f"Model {self.model_id}: fused engine unavailable ({e}); training under autograd")
             return None
 
-    def _drain_progress(self, trainer) -> None:
-        for epoch, cost, ratios, when in trainer.drain():
+    def _drain_progress(self, trainer, sample_size: int) -> None:
+        drained = trainer.drain()
+        world = trainer.ctx.world_size
+        for epoch, cost, ratios, when in drained:
             if ratios is not None:
-                self._progress_point(when, epoch, cost, ratios)
+                ms = trainer.step_ms.get(epoch)
+                extra = {"device": str(self.device), "dtype": self.precision.name, "world_size": world}
+                if ms:
+                    extra["step_ms"] = round(ms, 4)
+                    extra["samples_per_s"] = round(sample_size / (ms * 1e-3), 1)
+                self._progress_point(when, epoch, cost, ratios, extra)
             log.info(f"Model {self.model_id}: Epoch {epoch + 1}, Cost: {cost:.4f}")
 
     def _record_fused(self, trainer) -> None:
@@ -390,11 +401,11 @@ class NeuralNetworkModel(MultiLayerPerceptron):
             trainer.step(epoch, learning_rate * decay_rate ** epoch, sample_size, dropout_rate, l2_lambda,
                          want_ratios=epoch % every == 0, record=epoch + 1 == epochs or long_training)
             if long_training:
-                self._drain_progress(trainer)
+                self._drain_progress(trainer, sample_size)
                 self._record_fused(trainer)
                 self.serialize_background()
                 last_saved = time.time()
-        self._drain_progress(trainer)
+        self._drain_progress(trainer, sample_size)
         if epochs:
             self._record_fused(trainer)
 

@@ -130,6 +130,8 @@ def test_model_train_on_gpu_end_to_end(models_tmpdir, dtype):
     assert model.status == "Trained"
     assert len(model.progress) == 5
     assert all(math.isfinite(p["cost"]) for p in model.progress)
+    last = model.progress[-1]  # optional GPU telemetry beside the reference keys
+    assert last["world_size"] == 1 and last["dtype"] == dtype and last["step_ms"] > 0 and last["samples_per_s"] > 0
     assert model.stats is not None and len(model.stats["layers"]) == len(model.layers)
     assert model.stats["layers"][-1]["gradient"] is None
     loaded = NeuralNetworkModel.deserialize("gpu_e2e")
