@@ -317,14 +317,38 @@ class NeuralNetworkModel(MultiLayerPerceptron):
             point.update(extra)
         self.progress.append(point)
 
-    def _train_autograd(self, data, epochs, learning_rate, sample_size, decay_rate, dropout_rate, l2_lambda):
+    def _train_autograd(self, data, epochs, learning_rate, sample_size, decay_rate, dropout_rate, l2_lambda,
+                        context=None, sampler: torch.Generator | None = None):
         """The reference epoch loop (``neural_net_model.py:457-522``). On the CPU it is the
-        reference's exact op / RNG sequence; GPU models run it on the HIP kernels."""
+        reference's exact op / RNG sequence; GPU models run it on the HIP kernels.
+
+        Data parallel (a process group is up, e.g. gloo for CPU models): replicas start from rank
+        0's parameters, every rank draws the same global sample from a shared ``sampler`` seed and
+        trains on its contiguous shard, and gradients are averaged with one all-reduce before the
+        (identical) optimizer step — equivalent to one process training on the whole sample."""
+        from ..parallel.dist import get_context
+        ctx = context or get_context()
+        world, rank = ctx.world_size, ctx.rank
+        if world > 1:
+            dev = self.params[0].device if self.params else torch.device("cpu")
+            with torch.no_grad():
+                for p in self.params:
+                    ctx.broadcast_(p.data)
+            if sampler is None:
+                seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
+                ctx.broadcast_(seed)
+                sampler = torch.Generator().manual_seed(int(seed.item()))
+        shard = max(1, sample_size // world)
         activations = None
         every = max(1, epochs // MAX_PROGRESS_POINTS)
         last_saved = time.time()
         for epoch in range(epochs):
-            picks = torch.randint(0, len(data), (sample_size,))
+            if sampler is None:  # the reference's draw from the global RNG
+                picks = torch.randint(0, len(data), (sample_size,))
+            else:
+                picks = torch.randint(0, len(data), (sample_size,), generator=sampler)
+            if world > 1:
+                picks = picks[rank * shard:(rank + 1) * shard]
             sample = [data[i] for i in picks]
             lr = learning_rate * (decay_rate ** epoch)
             if self.optimizer is not None:
@@ -345,12 +369,16 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                 for a in activations:
                     a.retain_grad()
             cost.backward()
+            if world > 1:
+                self._average_gradients(ctx)
             if self.optimizer is not None:
                 self.optimizer.step()
             else:
                 for p in self.params:
                     p.data -= lr * p.grad
             when, value = datetime.now().isoformat(), cost.item()
+            if world > 1:
+                value = ctx.all_reduce_scalar(value) / world
             if epoch % every == 0:
                 with torch.no_grad():
                     ratios = [((w - pw).data.std() / (w.data.std() + 1e-8)).item()
@@ -363,6 +391,17 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                 last_saved = time.time()
         if activations is not None:
             self._record_training_overall_progress(activations)
+
+    def _average_gradients(self, ctx) -> None:
+        """Mean of every parameter gradient over the ranks: one flat bucket, one all-reduce."""
+        grads = [p.grad for p in self.params]
+        flat = torch.cat([g.reshape(-1) for g in grads])
+        ctx.wait_all([ctx.all_reduce_async(flat, exact=True)])
+        flat /= ctx.world_size
+        off = 0
+        for g in grads:
+            g.copy_(flat[off:off + g.numel()].view_as(g))
+            off += g.numel()
 
     def _fused_trainer(self):
         from ..engine.trainer import FusedTrainer, UnsupportedModel

@@ -47,3 +47,45 @@ def test_gloo_two_rank_communicator(tmp_path):
         assert torch.equal(got["rep"], torch.zeros(7))
         assert got["max"] == 1.5 and got["sum"] == 2.0
         assert torch.allclose(got["bf16"], torch.full((64,), 1.5))
+
+
+def _train_rank(rank, world, port, optimizer, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
+    init_from_env("gloo")
+    model, data = _dp_model(optimizer)
+    torch.manual_seed(100 + rank)  # ranks' own RNG streams differ; the shared sampler decides the data
+    model._train_autograd(data, 4, 0.05, 32, 0.9, 0.0, 1e-3, sampler=torch.Generator().manual_seed(21))
+    if rank == 0:
+        torch.save({"params": [p.detach() for p in model.params], "costs": [p["cost"] for p in model.progress]},
+                   os.path.join(out_dir, "dp.pt"))
+    shutdown()
+
+
+def _dp_model(optimizer):
+    from neural_net_model import NeuralNetworkModel
+    torch.manual_seed(3)
+    model = NeuralNetworkModel("dp", [6, 16, 4], "xavier", "random", ["tanh", "softmax"], optimizer)
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(200, 6, generator=g, dtype=torch.float64)
+    y = torch.randint(0, 4, (200,), generator=g)
+    return model, [(x[i].tolist(), [int(y[i])]) for i in range(200)]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
+def test_gloo_data_parallel_training_equals_single_process(tmp_path, optimizer):
+    """CPU data parallelism (reference fp64 path): 2 ranks x 16 samples == 1 process x 32."""
+    mp.start_processes(_train_rank, args=(2, _free_port(), optimizer, str(tmp_path)), nprocs=2, start_method="spawn")
+    dp = torch.load(tmp_path / "dp.pt", weights_only=True)
+    from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
+    model, data = _dp_model(optimizer)
+    model._train_autograd(data, 4, 0.05, 32, 0.9, 0.0, 1e-3, context=DataParallelContext(),
+                          sampler=torch.Generator().manual_seed(21))
+    for a, b in zip(dp["params"], model.params):
+        torch.testing.assert_close(a, b.detach(), rtol=1e-12, atol=1e-12)
+    for a, b in zip(dp["costs"], [p["cost"] for p in model.progress]):
+        assert abs(a - b) < 1e-12 * max(1.0, abs(b))
