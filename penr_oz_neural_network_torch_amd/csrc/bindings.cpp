@@ -236,6 +236,7 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
   a.cols = static_cast<int>(logits.size(1));
   a.dtype = dt_of(logits);
   a.loss = ptr_or_null<float>(loss);
+  a.loss_slots = a.loss != nullptr ? static_cast<int>(loss->numel()) : 1;
   a.loss_scale = static_cast<float>(loss_scale);
   if (dh.has_value() && dh->defined()) {
     TORCH_CHECK(dh->scalar_type() == logits.scalar_type() && dh->stride(1) == 1, "pz::xent_head: dh");
@@ -270,6 +271,7 @@ void mse_head_op(const Tensor& y, const Tensor& target, int64_t rows_valid, cons
   a.cols = static_cast<int>(y.size(1));
   a.dtype = dt_of(y);
   a.loss = ptr_or_null<float>(loss);
+  a.loss_slots = a.loss != nullptr ? static_cast<int>(loss->numel()) : 1;
   a.loss_scale = static_cast<float>(loss_scale);
   if (dh.has_value() && dh->defined()) {
     a.dh = dh->data_ptr();
@@ -565,6 +567,7 @@ void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tenso
   TORCH_CHECK(ratio_row != -2 || every >= 1, "pz::step_finalize: ratio rule needs every >= 1");
   pz::FinalizeArgs a{};
   a.loss = ptr_or_null<const float>(loss);
+  a.loss_slots = a.loss != nullptr ? static_cast<int>(loss->numel()) : 1;
   a.loss_div = static_cast<float>(loss_div);
   a.stats_prev = stats_prev.data_ptr<double>();
   a.stats_cur = stats_cur.data_ptr<double>();

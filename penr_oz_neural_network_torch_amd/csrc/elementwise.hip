@@ -57,11 +57,13 @@ int grid_for(int64_t n) {
 // atomic per column per block — per-element global atomics made this kernel 20x slower.
 constexpr int kHeadRows = 16;
 
-PZ_DEV void block_loss_flush(float* loss, float v, float* red) {
+// block loss -> one of `slots` accumulators (the consumer sums them): hundreds of blocks adding
+// to ONE address serialise at L2 (measured: 512 blocks cost the CE head ~10 us)
+PZ_DEV void block_loss_flush(float* loss, float v, float* red, int slots) {
   v = wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
-  if (threadIdx.x == 0) atomicAdd(loss, red[0] + red[1] + red[2] + red[3]);
+  if (threadIdx.x == 0) atomicAdd(loss + (slots > 1 ? blockIdx.x % slots : 0), red[0] + red[1] + red[2] + red[3]);
 }
 
 PZ_DEV void block_colsum_flush(float* colsum, const float* cs, int cols) {
@@ -118,7 +120,7 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
       for (int c = lane; c < a.cols; c += 64) std_<T>(dh, static_cast<int64_t>(row) * a.ld_dh + c, 0.0);
     }
   }
-  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red);
+  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red, a.loss_slots);
   if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
 }
 
@@ -148,21 +150,22 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
   for (int j = 0; j < NCH; ++j) ok[j] = (lane + 64 * j) * 8 < a.cols;
   const int row0 = blockIdx.x * kHeadRows + wave * RPW;
   uint4 raw[RPW][NCH];
+  int64_t labels[RPW];  // fetched with the logits: no dependent load inside the row loop
 #pragma unroll
-  for (int rr = 0; rr < RPW; ++rr)
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = row0 + rr;
+    labels[rr] = row < a.rows_valid ? a.labels[row] : -1;
 #pragma unroll
-    for (int j = 0; j < NCH; ++j) {
-      const int row = row0 + rr;
+    for (int j = 0; j < NCH; ++j)
       raw[rr][j] = (row < a.rows && ok[j])
                        ? *reinterpret_cast<const uint4*>(logits + static_cast<int64_t>(row) * a.ld + (lane + 64 * j) * 8)
                        : make_uint4(0, 0, 0, 0);
-    }
+  }
   float loss_acc = 0.f;
 #pragma unroll
   for (int rr = 0; rr < RPW; ++rr) {
     const int row = row0 + rr;
     if (row >= a.rows) break;
-    const uint16_t* lr = logits + static_cast<int64_t>(row) * a.ld;
     float v[NCH][8];
 #pragma unroll
     for (int j = 0; j < NCH; ++j) {
@@ -171,12 +174,16 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
       for (int e = 0; e < 4; ++e) { v[j][2 * e] = bf2f(w[e] & 0xFFFF); v[j][2 * e + 1] = bf2f(w[e] >> 16); }
     }
     if (row < a.rows_valid) {
-      float mx = -INFINITY;
+      const int64_t label = labels[rr];
+      float mx = -INFINITY, xl = 0.f;  // xl: the label's logit, taken from registers
 #pragma unroll
       for (int j = 0; j < NCH; ++j)
         if (ok[j])
 #pragma unroll
-          for (int e = 0; e < 8; ++e) mx = fmaxf(mx, v[j][e]);
+          for (int e = 0; e < 8; ++e) {
+            mx = fmaxf(mx, v[j][e]);
+            xl += (lane + 64 * j) * 8 + e == label ? v[j][e] : 0.f;
+          }
       mx = wave_max(mx);
       float se = 0.f;
 #pragma unroll
@@ -187,9 +194,9 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
           se += v[j][e];
         }
       se = wave_sum(se);
-      const int64_t label = a.labels[row];
+      xl = wave_sum(xl);
       const float inv = 1.f / se;
-      if (lane == 0) loss_acc += (mx + __logf(se) - bf2f(lr[label])) * a.loss_scale;
+      if (lane == 0) loss_acc += (mx + __logf(se) - xl) * a.loss_scale;
 #pragma unroll
       for (int j = 0; j < NCH; ++j) {
         if (!ok[j]) continue;
@@ -222,7 +229,7 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
               make_uint4(0, 0, 0, 0);
     }
   }
-  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red);
+  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red, a.loss_slots);
   if (cs_on) {
     float* mine = cs_lds + wave * a.cols;
 #pragma unroll
@@ -274,7 +281,7 @@ __global__ void __launch_bounds__(256) mse_head_kernel(MseArgs a) {
       }
     }
   }
-  if (a.loss != nullptr) block_loss_flush(a.loss, acc, red);
+  if (a.loss != nullptr) block_loss_flush(a.loss, acc, red, a.loss_slots);
   if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
 }
 

@@ -140,7 +140,11 @@ __global__ void step_finalize_kernel(FinalizeArgs a) {
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const double loss = a.loss != nullptr ? static_cast<double>(*a.loss) / a.loss_div : 0.0;
+    double loss = 0.0;
+    if (a.loss != nullptr) {
+      for (int k = 0; k < a.loss_slots; ++k) loss += static_cast<double>(a.loss[k]);
+      loss /= a.loss_div;
+    }
     if (a.epoch < a.n_costs) a.costs[a.epoch] = static_cast<float>(loss + static_cast<double>(a.l2) * l2sum);
     if (a.epoch_ptr != nullptr) *a.epoch_ptr = a.epoch + 1;
   }

@@ -14,6 +14,7 @@ struct XentArgs {
   int rows, rows_valid, cols;
   int dtype;
   float* loss;          // += sum_rows (lse - x_label) * loss_scale   (may be null)
+  int loss_slots;       // > 1: block b adds into loss[b % loss_slots] (the consumer sums them)
   float loss_scale;
   void* dh;             // [rows][ld_dh] gradient wrt the pre-dropout logits (may be null)
   int64_t ld_dh;
@@ -33,6 +34,7 @@ struct MseArgs {
   int rows, rows_valid, cols;
   int dtype;
   float* loss;
+  int loss_slots;       // > 1: block b adds into loss[b % loss_slots]
   float loss_scale;     // 1 / numel
   void* dh;
   int64_t ld_dh;
@@ -112,6 +114,7 @@ hipError_t segment_stats(const float* params, const OptSegment* segments, const 
 
 struct FinalizeArgs {
   const float* loss;        // accumulated loss (summed over ranks when data parallel)
+  int loss_slots;           // loss[0..loss_slots) are summed (the heads spread their block adds)
   float loss_div;           // world size
   double* stats_prev;       // [nslots][4] stats of the weights used by this step (zeroed afterwards)
   const double* stats_cur;  // [nslots][4] stats of the update just applied

@@ -44,6 +44,7 @@ from .optim import FusedOptimizer
 
 ROW_PAD = 64  # batch rows padded to the GEMM K-tile so dW = XᵀdZ stays on the MFMA path
 _M32 = 0xFFFFFFFF
+LOSS_SLOTS = 64
 # Steps below this are launch-bound (measured on MI355X: [4,8,2] at batch 32 runs 0.093 ms/step
 # replayed vs 0.172 eager; [256,1024,1024,64] at batch 1024 (8 GFLOP) is already GPU-bound and
 # replays 5 % slower, as does the 1.2 TFLOP bench step: ROCm executes the captured side-stream
@@ -173,8 +174,10 @@ class FusedTrainer:
         self.stages, self.head = compile_stages(model)
         for i, st in enumerate(self.stages):
             st.index = i
-        self.grads = torch.zeros(self.store.numel + 64, device=self.dev, dtype=torch.float32)
-        self.loss_slot = self.grads[self.store.numel:self.store.numel + 1]
+        # LOSS_SLOTS loss accumulators after the parameters (inside the exact fp32 DP bucket): the
+        # head's blocks spread their adds over them, step_finalize sums them
+        self.grads = torch.zeros(self.store.numel + LOSS_SLOTS, device=self.dev, dtype=torch.float32)
+        self.loss_slot = self.grads[self.store.numel:self.store.numel + LOSS_SLOTS]
         # low-precision GEMM copies of the weights, PING-PONG: step t's GEMMs read set `parity`
         # while its optimizer writes set 1-parity — so a weight can be updated as soon as its
         # gradient is reduced, even while the dX GEMM of the same layer still reads it
