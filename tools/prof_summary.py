@@ -3,7 +3,9 @@ import csv
 import sys
 
 
-def main(path_dir: str, marker: str = "optimizer_kernel") -> None:
+def main(path_dir: str, marker: str = "step_finalize_kernel") -> None:
+    """``marker``: a kernel launched exactly once per training step (step_finalize ends every step;
+    the optimizer runs as several launches per step when its updates overlap the backward)."""
     stats = list(csv.DictReader(open(f"{path_dir}/run_kernel_stats.csv")))
     print("== kernel totals ==")
     for r in stats[:30]:
@@ -14,8 +16,8 @@ def main(path_dir: str, marker: str = "optimizer_kernel") -> None:
     if len(idx) >= 2:
         a, b = idx[-2], idx[-1]
         t0 = int(rows[a]['End_Timestamp'])
-        print("== last step timeline (us since previous optimizer end) ==")
-        for r in rows[a + 1:b + 2]:
+        print(f"== last step timeline (us since the previous {marker} ended) ==")
+        for r in rows[a + 1:b + 1]:
             s, e = int(r['Start_Timestamp']), int(r['End_Timestamp'])
             print(f"{(s - t0) / 1e3:9.1f} {(e - s) / 1e3:9.1f}us vgpr={r['VGPR_Count']:>4} agpr={r['Accum_VGPR_Count']:>4} "
                   f"lds={r['LDS_Block_Size']:>6} grid={r['Grid_Size_X']:>7} {r['Kernel_Name'][:100]}")
