@@ -339,10 +339,10 @@ void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t
 // ------------------------------------------------------------------------------- optimizer
 Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::IntArrayRef is_weight,
                         at::IntArrayRef stat_slot, at::ArrayRef<optional<Tensor>> shadows,
-                        at::ArrayRef<optional<Tensor>> grads16) {
+                        at::ArrayRef<optional<Tensor>> grads16, at::IntArrayRef zero_grad) {
   const size_t n = offsets.size();
   TORCH_CHECK(numels.size() == n && is_weight.size() == n && stat_slot.size() == n && shadows.size() == n &&
-                  (grads16.empty() || grads16.size() == n),
+                  (grads16.empty() || grads16.size() == n) && (zero_grad.empty() || zero_grad.size() == n),
               "pz::pack_segments: length mismatch");
   Tensor out = at::empty({static_cast<int64_t>(n * sizeof(pz::OptSegment))}, at::TensorOptions().dtype(at::kByte));
   auto* segs = reinterpret_cast<pz::OptSegment*>(out.data_ptr<uint8_t>());
@@ -352,6 +352,7 @@ Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::Int
     s.numel = numels[i];
     s.is_weight = static_cast<int>(is_weight[i]);
     s.stat_slot = static_cast<int>(stat_slot[i]);
+    s.zero_grad = zero_grad.empty() ? 0 : static_cast<int>(zero_grad[i]);
     const auto& sh = shadows[i];
     if (sh.has_value() && sh->defined()) {
       TORCH_CHECK(sh->is_contiguous() && sh->numel() == numels[i], "pz::pack_segments: shadow shape");
@@ -566,7 +567,7 @@ void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tenso
   TORCH_CHECK(ratio_row < 0 || (ratio_row + 1) * nslots <= ratios.numel(), "pz::step_finalize: ratio row out of range");
   TORCH_CHECK(ratio_row != -2 || every >= 1, "pz::step_finalize: ratio rule needs every >= 1");
   pz::FinalizeArgs a{};
-  a.loss = ptr_or_null<const float>(loss);
+  a.loss = ptr_or_null<float>(loss);
   a.loss_slots = a.loss != nullptr ? static_cast<int>(loss->numel()) : 1;
   a.loss_div = static_cast<float>(loss_div);
   a.stats_prev = stats_prev.data_ptr<double>();
@@ -644,8 +645,8 @@ TORCH_LIBRARY(pz, m) {
   m.def("gather_rows(Tensor data, Tensor? indices, int seed_lo, int seed_hi, Tensor(a!) out, int rows_valid, "
         "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked, Tensor? epoch=None) -> ()");
   m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows, "
-        "Tensor?[] grads16) -> Tensor");
-  m.def("optimizer_step(Tensor(a!) params, Tensor grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
+        "Tensor?[] grads16, int[] zero_grad=[]) -> Tensor");
+  m.def("optimizer_step(Tensor(a!) params, Tensor(e!) grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
         "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
         "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats, Tensor? hp=None, "
         "Tensor? epoch=None) -> ()");
@@ -661,7 +662,7 @@ TORCH_LIBRARY(pz, m) {
         "float[] epi_f, int idx_ld) -> ()");
   m.def("embedding_fwd(Tensor table, Tensor idx, Tensor(a!) out) -> ()");
   m.def("embedding_bwd(Tensor dout, Tensor idx, Tensor(a!) dtable) -> ()");
-  m.def("step_finalize(Tensor? loss, float loss_div, Tensor(a!) stats_prev, Tensor stats_cur, Tensor slot_numel, "
+  m.def("step_finalize(Tensor(e!)? loss, float loss_div, Tensor(a!) stats_prev, Tensor stats_cur, Tensor slot_numel, "
         "int nslots, float l2, Tensor(b!) costs, int epoch, Tensor(c!) ratios, int ratio_row, "
         "Tensor(d!)? epoch_ctr=None, int every=1) -> ()");
   m.def("amax_abs(Tensor x, Tensor(a!) amax) -> ()");

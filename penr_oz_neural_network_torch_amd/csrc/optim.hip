@@ -45,6 +45,28 @@ PZ_DEV void block_reduce_add(double v[4], double* dst) {
   }
 }
 
+// one parameter's update: returns the new value; m / v are Adam's moments (in and out)
+template <bool ADAM>
+PZ_DEV float update_one(const OptArgs& a, float p0, float graw, float l2x2, float step_size, float& m, float& v) {
+  const float g = graw * a.grad_scale + l2x2 * p0;
+  if constexpr (ADAM) {
+    m = m + (1.f - a.beta1) * (g - m);
+    v = v * a.beta2 + (1.f - a.beta2) * g * g;
+    const float denom = sqrtf(v) / a.bias_c2_sqrt + a.eps;
+    return p0 - step_size * (m / denom);
+  } else {
+    return p0 - a.lr * g;
+  }
+}
+
+PZ_DEV void add_stats(double st[4], float p0, float p1) {
+  const double d = static_cast<double>(p1 - p0);
+  st[0] += d; st[1] += d * d; st[2] += p1; st[3] += static_cast<double>(p1) * p1;
+}
+
+// Segments whose offset and length are multiples of 4 (every dense weight: ParamStore aligns
+// offsets to 64) move 16 B per lane per stream — p, g, m, v in and p, m, v, shadow out — so a
+// wave instruction covers 1 KiB; other segments (odd-sized biases) take the scalar loop.
 template <bool ADAM>
 __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   if (a.hp != nullptr) {
@@ -59,40 +81,79 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   const bool weight = seg.is_weight != 0;
   const float l2x2 = weight ? 2.f * a.l2_lambda : 0.f;
   const float step_size = a.lr / a.bias_c1;
+  const bool stats = seg.stat_slot >= 0;
   double st[4] = {0.0, 0.0, 0.0, 0.0};
 
+  if (((seg.offset | seg.numel) & 3) == 0) {
 #pragma unroll
-  for (int u = 0; u < kPerThread; ++u) {
-    const int64_t li = local0 + static_cast<int64_t>(u) * kThreads + threadIdx.x;
-    if (li >= seg.numel) break;
-    const int64_t gi = seg.offset + li;
-    const float p0 = a.params[gi];
-    const float graw = seg.grad16 != nullptr ? bf2f(seg.grad16[li]) : a.grads[gi];
-    const float g = graw * a.grad_scale + l2x2 * p0;
-    float p1;
-    if constexpr (ADAM) {
-      float m = a.exp_avg[gi];
-      float v = a.exp_avg_sq[gi];
-      m = m + (1.f - a.beta1) * (g - m);
-      v = v * a.beta2 + (1.f - a.beta2) * g * g;
-      const float denom = sqrtf(v) / a.bias_c2_sqrt + a.eps;
-      p1 = p0 - step_size * (m / denom);
-      a.exp_avg[gi] = m;
-      a.exp_avg_sq[gi] = v;
-    } else {
-      p1 = p0 - a.lr * g;
+    for (int u = 0; u < kPerThread / 4; ++u) {
+      const int64_t li = local0 + (static_cast<int64_t>(u) * kThreads + threadIdx.x) * 4;
+      if (li >= seg.numel) break;
+      const int64_t gi = seg.offset + li;
+      const float4 p0 = *reinterpret_cast<const float4*>(a.params + gi);
+      float g[4];
+      if (seg.grad16 != nullptr) {
+        const uint2 q = *reinterpret_cast<const uint2*>(seg.grad16 + li);
+        g[0] = bf2f(q.x & 0xFFFF); g[1] = bf2f(q.x >> 16); g[2] = bf2f(q.y & 0xFFFF); g[3] = bf2f(q.y >> 16);
+      } else {
+        const float4 q = *reinterpret_cast<const float4*>(a.grads + gi);
+        g[0] = q.x; g[1] = q.y; g[2] = q.z; g[3] = q.w;
+        if (seg.zero_grad) *reinterpret_cast<float4*>(a.grads + gi) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m;
+      if constexpr (ADAM) {
+        m = *reinterpret_cast<const float4*>(a.exp_avg + gi);
+        v = *reinterpret_cast<const float4*>(a.exp_avg_sq + gi);
+      }
+      float4 p1;
+      p1.x = update_one<ADAM>(a, p0.x, g[0], l2x2, step_size, m.x, v.x);
+      p1.y = update_one<ADAM>(a, p0.y, g[1], l2x2, step_size, m.y, v.y);
+      p1.z = update_one<ADAM>(a, p0.z, g[2], l2x2, step_size, m.z, v.z);
+      p1.w = update_one<ADAM>(a, p0.w, g[3], l2x2, step_size, m.w, v.w);
+      if constexpr (ADAM) {
+        *reinterpret_cast<float4*>(a.exp_avg + gi) = m;
+        *reinterpret_cast<float4*>(a.exp_avg_sq + gi) = v;
+      }
+      *reinterpret_cast<float4*>(a.params + gi) = p1;
+      if (seg.shadow != nullptr) {
+        if (seg.shadow_dtype == DT_BF16)
+          *reinterpret_cast<uint2*>(static_cast<uint16_t*>(seg.shadow) + li) =
+              make_uint2(pack_bf2(p1.x, p1.y), pack_bf2(p1.z, p1.w));
+        else
+          *reinterpret_cast<float4*>(static_cast<float*>(seg.shadow) + li) = p1;
+      }
+      if (stats) {
+        add_stats(st, p0.x, p1.x); add_stats(st, p0.y, p1.y); add_stats(st, p0.z, p1.z); add_stats(st, p0.w, p1.w);
+      }
     }
-    a.params[gi] = p1;
-    if (seg.shadow != nullptr) {
-      if (seg.shadow_dtype == DT_BF16) static_cast<uint16_t*>(seg.shadow)[li] = f2bf(p1);
-      else static_cast<float*>(seg.shadow)[li] = p1;
-    }
-    if (seg.stat_slot >= 0) {
-      const double d = static_cast<double>(p1 - p0);
-      st[0] += d; st[1] += d * d; st[2] += p1; st[3] += static_cast<double>(p1) * p1;
+  } else {
+#pragma unroll
+    for (int u = 0; u < kPerThread; ++u) {
+      const int64_t li = local0 + static_cast<int64_t>(u) * kThreads + threadIdx.x;
+      if (li >= seg.numel) break;
+      const int64_t gi = seg.offset + li;
+      const float p0 = a.params[gi];
+      const float graw = seg.grad16 != nullptr ? bf2f(seg.grad16[li]) : a.grads[gi];
+      if (seg.zero_grad) a.grads[gi] = 0.f;
+      float m = 0.f, v = 0.f;
+      if constexpr (ADAM) {
+        m = a.exp_avg[gi];
+        v = a.exp_avg_sq[gi];
+      }
+      const float p1 = update_one<ADAM>(a, p0, graw, l2x2, step_size, m, v);
+      if constexpr (ADAM) {
+        a.exp_avg[gi] = m;
+        a.exp_avg_sq[gi] = v;
+      }
+      a.params[gi] = p1;
+      if (seg.shadow != nullptr) {
+        if (seg.shadow_dtype == DT_BF16) static_cast<uint16_t*>(seg.shadow)[li] = f2bf(p1);
+        else static_cast<float*>(seg.shadow)[li] = p1;
+      }
+      if (stats) add_stats(st, p0, p1);
     }
   }
-  if (seg.stat_slot >= 0 && a.stats != nullptr) block_reduce_add(st, a.stats + 4 * seg.stat_slot);
+  if (stats && a.stats != nullptr) block_reduce_add(st, a.stats + 4 * seg.stat_slot);
 }
 
 __global__ void __launch_bounds__(kThreads) segment_stats_kernel(const float* __restrict__ params,
@@ -142,7 +203,10 @@ __global__ void step_finalize_kernel(FinalizeArgs a) {
   if (threadIdx.x == 0) {
     double loss = 0.0;
     if (a.loss != nullptr) {
-      for (int k = 0; k < a.loss_slots; ++k) loss += static_cast<double>(a.loss[k]);
+      for (int k = 0; k < a.loss_slots; ++k) {
+        loss += static_cast<double>(a.loss[k]);
+        a.loss[k] = 0.f;  // ready for the next step's head
+      }
       loss /= a.loss_div;
     }
     if (a.epoch < a.n_costs) a.costs[a.epoch] = static_cast<float>(loss + static_cast<double>(a.l2) * l2sum);

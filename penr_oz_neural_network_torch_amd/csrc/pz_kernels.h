@@ -80,13 +80,15 @@ struct OptSegment {
   int stat_slot;        // index into stats (4 doubles per slot), -1 = none
   void* shadow;         // optional low-precision copy written after the update
   int shadow_dtype;
+  int zero_grad;        // accumulated gradient (atomics / colsums): reset to 0 once read, so
+                        // the next step needs no separate zeroing pass
   const uint16_t* grad16;  // optional bf16 gradient of this segment (data parallel: the GEMM
                            // writes it and RCCL reduces it in bf16); replaces grads[offset..]
 };
 
 struct OptArgs {
   float* params;
-  const float* grads;
+  float* grads;                // read; zero_grad segments are reset to 0
   float* exp_avg;
   float* exp_avg_sq;
   const OptSegment* segments;  // device array
@@ -113,7 +115,7 @@ hipError_t segment_stats(const float* params, const OptSegment* segments, const 
                          int total_blocks, double* stats, hipStream_t s);
 
 struct FinalizeArgs {
-  const float* loss;        // accumulated loss (summed over ranks when data parallel)
+  float* loss;              // accumulated loss (summed over ranks when data parallel); reset to 0
   int loss_slots;           // loss[0..loss_slots) are summed (the heads spread their block adds)
   float loss_div;           // world size
   double* stats_prev;       // [nslots][4] stats of the weights used by this step (zeroed afterwards)

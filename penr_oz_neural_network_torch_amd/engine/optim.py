@@ -57,7 +57,7 @@ class FusedOptimizer:
         self.segments_p = [torch.ops.pz.pack_segments(
             [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
             [slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
-            [self.grads16.get(s.offset) for s in segs]).to(dev) for sh in shadow_sets]
+            [self.grads16.get(s.offset) for s in segs], self._zero_flags(segs)).to(dev) for sh in shadow_sets]
         self.segments = self.segments_p[0]
         self.block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
         self.num_segments = len(segs)
@@ -94,8 +94,14 @@ class FusedOptimizer:
                 packed = torch.ops.pz.pack_segments(
                     [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
                     [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
-                    [self.grads16.get(s.offset) for s in segs]).to(dev)
+                    [self.grads16.get(s.offset) for s in segs], self._zero_flags(segs)).to(dev)
                 self.groups[(key, parity)] = (packed, block_seg, len(segs), acc)
+
+    def _zero_flags(self, segs) -> list[int]:
+        """Accumulated-gradient segments (biases, batchnorm, embeddings: filled by atomics and
+        column sums) are reset to zero by the update kernel right after it reads them, which
+        replaces a per-step zeroing pass; dense GEMM-written gradients are overwritten anyway."""
+        return [int(s.offset >= self.store.accum_offset) for s in segs]
 
     # ------------------------------------------------------------------------------------
     def _adopt_state(self) -> None:

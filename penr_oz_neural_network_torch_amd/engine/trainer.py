@@ -583,9 +583,6 @@ class FusedTrainer:
         keys = self._keys(epoch)
         ops = torch.ops.pz
         main = torch.cuda.current_stream(self.dev)
-        if self._opt_done is not None:  # the previous step's side-stream updates
-            main.wait_event(self._opt_done)
-            self._opt_done = None
         overlap = self.overlap and not record
         if overlap:
             if not capture:
@@ -593,8 +590,8 @@ class FusedTrainer:
             self._ov = (main, l2, 1.0 / world)
             self._late_stages, self._late_handles = [], []
 
-        # zero the accumulated-gradient region (+ loss slot)
-        self.grads[self.store.accum_offset:].zero_()
+        # (no zeroing pass: the previous step's update kernel reset the accumulated-gradient region
+        # as it read it, and its step_finalize the loss slots)
 
         # ---------------- sample + input
         self._phase("pz.sample")
@@ -610,6 +607,11 @@ class FusedTrainer:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
         rec = {} if record else None
+        # the previous step's side-stream updates (weights, biases, gradient and loss resets) are
+        # first needed here: the sampling above overlaps the cross-stream wait
+        if self._opt_done is not None:
+            main.wait_event(self._opt_done)
+            self._opt_done = None
         self._phase("pz.forward")
         if self.fp8 and not record and self.x8 is not None:  # current-scaled e4m3 input
             ops.amax_abs(self.x_in, self.xamax)
