@@ -128,12 +128,16 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
 // 16-B loads / stores, dropout masks two hashes per 4 elements. A wave's RPW rows are loaded up
 // front (memory-level parallelism), bias-gradient column partials stay in registers and are
 // reduced across the block's waves through LDS once (no LDS atomics: they made this 60 us).
-template <int NCH>
-__global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
+// WAVES = 16 (one row per wave, 1024-thread blocks): the row's reductions are serial shuffle
+// chains, so the kernel is latency-bound and wants many resident waves; the block still owns
+// kHeadRows rows, which keeps the bias-gradient atomics at one per column per 16 rows.
+template <int NCH, int WAVES>
+__global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) {
   a.epi = epi_resolve(a.epi);
-  extern __shared__ float cs_lds[];  // [4][cols] wave partials (when colsum)
-  __shared__ float red[4];
-  constexpr int RPW = kHeadRows / 4;
+  extern __shared__ float cs_lds[];  // [WAVES][cols] wave partials (when colsum)
+  __shared__ float red[WAVES];
+  constexpr int RPW = kHeadRows / WAVES;
+  static_assert(RPW * WAVES == kHeadRows, "rows per block split over the waves");
   const uint16_t* __restrict__ logits = static_cast<const uint16_t*>(a.logits);
   uint16_t* __restrict__ dh = static_cast<uint16_t*>(a.dh);
   uint16_t* __restrict__ probs = static_cast<uint16_t*>(a.probs);
@@ -229,7 +233,17 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
               make_uint4(0, 0, 0, 0);
     }
   }
-  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red, a.loss_slots);
+  if (a.loss != nullptr) {
+    const float v = wave_sum(loss_acc);
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) t += red[w];
+      atomicAdd(a.loss + (a.loss_slots > 1 ? blockIdx.x % a.loss_slots : 0), t);
+    }
+  }
   if (cs_on) {
     float* mine = cs_lds + wave * a.cols;
 #pragma unroll
@@ -238,8 +252,10 @@ __global__ void __launch_bounds__(256) xent_head_bf16_kernel(XentArgs a) {
 #pragma unroll
         for (int e = 0; e < 8; ++e) mine[(lane + 64 * j) * 8 + e] = cs[j][e];
     __syncthreads();
-    for (int c = threadIdx.x; c < a.cols; c += 256) {
-      const float t = cs_lds[c] + cs_lds[a.cols + c] + cs_lds[2 * a.cols + c] + cs_lds[3 * a.cols + c];
+    for (int c = threadIdx.x; c < a.cols; c += WAVES * 64) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) t += cs_lds[w * a.cols + c];
       if (t != 0.f) atomicAdd(a.colsum + c, t);
     }
   }
@@ -449,6 +465,19 @@ hipError_t stage_bwd(const void* g, const void* y, void* dx, int dtype, int64_t 
   return hipGetLastError();
 }
 
+template <int NCH, int W>
+hipError_t launch_xent_bf16(const XentArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  static bool attr = false;  // > 64 KiB of dynamic LDS (W partial rows of up to 2048 columns)
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(xent_head_bf16_kernel<NCH, W>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, W * 512 * NCH * 4);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((xent_head_bf16_kernel<NCH, W>), grid, dim3(W * 64), lds, s, a);
+  return hipGetLastError();
+}
+
 constexpr int kMaxLdsCols = 16384;  // 64 KiB of fp32 column partials
 
 hipError_t xent_head(const XentArgs& in, hipStream_t s) {
@@ -465,16 +494,19 @@ hipError_t xent_head(const XentArgs& in, hipStream_t s) {
                    (a.probs == nullptr || a.ld_probs % 8 == 0) && a.idx_ld % 2 == 0 &&
                    (reinterpret_cast<uintptr_t>(a.logits) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dh) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(a.probs) & 15) == 0;
-  const size_t lds4 = 4 * lds;  // the bf16 kernel keeps one partial row per wave
-  if (vec && a.cols <= 512) hipLaunchKernelGGL(xent_head_bf16_kernel<1>, grid, dim3(256), lds4, s, a);
-  else if (vec && a.cols <= 1024) hipLaunchKernelGGL(xent_head_bf16_kernel<2>, grid, dim3(256), lds4, s, a);
-  else if (vec && a.cols <= 2048) hipLaunchKernelGGL(xent_head_bf16_kernel<4>, grid, dim3(256), lds4, s, a);
+  constexpr int kW = 16;         // waves per bf16 block: one row each
+  const size_t ldsw = kW * lds;  // the bf16 kernel keeps one partial row per wave (up to 128 KiB)
+  hipError_t le = hipSuccess;
+  if (vec && a.cols <= 512) le = launch_xent_bf16<1, kW>(a, grid, ldsw, s);
+  else if (vec && a.cols <= 1024) le = launch_xent_bf16<2, kW>(a, grid, ldsw, s);
+  else if (vec && a.cols <= 2048) le = launch_xent_bf16<4, kW>(a, grid, ldsw, s);
   else {
     PZ_DISPATCH_FLOAT(a.dtype, T, {
       using F = typename MathOf<T>::type;
       hipLaunchKernelGGL((xent_head_kernel<T, F>), grid, dim3(256), lds, s, a);
     });
   }
+  if (le != hipSuccess) return le;
   if (colsum_direct != nullptr && a.dh != nullptr) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
