@@ -56,6 +56,9 @@ int grid_for(int64_t n) {
 // bias-gradient column sums are accumulated in LDS (ds_add_f32) and flushed with ONE global
 // atomic per column per block — per-element global atomics made this kernel 20x slower.
 constexpr int kHeadRows = 16;
+// bf16 CE head: rows per 16-wave block (2 per wave): halves the blocks adding into the same
+// bias-gradient columns, whose contended atomics were half the kernel's time at 16
+constexpr int kBf16HeadRows = 32;
 
 // block loss -> one of `slots` accumulators (the consumer sums them): hundreds of blocks adding
 // to ONE address serialise at L2 (measured: 512 blocks cost the CE head ~10 us)
@@ -130,14 +133,14 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
 // reduced across the block's waves through LDS once (no LDS atomics: they made this 60 us).
 // WAVES = 16 (one row per wave, 1024-thread blocks): the row's reductions are serial shuffle
 // chains, so the kernel is latency-bound and wants many resident waves; the block still owns
-// kHeadRows rows, which keeps the bias-gradient atomics at one per column per 16 rows.
+// kBf16HeadRows rows, which keeps the bias-gradient atomics at one per column per 32 rows.
 template <int NCH, int WAVES>
 __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) {
   a.epi = epi_resolve(a.epi);
   extern __shared__ float cs_lds[];  // [WAVES][cols] wave partials (when colsum)
   __shared__ float red[WAVES];
-  constexpr int RPW = kHeadRows / WAVES;
-  static_assert(RPW * WAVES == kHeadRows, "rows per block split over the waves");
+  constexpr int RPW = kBf16HeadRows / WAVES;
+  static_assert(RPW * WAVES == kBf16HeadRows, "rows per block split over the waves");
   const uint16_t* __restrict__ logits = static_cast<const uint16_t*>(a.logits);
   uint16_t* __restrict__ dh = static_cast<uint16_t*>(a.dh);
   uint16_t* __restrict__ probs = static_cast<uint16_t*>(a.probs);
@@ -152,7 +155,7 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
   bool ok[NCH];
 #pragma unroll
   for (int j = 0; j < NCH; ++j) ok[j] = (lane + 64 * j) * 8 < a.cols;
-  const int row0 = blockIdx.x * kHeadRows + wave * RPW;
+  const int row0 = blockIdx.x * kBf16HeadRows + wave * RPW;
   uint4 raw[RPW][NCH];
   int64_t labels[RPW];  // fetched with the logits: no dependent load inside the row loop
 #pragma unroll
@@ -494,12 +497,13 @@ hipError_t xent_head(const XentArgs& in, hipStream_t s) {
                    (a.probs == nullptr || a.ld_probs % 8 == 0) && a.idx_ld % 2 == 0 &&
                    (reinterpret_cast<uintptr_t>(a.logits) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dh) & 15) == 0 &&
                    (reinterpret_cast<uintptr_t>(a.probs) & 15) == 0;
+  const dim3 grid16((a.rows + kBf16HeadRows - 1) / kBf16HeadRows);
   constexpr int kW = 16;         // waves per bf16 block: one row each
   const size_t ldsw = kW * lds;  // the bf16 kernel keeps one partial row per wave (up to 128 KiB)
   hipError_t le = hipSuccess;
-  if (vec && a.cols <= 512) le = launch_xent_bf16<1, kW>(a, grid, ldsw, s);
-  else if (vec && a.cols <= 1024) le = launch_xent_bf16<2, kW>(a, grid, ldsw, s);
-  else if (vec && a.cols <= 2048) le = launch_xent_bf16<4, kW>(a, grid, ldsw, s);
+  if (vec && a.cols <= 512) le = launch_xent_bf16<1, kW>(a, grid16, ldsw, s);
+  else if (vec && a.cols <= 1024) le = launch_xent_bf16<2, kW>(a, grid16, ldsw, s);
+  else if (vec && a.cols <= 2048) le = launch_xent_bf16<4, kW>(a, grid16, ldsw, s);
   else {
     PZ_DISPATCH_FLOAT(a.dtype, T, {
       using F = typename MathOf<T>::type;
