@@ -293,13 +293,25 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(m));
     }
   }
-  if (!FWD_ONLY && p.colsum != nullptr) {  // fire-and-forget: nothing waits for them in this kernel
+  if (!FWD_ONLY && p.colsum != nullptr) {
+    // the WM waves that share a column range meet in LDS (the image has been read out), then ONE
+    // atomic per tile column, 64 consecutive columns per wave instruction: the full-rate atomic
+    // shape (256 contiguous bytes), instead of 4-lane instructions from every wave (measured:
+    // the column sums cost 11% of the K = 1024 dX GEMM that way)
+    PZ_LDS float* part = (PZ_LDS float*)(smem);  // [WM][BN]
+    __syncthreads();
+    if ((lane & (L::RED - 1)) == 0) {
 #pragma unroll
-    for (int j = 0; j < COLS; ++j) {
-      const int n = n0 + nl0 + L::n_off(j);
+      for (int j = 0; j < COLS; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r)
-        if ((lane & (L::RED - 1)) == 0 && n + r < p.N) atomicAdd(p.colsum + n + r, cs[j][r]);
+        for (int r = 0; r < 4; ++r) part[wm * BN + nl0 + L::n_off(j) + r] = cs[j][r];
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {  // fire-and-forget: nothing waits for them in this kernel
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WM; ++w) s += part[w * BN + c];
+      if (n0 + c < p.N) atomicAdd(p.colsum + n0 + c, s);
     }
   }
 }
