@@ -234,6 +234,7 @@ class FusedTrainer:
         self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "2")))  # first-layer dW under DP
         self.opt.define_groups(gemm_w[1:])
         self._opt_done = None
+        self._opt_params_done = None  # previous step's updates done, its step_finalize maybe not
         self._ov = None
         self._rows = None
         # hipGraph replay of whole steps (single GPU) when a step is launch-bound: PZ_GRAPHS=auto
@@ -550,6 +551,7 @@ class FusedTrainer:
         if self._opt_done is not None:
             main.wait_event(self._opt_done)
             self._opt_done = None
+        self._opt_params_done = None
         if self._ctr_epoch != epoch:
             self.epoch_ctr.fill_(epoch)
         parity = self.parity
@@ -607,11 +609,11 @@ class FusedTrainer:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
         rec = {} if record else None
-        # the previous step's side-stream updates (weights, biases, gradient and loss resets) are
-        # first needed here: the sampling above overlaps the cross-stream wait
+        # the previous step's side-stream updates (weights, biases, gradient resets) are first
+        # needed here: the sampling above overlaps the cross-stream wait; its step_finalize (loss
+        # slot reset) only before the head, so it runs beside this forward
         if self._opt_done is not None:
-            main.wait_event(self._opt_done)
-            self._opt_done = None
+            main.wait_event(self._opt_params_done if self._opt_params_done is not None else self._opt_done)
         self._phase("pz.forward")
         if self.fp8 and not record and self.x8 is not None:  # current-scaled e4m3 input
             ops.amax_abs(self.x_in, self.xamax)
@@ -627,6 +629,10 @@ class FusedTrainer:
             ops.scale_update(self.aamax, self.aqs, 1.25, True)
 
         # ---------------- head
+        if self._opt_done is not None:
+            main.wait_event(self._opt_done)
+            self._opt_done = None
+        self._opt_params_done = None
         self._phase("pz.head")
         g_pre = self._head(last, x, batch, dropout, keys, rec)
 
@@ -649,6 +655,10 @@ class FusedTrainer:
             self._opt_async("rest", late + [handles[-1]], self._late_stages)
             self._ov = None
             with torch.cuda.stream(self.opt_stream):
+                params_ev = None
+                if not capture:
+                    params_ev = torch.cuda.Event()
+                    params_ev.record(self.opt_stream)
                 self.opt.finalize(self.loss_slot, world, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
                 ev = torch.cuda.Event(enable_timing=not capture)
@@ -657,6 +667,7 @@ class FusedTrainer:
                 main.wait_event(ev)
             else:
                 self._opt_done = ev
+                self._opt_params_done = params_ev
                 self._last_event = ev
             self.parity = 1 - self.parity
             self._phase(None)
