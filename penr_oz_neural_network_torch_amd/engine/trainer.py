@@ -234,7 +234,7 @@ class FusedTrainer:
         self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "2")))  # first-layer dW under DP
         self.opt.define_groups(gemm_w[1:])
         self._opt_done = None
-        self._opt_params_done = None  # previous step's updates done, its step_finalize maybe not
+        self._early_done = None  # previous step's side-stream weight updates (layers 2..n) done
         self._ov = None
         self._rows = None
         # hipGraph replay of whole steps (single GPU) when a step is launch-bound: PZ_GRAPHS=auto
@@ -551,7 +551,7 @@ class FusedTrainer:
         if self._opt_done is not None:
             main.wait_event(self._opt_done)
             self._opt_done = None
-        self._opt_params_done = None
+        self._early_done = None
         if self._ctr_epoch != epoch:
             self.epoch_ctr.fill_(epoch)
         parity = self.parity
@@ -609,11 +609,9 @@ class FusedTrainer:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
         rec = {} if record else None
-        # the previous step's side-stream updates (weights, biases, gradient resets) are first
-        # needed here: the sampling above overlaps the cross-stream wait; its step_finalize (loss
-        # slot reset) only before the head, so it runs beside this forward
-        if self._opt_done is not None:
-            main.wait_event(self._opt_params_done if self._opt_params_done is not None else self._opt_done)
+        # the previous step's first-layer / bias update ran on this stream; its side-stream updates
+        # (layers 2..n) are awaited before the first stage that reads them, its step_finalize (loss
+        # slot reset) before the head
         self._phase("pz.forward")
         if self.fp8 and not record and self.x8 is not None:  # current-scaled e4m3 input
             ops.amax_abs(self.x_in, self.xamax)
@@ -622,6 +620,9 @@ class FusedTrainer:
         x = self.x_in
         prev = None
         for st in self.stages:
+            if self._early_done is not None and st.kind == "gemm" and st.seg_w.offset in self._early_keys:
+                main.wait_event(self._early_done)
+                self._early_done = None
             x = self._forward_stage(st, x, batch, dropout, keys, rec)
             prev = st
         last = prev
@@ -632,7 +633,7 @@ class FusedTrainer:
         if self._opt_done is not None:
             main.wait_event(self._opt_done)
             self._opt_done = None
-        self._opt_params_done = None
+        self._early_done = None
         self._phase("pz.head")
         g_pre = self._head(last, x, batch, dropout, keys, rec)
 
@@ -651,14 +652,25 @@ class FusedTrainer:
         handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:], exact=True))
         fin = dict(epoch_ctr=self.epoch_ctr, every=self._plan["every"] if self._plan else 1)
         if overlap:
-            late = list(self._late_handles)
-            self._opt_async("rest", late + [handles[-1]], self._late_stages)
+            # the last update (first-layer weights, biases, batchnorm, embeddings) runs on THIS
+            # stream right behind the last dW: the next step's first GEMM follows it in order (no
+            # cross-stream wait), and it overlaps the side stream's still-running updates instead
+            # of queueing behind them; step_finalize (side) waits for both
+            for h in list(self._late_handles) + [handles[-1]]:
+                self.ctx.wait_one(h)
+            self.opt.step_group("rest", self.grads, l2, 1.0 / world, 1 - self.parity)
+            if self.fp8:
+                for st in self._late_stages:
+                    self._refresh_fp8_weights(st)
             self._ov = None
+            rest_ev = torch.cuda.Event()
+            rest_ev.record(main)
+            early_ev = None
             with torch.cuda.stream(self.opt_stream):
-                params_ev = None
                 if not capture:
-                    params_ev = torch.cuda.Event()
-                    params_ev.record(self.opt_stream)
+                    early_ev = torch.cuda.Event()
+                    early_ev.record(self.opt_stream)
+                self.opt_stream.wait_event(rest_ev)
                 self.opt.finalize(self.loss_slot, world, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
                 ev = torch.cuda.Event(enable_timing=not capture)
@@ -667,7 +679,7 @@ class FusedTrainer:
                 main.wait_event(ev)
             else:
                 self._opt_done = ev
-                self._opt_params_done = params_ev
+                self._early_done = early_ev
                 self._last_event = ev
             self.parity = 1 - self.parity
             self._phase(None)
