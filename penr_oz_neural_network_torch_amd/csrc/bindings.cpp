@@ -311,7 +311,7 @@ void colsum_op(const Tensor& x, const Tensor& out) {
 void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t seed_lo, int64_t seed_hi,
                     const Tensor& out, int64_t rows_valid, const optional<Tensor>& labels_in,
                     const optional<Tensor>& labels_out, const optional<Tensor>& picked,
-                    const optional<Tensor>& epoch) {
+                    const optional<Tensor>& epoch, const optional<Tensor>& data8, const optional<Tensor>& out8) {
   check_dev(data, "data");
   TORCH_CHECK(data.dim() == 2 && out.dim() == 2 && data.stride(1) == 1 && out.stride(1) == 1, "pz::gather_rows: 2-D");
   TORCH_CHECK(out.size(1) == data.size(1), "pz::gather_rows: width mismatch");
@@ -333,16 +333,31 @@ void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t
   a.labels_out = ptr_or_null<int64_t>(labels_out);
   a.picked = ptr_or_null<int64_t>(picked);
   a.epoch_ptr = epoch_counter(epoch);
+  if (out8.has_value() && out8->defined()) {
+    TORCH_CHECK(data8.has_value() && data8->defined(), "pz::gather_rows: out8 needs data8");
+    const Tensor& d8 = *data8;
+    const Tensor& o8 = *out8;
+    TORCH_CHECK(d8.element_size() == 1 && o8.element_size() == 1 && d8.dim() == 2 && o8.dim() == 2 &&
+                    d8.stride(1) == 1 && o8.stride(1) == 1 && d8.size(0) == data.size(0) &&
+                    d8.size(1) == data.size(1) && o8.size(0) == out.size(0) && o8.size(1) == out.size(1),
+                "pz::gather_rows: data8 [n_data, cols] / out8 [rows, cols] 1-byte tables");
+    a.data8 = static_cast<const uint8_t*>(d8.data_ptr());
+    a.ld_data8 = d8.stride(0);
+    a.out8 = static_cast<uint8_t*>(o8.data_ptr());
+    a.ld_out8 = o8.stride(0);
+  }
   PZ_HIP_CHECK(pz::gather_rows(a, cur_stream(data)));
 }
 
 // ------------------------------------------------------------------------------- optimizer
 Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::IntArrayRef is_weight,
                         at::IntArrayRef stat_slot, at::ArrayRef<optional<Tensor>> shadows,
-                        at::ArrayRef<optional<Tensor>> grads16, at::IntArrayRef zero_grad) {
+                        at::ArrayRef<optional<Tensor>> grads16, at::IntArrayRef zero_grad,
+                        at::ArrayRef<optional<Tensor>> amax) {
   const size_t n = offsets.size();
   TORCH_CHECK(numels.size() == n && is_weight.size() == n && stat_slot.size() == n && shadows.size() == n &&
-                  (grads16.empty() || grads16.size() == n) && (zero_grad.empty() || zero_grad.size() == n),
+                  (grads16.empty() || grads16.size() == n) && (zero_grad.empty() || zero_grad.size() == n) &&
+                  (amax.empty() || amax.size() == n),
               "pz::pack_segments: length mismatch");
   Tensor out = at::empty({static_cast<int64_t>(n * sizeof(pz::OptSegment))}, at::TensorOptions().dtype(at::kByte));
   auto* segs = reinterpret_cast<pz::OptSegment*>(out.data_ptr<uint8_t>());
@@ -364,6 +379,10 @@ Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::Int
       TORCH_CHECK(g.is_contiguous() && g.numel() == numels[i] && g.scalar_type() == at::kBFloat16,
                   "pz::pack_segments: bf16 gradient shape");
       s.grad16 = reinterpret_cast<const uint16_t*>(g.data_ptr());
+    }
+    if (!amax.empty() && amax[i].has_value() && amax[i]->defined()) {
+      TORCH_CHECK(amax[i]->scalar_type() == at::kFloat && amax[i]->numel() >= 1, "pz::pack_segments: fp32 amax");
+      s.amax = amax[i]->data_ptr<float>();
     }
     std::memcpy(segs + i, &s, sizeof(s));
   }
@@ -534,15 +553,22 @@ void scale_update_op(const Tensor& amax, const Tensor& qs, double headroom, bool
                                 static_cast<float>(headroom), reset, cur_stream(amax)));
 }
 
-void quant_transpose_op(const Tensor& w, const Tensor& out, const Tensor& qs) {
+void quant_transpose_op(const Tensor& w, const Tensor& out, const Tensor& qs, const optional<Tensor>& amax,
+                        const optional<Tensor>& amax_clear) {
   check_dev(w, "w");
   TORCH_CHECK(w.scalar_type() == at::kFloat && w.dim() == 2 && w.stride(1) == 1, "pz::quant_transpose: fp32 [K,N] w");
   TORCH_CHECK(out.scalar_type() == at::kFloat8_e4m3fn && out.dim() == 2 && out.stride(1) == 1 &&
                   out.size(0) == w.size(1) && out.size(1) == w.size(0) && out.stride(0) % 4 == 0,
               "pz::quant_transpose: out must be e4m3 [N,K]");
+  TORCH_CHECK(qs.scalar_type() == at::kFloat && qs.numel() >= 2, "pz::quant_transpose: fp32 qs[2]");
+  const bool fused = amax.has_value() && amax->defined();
+  TORCH_CHECK(!fused || (amax_clear.has_value() && amax_clear->defined() && amax->scalar_type() == at::kFloat &&
+                         amax_clear->scalar_type() == at::kFloat && amax->numel() >= 1 && amax_clear->numel() >= 1),
+              "pz::quant_transpose: fp32 amax and amax_clear go together");
   PZ_HIP_CHECK(pz::quant_transpose(w.data_ptr<float>(), w.stride(0), static_cast<int>(w.size(0)),
                                    static_cast<int>(w.size(1)), static_cast<uint8_t*>(out.data_ptr()), out.stride(0),
-                                   qs.data_ptr<float>(), cur_stream(w)));
+                                   qs.data_ptr<float>(), fused ? amax->data_ptr<float>() : nullptr,
+                                   fused ? amax_clear->data_ptr<float>() : nullptr, cur_stream(w)));
 }
 
 void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, const optional<Tensor>& amax) {
@@ -643,9 +669,10 @@ TORCH_LIBRARY(pz, m) {
   m.def("softmax_bwd(Tensor g, Tensor y, Tensor(a!) dx) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()");
   m.def("gather_rows(Tensor data, Tensor? indices, int seed_lo, int seed_hi, Tensor(a!) out, int rows_valid, "
-        "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked, Tensor? epoch=None) -> ()");
+        "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked, Tensor? epoch=None, Tensor? data8=None, "
+        "Tensor(d!)? out8=None) -> ()");
   m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows, "
-        "Tensor?[] grads16, int[] zero_grad=[]) -> Tensor");
+        "Tensor?[] grads16, int[] zero_grad, Tensor?[] amax) -> Tensor");
   m.def("optimizer_step(Tensor(a!) params, Tensor(e!) grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
         "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
         "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats, Tensor? hp=None, "
@@ -667,7 +694,7 @@ TORCH_LIBRARY(pz, m) {
         "Tensor(d!)? epoch_ctr=None, int every=1) -> ()");
   m.def("amax_abs(Tensor x, Tensor(a!) amax) -> ()");
   m.def("scale_update(Tensor(a!) amax, Tensor(b!) qs, float headroom, bool reset) -> ()");
-  m.def("quant_transpose(Tensor w, Tensor(a!) out, Tensor qs) -> ()");
+  m.def("quant_transpose(Tensor w, Tensor(a!) out, Tensor(b!) qs, Tensor? amax=None, Tensor(c!)? amax_clear=None) -> ()");
   m.def("quantize_rows(Tensor x, Tensor(a!) out, Tensor qs, Tensor(b!)? amax) -> ()");
   m.def("format_json_array(Tensor t, int level) -> str");
   m.def("repr_double(float x) -> str");

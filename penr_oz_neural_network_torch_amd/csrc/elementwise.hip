@@ -390,6 +390,9 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(GatherArgs a) {
     const double v = row < a.rows_valid ? ldd<Tin>(src, so + c) : 0.0;
     std_<Tout>(dst, dof + c, v);
   }
+  if (a.out8 != nullptr)
+    for (int c = threadIdx.x; c < a.cols; c += 256)
+      a.out8[static_cast<int64_t>(row) * a.ld_out8 + c] = row < a.rows_valid ? a.data8[pick * a.ld_data8 + c] : 0;
 }
 
 // vectorised bf16-output gather (fp32 or bf16 table): one wave per row, 8 elements (one 16-B
@@ -432,6 +435,10 @@ __global__ void __launch_bounds__(256) gather_rows_vec_kernel(GatherArgs a) {
       }
     }
     *reinterpret_cast<uint4*>(d + c) = o;
+    if (a.out8 != nullptr) {  // the same 8 columns of the e4m3 table: one 8-B load / store
+      const uint2 q = valid ? *reinterpret_cast<const uint2*>(a.data8 + pick * a.ld_data8 + c) : make_uint2(0, 0);
+      *reinterpret_cast<uint2*>(a.out8 + static_cast<int64_t>(row) * a.ld_out8 + c) = q;
+    }
   }
 }
 
@@ -574,7 +581,9 @@ hipError_t gather_rows(const GatherArgs& a, hipStream_t s) {
   if (a.rows <= 0) return hipSuccess;
   const bool vec = a.out_dtype == DT_BF16 && (a.data_dtype == DT_F32 || a.data_dtype == DT_BF16) && a.cols % 8 == 0 &&
                    a.ld_data % 8 == 0 && a.ld_out % 8 == 0 && (reinterpret_cast<uintptr_t>(a.data) & 15) == 0 &&
-                   (reinterpret_cast<uintptr_t>(a.out) & 15) == 0;
+                   (reinterpret_cast<uintptr_t>(a.out) & 15) == 0 &&
+                   (a.out8 == nullptr || ((a.ld_data8 | a.ld_out8) % 8 == 0 &&
+                                          ((reinterpret_cast<uintptr_t>(a.data8) | reinterpret_cast<uintptr_t>(a.out8)) & 7) == 0));
   if (vec) {
     if (a.data_dtype == DT_F32)
       hipLaunchKernelGGL(gather_rows_vec_kernel<float>, dim3((a.rows + 3) / 4), dim3(256), 0, s, a);

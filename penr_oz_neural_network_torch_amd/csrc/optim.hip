@@ -59,6 +59,18 @@ PZ_DEV float update_one(const OptArgs& a, float p0, float graw, float l2x2, floa
   }
 }
 
+// max |w_new| of the block -> one atomic per block (non-negative floats order like their bits)
+PZ_DEV void block_amax_commit(float m, float* amax) {
+  __shared__ float part[kThreads / 64];
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < kThreads / 64; ++i) m = fmaxf(m, part[i]);
+    atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(m));
+  }
+}
+
 PZ_DEV void add_stats(double st[4], float p0, float p1) {
   const double d = static_cast<double>(p1 - p0);
   st[0] += d; st[1] += d * d; st[2] += p1; st[3] += static_cast<double>(p1) * p1;
@@ -83,6 +95,7 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   const float step_size = a.lr / a.bias_c1;
   const bool stats = seg.stat_slot >= 0;
   double st[4] = {0.0, 0.0, 0.0, 0.0};
+  float am = 0.f;  // max |w_new| (fp8 weight scaling, seg.amax)
 
   if (((seg.offset | seg.numel) & 3) == 0) {
 #pragma unroll
@@ -125,6 +138,7 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
       if (stats) {
         add_stats(st, p0.x, p1.x); add_stats(st, p0.y, p1.y); add_stats(st, p0.z, p1.z); add_stats(st, p0.w, p1.w);
       }
+      am = fmaxf(am, fmaxf(fmaxf(fabsf(p1.x), fabsf(p1.y)), fmaxf(fabsf(p1.z), fabsf(p1.w))));
     }
   } else {
 #pragma unroll
@@ -151,9 +165,11 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
         else static_cast<float*>(seg.shadow)[li] = p1;
       }
       if (stats) add_stats(st, p0, p1);
+      am = fmaxf(am, fabsf(p1));
     }
   }
   if (stats && a.stats != nullptr) block_reduce_add(st, a.stats + 4 * seg.stat_slot);
+  if (seg.amax != nullptr) block_amax_commit(am, seg.amax);
 }
 
 __global__ void __launch_bounds__(kThreads) segment_stats_kernel(const float* __restrict__ params,

@@ -59,6 +59,12 @@ struct GatherArgs {
   int64_t* labels_out;       // optional [rows]
   int64_t* picked;           // optional [rows]: chosen data index per row
   const int* epoch_ptr;      // graph-replayed steps: seeds += epoch (gather_seed), read on device
+  // optional second table gathered with the same picks: the dataset pre-quantised to e4m3 once
+  // (fp8 policy, static scale) -> the first GEMM's fp8 operand, no per-step quantisation pass
+  const uint8_t* data8;      // [n_data][ld_data8]
+  int64_t ld_data8;
+  uint8_t* out8;             // [rows][ld_out8]
+  int64_t ld_out8;
 };
 
 
@@ -84,6 +90,8 @@ struct OptSegment {
                         // the next step needs no separate zeroing pass
   const uint16_t* grad16;  // optional bf16 gradient of this segment (data parallel: the GEMM
                            // writes it and RCCL reduces it in bf16); replaces grads[offset..]
+  float* amax;             // optional: max |w_new| of the segment is atomically max-ed into *amax
+                           // (fp8 policy: the weight's current-scaling amax, no separate pass)
 };
 
 struct OptArgs {
@@ -194,7 +202,10 @@ hipError_t embedding_bwd(const void* dout, int dout_dtype, const void* idx, int 
 // qs records are {q, s}: T8 = sat(T * q), T ~= T8 * s
 hipError_t amax_abs(const void* x, int dtype, int64_t n, float* amax, hipStream_t s);
 hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool reset, hipStream_t s);
-hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, const float* qs,
+// amax != nullptr: q = 448 / *amax is derived in-kernel (the optimizer reduced it), {q, 1/q} are
+// written to qs, and *amax_clear (the other parity's accumulator) is reset for the next update
+hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, float* qs,
+                           const float* amax, float* amax_clear,
                            hipStream_t s);
 hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
                          const float* qs, float* amax, hipStream_t s);

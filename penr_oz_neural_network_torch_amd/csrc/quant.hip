@@ -64,15 +64,29 @@ __global__ void scale_update_kernel(float* amax, float* qs, int n, float headroo
   if (reset) amax[i] = 0.f;
 }
 
-// W [K][N] (fp32, row stride ldw) -> W8 [N][K] e4m3 (row stride ldo): 64x64 tiles through LDS;
-// the scale comes from the amax already reduced into qs[0] (q).
+// W [K][N] (fp32, row stride ldw) -> W8 [N][K] e4m3 (row stride ldo): 64x64 tiles through LDS.
+// The scale comes from qs[0] (q, already derived from the amax) or, when `amax` is given, from the
+// amax the optimizer reduced while writing W: every block derives q itself, block 0 publishes
+// {q, 1/q} for the GEMM and clears the other parity's accumulator (its last reader, the previous
+// transpose of this weight, finished before this launch in stream order).
 __global__ void __launch_bounds__(256) quant_transpose_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
-                                                              uint8_t* __restrict__ out, int64_t ldo,
-                                                              const float* __restrict__ qs) {
+                                                              uint8_t* __restrict__ out, int64_t ldo, float* qs,
+                                                              const float* amax, float* amax_clear) {
   __shared__ float tile[64][65];
   const int k0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4
-  const float q = qs[0];
+  float q;
+  if (amax != nullptr) {
+    const float am = *amax;
+    q = am > 0.f ? kE4m3Max / am : 1.f;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+      qs[0] = q;
+      qs[1] = 1.f / q;
+      *amax_clear = 0.f;
+    }
+  } else {
+    q = qs[0];
+  }
 #pragma unroll
   for (int r = ty; r < 64; r += 4) {
     const int k = k0 + r, n = n0 + tx;
@@ -144,11 +158,12 @@ hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool rese
   return hipGetLastError();
 }
 
-hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, const float* qs,
-                           hipStream_t s) {
+hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, float* qs,
+                           const float* amax, float* amax_clear, hipStream_t s) {
   if (K <= 0 || N <= 0) return hipSuccess;
+  if (amax != nullptr && amax_clear == nullptr) return hipErrorInvalidValue;
   hipLaunchKernelGGL(quant_transpose_kernel, dim3((N + 63) / 64, (K + 63) / 64), dim3(256), 0, s, w, ldw, K, N, out, ldo,
-                     qs);
+                     qs, amax, amax_clear);
   return hipGetLastError();
 }
 

@@ -54,11 +54,11 @@ class FusedOptimizer:
             starts.append(acc)
             acc += b
         self.total_blocks = acc
-        self.segments_p = [torch.ops.pz.pack_segments(
-            [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
-            [slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
-            [self.grads16.get(s.offset) for s in segs], self._zero_flags(segs)).to(dev) for sh in shadow_sets]
-        self.segments = self.segments_p[0]
+        self.slot_of = slot_of
+        self.shadow_sets = shadow_sets
+        self.amax_sets: list[dict[int, torch.Tensor]] = [{} for _ in shadow_sets]
+        self._segs = segs
+        self._pack_all()
         self.block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
         self.num_segments = len(segs)
         self.nslots = len(self.weight_slots)
@@ -67,8 +67,6 @@ class FusedOptimizer:
         # double-buffered per-slot stats: sum(dw), sum(dw^2), sum(w), sum(w^2)
         self.stats = [torch.zeros(max(1, self.nslots) * 4, device=dev, dtype=torch.float64) for _ in range(2)]
         self.cur = 0
-        self.shadow_sets = shadow_sets
-        self.slot_of = slot_of
         self.groups: dict = {}
         # (hp table, epoch counter) while a hipGraph is being captured: the kernels then read the
         # epoch's lr / bias corrections from the table instead of the baked-in scalars
@@ -90,12 +88,28 @@ class FusedOptimizer:
                 starts.append(acc)
                 acc += b
             block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
-            for parity, sh in enumerate(self.shadow_sets):
-                packed = torch.ops.pz.pack_segments(
-                    [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
-                    [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
-                    [self.grads16.get(s.offset) for s in segs], self._zero_flags(segs)).to(dev)
-                self.groups[(key, parity)] = (packed, block_seg, len(segs), acc)
+            for parity in range(len(self.shadow_sets)):
+                self.groups[(key, parity)] = (self._pack(segs, parity), block_seg, len(segs), acc)
+
+    def _pack(self, segs, parity: int) -> torch.Tensor:
+        sh, am = self.shadow_sets[parity], self.amax_sets[parity]
+        return torch.ops.pz.pack_segments(
+            [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
+            [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
+            [self.grads16.get(s.offset) for s in segs], self._zero_flags(segs),
+            [am.get(s.offset) for s in segs]).to(self.store.device)
+
+    def _pack_all(self) -> None:
+        self.segments_p = [self._pack(self._segs, p) for p in range(len(self.shadow_sets))]
+        self.segments = self.segments_p[0]
+
+    def set_amax(self, amax_sets: list[dict[int, torch.Tensor]]) -> None:
+        """fp8 policy: per parity, segment offset -> fp32 scalar that the update max-es |w_new| into
+        (the weight's current-scaling amax, consumed by the transpose-quantise that follows).
+        Call before define_groups()."""
+        assert len(amax_sets) == len(self.shadow_sets)
+        self.amax_sets = amax_sets
+        self._pack_all()
 
     def _zero_flags(self, segs) -> list[int]:
         """Accumulated-gradient segments (biases, batchnorm, embeddings: filled by atomics and

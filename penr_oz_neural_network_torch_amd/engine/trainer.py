@@ -216,11 +216,17 @@ class FusedTrainer:
             self.aamax = torch.zeros(len(self.stages), device=self.dev)
             self.xqs = torch.ones(2, device=self.dev)                       # first-layer input
             self.xamax = torch.zeros(1, device=self.dev)
+            # weight amax accumulators per shadow parity: the optimizer update max-es |w_new| into
+            # its parity's slot, the transpose-quantise right behind it consumes that slot and
+            # clears the other parity's (no separate amax pass over the fp32 weights)
+            self.wamax2 = torch.zeros(2, len(gemms), device=self.dev)
             for k, st in enumerate(gemms):
                 st.w8_index = k
                 self.w8[st.seg_w.offset] = torch.empty(st.seg_w.shape[1], st.seg_w.shape[0], device=self.dev,
                                                        dtype=torch.float8_e4m3fn)
             self._refresh_fp8_weights()
+            self.opt.set_amax([{st.seg_w.offset: self.wamax2[p % 2, st.w8_index:st.w8_index + 1] for st in gemms}
+                               for p in range(len(self.shadow_sets))])
         # Optimizer overlap: each GEMM weight is updated on a side stream as soon as its gradient
         # bucket is complete (its dW GEMM on one GPU, its all-reduce under DP), while the rest of
         # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
@@ -254,6 +260,7 @@ class FusedTrainer:
         self._drained = 0
         self._record = None
         self.data = None
+        self.data8 = None  # fp8 policy: e4m3 copy of the dataset (first-layer operand)
 
     # ------------------------------------------------------------------------------------
     # data
@@ -354,14 +361,21 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------------------------
     # epilogue specs
-    def _refresh_fp8_weights(self, only: Stage | None = None) -> None:
-        """Current-scaled e4m3 weight copies, transposed to [out, in] (K-contiguous GEMM operand)."""
+    def _refresh_fp8_weights(self, only: Stage | None = None, parity: int | None = None) -> None:
+        """Current-scaled e4m3 weight copies, transposed to [out, in] (K-contiguous GEMM operand).
+        ``parity``: the shadow parity of the optimizer update that just wrote the weights (its amax
+        is already reduced); None: reduce the amax here (initial copies)."""
         ops = torch.ops.pz
         for st in self.stages if only is None else [only]:
             if st.kind != "gemm":
                 continue
             k = st.w8_index
             w = self.store.view(st.seg_w)
+            if parity is not None:
+                p = parity % 2
+                ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k], self.wamax2[p, k:k + 1],
+                                    self.wamax2[1 - p, k:k + 1])
+                continue
             ops.amax_abs(w, self.wamax[k:k + 1])
             ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
             ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
@@ -378,7 +392,7 @@ class FusedTrainer:
             self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
             if self.fp8:
                 for st in stages:
-                    self._refresh_fp8_weights(st)
+                    self._refresh_fp8_weights(st, 1 - self.parity)
 
     def _plan_fp8(self, rows_b: int) -> None:
         """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
@@ -415,6 +429,17 @@ class FusedTrainer:
                 self.x8 = x8
             else:
                 prev.buffers["y8"] = x8
+        self.data8 = None
+        if self.x8 is not None:
+            # first-layer input: the device-resident dataset is quantised to e4m3 ONCE with a static
+            # dataset-wide scale (its amax bounds every minibatch's), and the per-step gather copies
+            # the sampled e4m3 rows next to the bf16 ones: no per-step amax / quantise pass
+            ops = torch.ops.pz
+            self.data8 = torch.empty(self.data.shape, device=self.dev, dtype=torch.float8_e4m3fn)
+            self.xamax.zero_()
+            ops.amax_abs(self.data, self.xamax)
+            ops.scale_update(self.xamax, self.xqs, 1.0, True)
+            ops.quantize_rows(self.data, self.data8, self.xqs, None)
 
     def _plan_relu_masks(self, rows_b: int) -> None:
         """ReLU GEMM stages feeding a GEMM stage keep a 1-bit mask of ``y > 0`` next to ``y``: the
@@ -604,7 +629,7 @@ class FusedTrainer:
             if idx.numel() < batch:
                 raise ValueError(f"need {batch} indices, got {idx.numel()}")
         ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
-                        self.epoch_ctr if capture else None)
+                        self.epoch_ctr if capture else None, self.data8, self.x8 if self.data8 is not None else None)
         if self.tgt is not None:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
@@ -613,10 +638,6 @@ class FusedTrainer:
         # (layers 2..n) are awaited before the first stage that reads them, its step_finalize (loss
         # slot reset) before the head
         self._phase("pz.forward")
-        if self.fp8 and not record and self.x8 is not None:  # current-scaled e4m3 input
-            ops.amax_abs(self.x_in, self.xamax)
-            ops.scale_update(self.xamax, self.xqs, 1.0, True)
-            ops.quantize_rows(self.x_in, self.x8, self.xqs, None)
         x = self.x_in
         prev = None
         for st in self.stages:
@@ -661,7 +682,7 @@ class FusedTrainer:
             self.opt.step_group("rest", self.grads, l2, 1.0 / world, 1 - self.parity)
             if self.fp8:
                 for st in self._late_stages:
-                    self._refresh_fp8_weights(st)
+                    self._refresh_fp8_weights(st, 1 - self.parity)
             self._ov = None
             rest_ev = torch.cuda.Event()
             rest_ev.record(main)
@@ -690,7 +711,7 @@ class FusedTrainer:
         self.opt.step(self.grads, lr, l2, 1.0 / world, 1 - self.parity)
         self.parity = 1 - self.parity
         if self.fp8:
-            self._refresh_fp8_weights()
+            self._refresh_fp8_weights(parity=self.parity)
         self.opt.finalize(self.loss_slot, world, l2, self.costs, epoch, self.ratios, row, **fin)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()

@@ -165,7 +165,8 @@ def test_record_mode_matches_fused_cost():
 
 def test_fp8_training_tracks_bf16():
     """fp8 policy: e4m3 forward GEMMs (current-scaled weights, delayed-scaled activations, e4m3
-    input) with bf16 backward; the loss curve follows the bf16 run of the same model + batches."""
+    input at a static dataset scale) with bf16 backward; the loss curve follows the bf16 run of the
+    same model + batches."""
     sizes = [256, 512, 512, 128]
     algos = ["relu", "relu", "softmax"]
     n, S, steps = 4096, 1024, 12
@@ -188,6 +189,26 @@ def test_fp8_training_tracks_bf16():
             assert "y8" in tr.stages[0].buffers and "y8" in tr.stages[1].buffers
             s_w = tr.wqs[:, 1].cpu()
             assert torch.all(s_w > 0) and torch.all(torch.isfinite(s_w))
+            # weight scales: the amax the optimizer reduced equals max|w| of the current weights,
+            # the other parity's accumulator was cleared, and the e4m3 copy is W^T * q
+            torch.cuda.synchronize()
+            gemms = [st for st in tr.stages if st.kind == "gemm"]
+            amax = torch.stack([tr.store.view(st.seg_w).abs().max() for st in gemms])
+            rows = tr.wamax2.cpu()
+            assert (rows == 0).all(dim=1).sum() == 1, rows
+            assert torch.equal(rows.max(dim=0).values, amax.cpu()), (rows, amax)
+            for st in gemms:
+                q = tr.wqs[st.w8_index, 0]
+                assert torch.allclose(q, 448.0 / amax[st.w8_index], rtol=1e-6)
+                ref = (tr.store.view(st.seg_w) * q).clamp(-448, 448).t()
+                got = tr.w8[st.seg_w.offset].float()
+                assert torch.all((got - ref).abs() <= ref.abs() * 0.0625 + 2 ** -9), st.index
+            # first-layer input: the sampled rows of the once-quantised dataset
+            assert torch.allclose(tr.xqs[0].cpu(), 448.0 / inputs.to(torch.bfloat16).float().abs().max(), rtol=1e-6)
+            picked = tr.picked[:S]
+            assert torch.equal(tr.x8[:S].view(torch.uint8), tr.data8[picked].view(torch.uint8))
+            ref = (tr.x_in[:S].float() * tr.xqs[0]).clamp(-448, 448)
+            assert torch.all((tr.x8[:S].float() - ref).abs() <= ref.abs() * 0.0625 + 2 ** -9)
     bf, f8 = curves["bfloat16"], curves["fp8"]
     assert all(math.isfinite(c) for c in f8)
     assert f8[-1] < f8[0] - 0.05  # it learns
