@@ -240,7 +240,7 @@ class FusedTrainer:
         self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "2")))  # first-layer dW under DP
         self.opt.define_groups(gemm_w[1:])
         self._opt_done = None
-        self._early_done = None  # previous step's side-stream weight updates (layers 2..n) done
+        self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
         self._ov = None
         self._rows = None
         # hipGraph replay of whole steps (single GPU) when a step is launch-bound: PZ_GRAPHS=auto
@@ -635,15 +635,15 @@ class FusedTrainer:
 
         rec = {} if record else None
         # the previous step's first-layer / bias update ran on this stream; its side-stream updates
-        # (layers 2..n) are awaited before the first stage that reads them, its step_finalize (loss
-        # slot reset) before the head
+        # (layers 2..n) and step_finalize (loss-slot / statistics reset) are awaited together
+        # before the first stage that reads a side-updated weight (else before the head)
         self._phase("pz.forward")
         x = self.x_in
         prev = None
         for st in self.stages:
             if self._early_done is not None and st.kind == "gemm" and st.seg_w.offset in self._early_keys:
                 main.wait_event(self._early_done)
-                self._early_done = None
+                self._early_done = self._opt_done = None
             x = self._forward_stage(st, x, batch, dropout, keys, rec)
             prev = st
         last = prev
@@ -686,11 +686,7 @@ class FusedTrainer:
             self._ov = None
             rest_ev = torch.cuda.Event()
             rest_ev.record(main)
-            early_ev = None
             with torch.cuda.stream(self.opt_stream):
-                if not capture:
-                    early_ev = torch.cuda.Event()
-                    early_ev.record(self.opt_stream)
                 self.opt_stream.wait_event(rest_ev)
                 self.opt.finalize(self.loss_slot, world, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
@@ -699,8 +695,12 @@ class FusedTrainer:
             if capture:  # join the side stream into the capture stream
                 main.wait_event(ev)
             else:
+                # ONE cross-stream wait in the next step, before the first GEMM that reads a
+                # side-stream-updated weight: step_finalize (behind this stream's first-layer
+                # update) finishes long before the next step's first GEMM does, and its loss-slot
+                # and statistics resets are then ordered before the head and the updates
                 self._opt_done = ev
-                self._early_done = early_ev
+                self._early_done = ev
                 self._last_event = ev
             self.parity = 1 - self.parity
             self._phase(None)
