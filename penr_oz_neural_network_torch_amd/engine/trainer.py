@@ -239,6 +239,11 @@ class FusedTrainer:
         self._after_dx = os.environ.get("PZ_OPT_AFTER_DX", "1") == "1"  # measured 0.6% faster on one GPU
         self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "2")))  # first-layer dW under DP
         self.opt.define_groups(gemm_w[1:])
+        # PZ_OPT_MERGE=1: the side-stream updates of all layers but the first are queued together
+        # behind the last of their gradients (one event instead of one per layer)
+        self._merge_side = os.environ.get("PZ_OPT_MERGE", "0") == "1"
+        self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
+        self._side_pending: list = []
         self._opt_done = None
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
         self._ov = None
@@ -380,19 +385,22 @@ class FusedTrainer:
             ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
             ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
 
-    def _opt_async(self, key, handles: list, stages: list[Stage]) -> None:
-        """Queue the update of one optimizer group on the side stream behind its gradient(s)."""
+    def _opt_async(self, items: list) -> None:
+        """Queue the updates of optimizer groups ``[(key, handles, stages)]`` on the side stream
+        behind their gradients: ONE event recorded on the compute stream for all of them (each
+        record / cross-stream wait costs the compute stream a few microseconds of idle)."""
         main, l2, scale = self._ov
         ready = torch.cuda.Event()
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             self.opt_stream.wait_event(ready)
-            for h in handles:
-                self.ctx.wait_one(h)
-            self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
-            if self.fp8:
-                for st in stages:
-                    self._refresh_fp8_weights(st, 1 - self.parity)
+            for key, handles, stages in items:
+                for h in handles:
+                    self.ctx.wait_one(h)
+                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
+                if self.fp8:
+                    for st in stages:
+                        self._refresh_fp8_weights(st, 1 - self.parity)
 
     def _plan_fp8(self, rows_b: int) -> None:
         """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
@@ -616,6 +624,7 @@ class FusedTrainer:
                 self.opt.begin_step(lr)
             self._ov = (main, l2, 1.0 / world)
             self._late_stages, self._late_handles = [], []
+            self._side_pending = []
 
         # (no zeroing pass: the previous step's update kernel reset the accumulated-gradient region
         # as it read it, and its step_finalize the loss slots)
@@ -677,6 +686,9 @@ class FusedTrainer:
             # stream right behind the last dW: the next step's first GEMM follows it in order (no
             # cross-stream wait), and it overlaps the side stream's still-running updates instead
             # of queueing behind them; step_finalize (side) waits for both
+            if self._side_pending:  # (merged side updates not flushed by their last layer)
+                self._opt_async(self._side_pending)
+                self._side_pending = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
             self.opt.step_group("rest", self.grads, l2, 1.0 / world, 1 - self.parity)
@@ -889,10 +901,13 @@ class FusedTrainer:
             self._late_stages.append(st)
             self._late_handles.extend(mine)
         if self._ov is not None and own and early:
-            self._opt_async(st.seg_w.offset, mine, [st])
+            self._opt_async([(st.seg_w.offset, mine, [st])])
         out = self._backward_dx(st, before, g, batch, p, keys, rec)
         if self._ov is not None and own and not early:
-            self._opt_async(st.seg_w.offset, mine, [st])
+            self._side_pending.append((st.seg_w.offset, mine, [st]))
+            if not self._merge_side or st.seg_w.offset == self._flush_key:
+                self._opt_async(self._side_pending)
+                self._side_pending = []
         return out
 
     def _backward_dx(self, st: Stage, before: Stage | None, g, batch, p, keys, rec):
