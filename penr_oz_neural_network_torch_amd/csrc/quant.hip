@@ -1,10 +1,12 @@
 // fp8 (OCP e4m3) quantisation kernels for the fp8 precision policy.
 //
 // Per-tensor scaling: a tensor T is stored as T8 = sat(T * q) with q = 448 / (amax * headroom)
-// and multiplied back by s = 1/q inside the GEMM epilogue. Weights use CURRENT scaling (their
-// amax is reduced right before the transpose-quantise that follows every optimizer step);
-// activations use DELAYED scaling: the producing GEMM epilogue records this step's amax and
-// scale_update() turns it into the (q, s) pair of the next step.
+// and multiplied back by s = 1/q inside the GEMM epilogue. Weights use CURRENT scaling: the
+// optimizer update reduces max |w_new| as it writes the weights (optim.hip, seg.amax) and the
+// transpose-quantise that follows derives q from it; activations use DELAYED scaling: the
+// producing GEMM epilogue records this step's amax and scale_update() turns it into the (q, s)
+// pair of the next step; the first layer's input uses one STATIC scale per dataset (the dataset
+// is quantised once, quantize_rows, and the minibatch gather copies its e4m3 rows).
 //
 // Scale records are fp32 device arrays {q, s} so no host sync is ever needed.
 #include "pz_common.h"
