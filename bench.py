@@ -73,7 +73,8 @@ def main(argv=None) -> int:
     world, rank = ctx.world_size, ctx.rank
     if world != args.gpus:
         log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # modulo: a gloo rehearsal (PZ_DIST_BACKEND=gloo) may put several ranks on one GPU
+    local = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     torch.cuda.set_device(local)
     cfg = CONFIGS[args.config]
     batch = args.batch or cfg["batch"]

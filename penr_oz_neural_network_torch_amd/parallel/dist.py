@@ -92,9 +92,10 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # PZ_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
+            backend = os.environ.get("PZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
-            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
             # failure detection: a rank that dies or a collective that hangs must abort the job
             # (RCCL async error handling + the collective watchdog timeout) instead of hanging the
             # node; the REST layer then persists status "Failed" 
