@@ -11,8 +11,16 @@ xGMI) overlapped with backward when launched with torchrun.
 
     python bench.py                                  # 1 GPU, defaults
     python bench.py --gpus 1 --steps 50 --warmup 10
+    python bench.py --gpus 8 --steps 50 --warmup 10  # starts 8 rank processes itself
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
         --master-port 29500 bench.py --gpus 8 --steps 50 --warmup 10
+
+``--gpus N`` without a launcher (no ``WORLD_SIZE`` in the environment) makes this process a pure
+launcher: it starts N fresh rank processes of this script (one per GPU, RCCL over xGMI) before
+anything here touches the GPU, forwards their output and exits with the first failing rank's
+code. With fewer visible GPUs than N the ranks rehearse over gloo, several per GPU (the JSON
+says ``"backend": "gloo"``). A rank whose process group does not hold exactly N ranks exits
+non-zero.
 
 Scaling is WEAK: each GPU processes 8192 samples per step; ``value`` is the whole-job
 samples/s. Data are synthetic (random inputs / labels of the config's shape), weights random.
@@ -53,6 +61,43 @@ def log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
 
+def _launch_ranks(n: int, argv: list[str]) -> int:
+    """Start ``n`` rank processes of this script and wait for them (this process never
+    initialises the GPU: ``device_count`` does not, on this ROCm build)."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
+               LOCAL_WORLD_SIZE=str(n), PZ_BENCH_LAUNCHER="self")
+    visible = torch.cuda.device_count()
+    if visible < n and "PZ_DIST_BACKEND" not in os.environ:
+        log(f"{visible} GPU(s) visible for {n} ranks: rehearsing over gloo with ranks sharing GPUs")
+        env["PZ_DIST_BACKEND"] = "gloo"
+    procs = []
+    for r in range(n):
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                      env=dict(env, RANK=str(r), LOCAL_RANK=str(r))))
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                log(f"rank process {p.pid} exited with {code}; stopping the others")
+                for q in alive:  # our own children only, by exact pid
+                    q.send_signal(signal.SIGTERM)
+        time.sleep(0.05)
+    return rc
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -62,7 +107,10 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: config)")
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--l2", type=float, default=1e-3)
-    args = ap.parse_args(argv)
+    raw = list(sys.argv[1:] if argv is None else argv)
+    args = ap.parse_args(raw)
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        return _launch_ranks(args.gpus, raw)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
@@ -72,7 +120,8 @@ def main(argv=None) -> int:
     ctx = init_from_env()
     world, rank = ctx.world_size, ctx.rank
     if world != args.gpus:
-        log(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but the process group holds {world} rank(s)")
+        return 2
     # modulo: a gloo rehearsal (PZ_DIST_BACKEND=gloo) may put several ranks on one GPU
     local = int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count()
     torch.cuda.set_device(local)
@@ -140,6 +189,8 @@ def main(argv=None) -> int:
             "data": "synthetic (random inputs/labels, random-init weights)",
             "config": {"model": cfg["name"], "global_batch": global_batch, "per_gpu_batch": batch,
                        "seq_len": None, "parallelism": f"dp{world}", "optimizer": cfg["optimizer"],
+                       "dist_backend": ctx.backend or "none", "dist_world_size": world,
+                       "launcher": os.environ.get("PZ_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
                        "dropout": args.dropout, "l2": args.l2, "config_key": args.config},
         }), flush=True)
     if dist.is_initialized():

@@ -10,7 +10,9 @@ existing clients, its test-suite and the dashboard work unchanged:
     DELETE /model/      204
 
 Additions (optional, defaults reproduce the reference): ``dtype`` and ``device`` on model
-creation (``"bfloat16"`` + ``"cuda"`` trains on the MI355X fused engine), ``GET /health``.
+creation (``"bfloat16"`` + ``"cuda"`` trains on the MI355X fused engine), ``GET /health``, and
+multi-GPU data-parallel training of GPU models (``PZ_SERVICE_GPUS=N|auto``: this process is rank 0
+of an N-rank RCCL group whose workers it starts at startup — ``parallel/service.py``).
 Fixes of reference races: the 409 check happens before the model is loaded,
 checkpoint files are replaced atomically (no torn reads from ``/progress/``), and exceptions in a
 background training task are logged instead of vanishing.
@@ -20,6 +22,7 @@ from __future__ import annotations
 import logging
 import os
 from asyncio import Lock, create_task
+from contextlib import asynccontextmanager
 from typing import Dict
 
 from fastapi import Body, FastAPI, HTTPException, Request
@@ -31,13 +34,27 @@ from fastapi.templating import Jinja2Templates
 from pydantic import BaseModel, Field
 
 from neural_net_model import NeuralNetworkModel
+from penr_oz_neural_network_torch_amd.parallel import service
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@asynccontextmanager
+async def lifespan(_: FastAPI):
+    # PZ_SERVICE_GPUS=N|auto: GPU models train data-parallel on N GPUs (rank 0 = this process);
+    # the worker ranks are started here, before anything in this process touches the GPU
+    service.start_from_env()
+    try:
+        yield
+    finally:
+        service.stop()
+
 
 app = FastAPI(
     title="Neural Network Model API",
     description="API to create, serialize, compute output and diagnose of neural network models.",
     version="0.0.1",
+    lifespan=lifespan,
 )
 app.mount("/static", StaticFiles(directory=os.path.join(_HERE, "static")), name="static")
 templates = Jinja2Templates(directory=os.path.join(_HERE, "templates"))
@@ -145,8 +162,9 @@ def health():
     import torch
     gpus = torch.cuda.device_count() if torch.cuda.is_available() else 0
     from penr_oz_neural_network_torch_amd.ops import native
+    group = service.get_group()
     return {"status": "ok", "gpus": gpus, "native": native.has_host_ops(), "training": sorted(
-        k for k, v in model_locks.items() if v.locked())}
+        k for k, v in model_locks.items() if v.locked()), "train_group": group.status() if group else None}
 
 
 @app.post("/model/")
@@ -195,11 +213,14 @@ async def train_model(body: TrainingRequest = Body(...)):
     model = NeuralNetworkModel.deserialize(model_id)
     data = [(item.activation_vector, item.target_vector) for item in body.training_data]
 
+    hp = dict(epochs=body.epochs, learning_rate=body.learning_rate, batch_size=body.batch_size,
+              decay_rate=body.decay_rate, dropout_rate=body.dropout_rate, l2_lambda=body.l2_lambda,
+              beta1=body.adam_beta1, beta2=body.adam_beta2, epsilon=body.adam_epsilon)
+
     async def train():
         async with lock:
-            await run_in_threadpool(model.train, data, body.epochs, body.learning_rate, body.batch_size,
-                                    body.decay_rate, body.dropout_rate, body.l2_lambda, body.adam_beta1,
-                                    body.adam_beta2, body.adam_epsilon)
+            # one thread trains; with a multi-GPU train group up, a GPU model trains on every rank
+            await run_in_threadpool(service.train, model, data, hp)
 
     create_task(train()).add_done_callback(_log_task_failure)
     return JSONResponse(content={"message": f"Training for model {model_id} started asynchronously."},

@@ -193,7 +193,7 @@ class FusedTrainer:
         # the loss stay in the exact fp32 bucket. PZ_GRAD_COMM_DTYPE=fp32 keeps fp32 gradients.
         self.grads16: dict[int, torch.Tensor] = {}
         policy = os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower()
-        if self.ctx.world_size > 1 and self.compute == torch.bfloat16 and policy in ("bf16", "bfloat16"):
+        if self.ctx.enabled and self.compute == torch.bfloat16 and policy in ("bf16", "bfloat16"):
             buf16 = torch.zeros(max(1, self.store.accum_offset), device=self.dev, dtype=torch.bfloat16)
             for st in self.stages:
                 if st.kind == "gemm":
@@ -533,7 +533,7 @@ class FusedTrainer:
 
     def _graphs_possible(self) -> bool:
         # single GPU only (collectives are not captured); no per-phase host syncs (PZ_DEBUG_SYNC)
-        return self.use_graphs and self.overlap and self.ctx.world_size == 1 and not _DEBUG_SYNC
+        return self.use_graphs and self.overlap and not self.ctx.enabled and not _DEBUG_SYNC
 
     def _launch_bound(self, batch: int) -> bool:
         """Replay pays where the host's ~0.17 ms of per-step launches exceeds the GPU time."""
@@ -553,7 +553,10 @@ class FusedTrainer:
         keys, sampler seeds, optimizer hyper-parameters, cost slot, ratio row) are then read from
         the device epoch counter, which every step advances in ``step_finalize``."""
         world = self.ctx.world_size
-        batch = max(1, sample_size // world) if world > 1 else sample_size
+        if sample_size < world:
+            raise ValueError(f"sample size {sample_size} is smaller than the {world} data-parallel ranks")
+        # weak sharding: every rank draws sample_size // world rows (the remainder is not drawn)
+        batch = sample_size // world
         self._ensure_buffers(batch)
         if not hasattr(self, "costs") or epoch >= self.costs.numel():
             self._alloc_progress(epoch + 1)
@@ -885,7 +888,7 @@ class FusedTrainer:
         # Data parallel: the first layer's gradient is the last bucket of the backward and nothing
         # is left to hide its all-reduce behind, so its dW GEMM runs in row chunks and chunk c's
         # all-reduce travels while chunk c+1 is computed (only the last chunk's is exposed)
-        chunks = self._dw_chunks if (before is None and self.ctx.world_size > 1) else 1
+        chunks = self._dw_chunks if (before is None and self.ctx.enabled) else 1
         if chunks < 2 or w_grad.shape[0] % (8 * chunks):
             chunks = 1
         mine = []

@@ -73,6 +73,9 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         self.avg_cost_history = []
         self.stats = None
         self.status = "Created"
+        # data-parallel group this model trains in (None: the process-wide context); set by the
+        # REST service's multi-GPU train group (parallel/service.py) around ``train``
+        self._context = None
 
     # ------------------------------------------------------------------------------------
     # placement
@@ -148,11 +151,13 @@ class NeuralNetworkModel(MultiLayerPerceptron):
     def _optimizer_state(self) -> dict | None:
         return self.optimizer.state_dict() if self.optimizer is not None else None
 
-    @staticmethod
-    def _is_writer() -> bool:
-        """Under data parallelism every rank holds the same model; rank 0 owns the files."""
+    def _dp_context(self):
         from ..parallel.dist import get_context
-        return get_context().rank == 0
+        return self._context if self._context is not None else get_context()
+
+    def _is_writer(self) -> bool:
+        """Under data parallelism every rank holds the same model; rank 0 owns the files."""
+        return self._dp_context().rank == 0
 
     def serialize(self):
         if not self._is_writer():
@@ -326,8 +331,7 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         0's parameters, every rank draws the same global sample from a shared ``sampler`` seed and
         trains on its contiguous shard, and gradients are averaged with one all-reduce before the
         (identical) optimizer step — equivalent to one process training on the whole sample."""
-        from ..parallel.dist import get_context
-        ctx = context or get_context()
+        ctx = context or self._dp_context()
         world, rank = ctx.world_size, ctx.rank
         if world > 1:
             dev = self.params[0].device if self.params else torch.device("cpu")
@@ -338,7 +342,11 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                 seed = torch.randint(0, 2 ** 62, (1,), dtype=torch.int64).to(dev)
                 ctx.broadcast_(seed)
                 sampler = torch.Generator().manual_seed(int(seed.item()))
-        shard = max(1, sample_size // world)
+        if sample_size < world:
+            raise ValueError(f"sample size {sample_size} is smaller than the {world} data-parallel ranks")
+        # contiguous shards of the global sample; the first sample_size % world ranks take one more
+        lo, hi = rank * sample_size // world, (rank + 1) * sample_size // world
+        weight = (hi - lo) / sample_size  # this rank's share of the global mean loss
         activations = None
         every = max(1, epochs // MAX_PROGRESS_POINTS)
         last_saved = time.time()
@@ -348,7 +356,7 @@ class NeuralNetworkModel(MultiLayerPerceptron):
             else:
                 picks = torch.randint(0, len(data), (sample_size,), generator=sampler)
             if world > 1:
-                picks = picks[rank * shard:(rank + 1) * shard]
+                picks = picks[lo:hi]
             sample = [data[i] for i in picks]
             lr = learning_rate * (decay_rate ** epoch)
             if self.optimizer is not None:
@@ -370,7 +378,7 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                     a.retain_grad()
             cost.backward()
             if world > 1:
-                self._average_gradients(ctx)
+                self._average_gradients(ctx, weight)
             if self.optimizer is not None:
                 self.optimizer.step()
             else:
@@ -378,12 +386,12 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                     p.data -= lr * p.grad
             when, value = datetime.now().isoformat(), cost.item()
             if world > 1:
-                value = ctx.all_reduce_scalar(value) / world
+                value = ctx.all_reduce_scalar(value * weight)
             if epoch % every == 0:
                 with torch.no_grad():
                     ratios = [((w - pw).data.std() / (w.data.std() + 1e-8)).item()
                               for pw, w in zip(prev_weights, self.weights)]
-                self._progress_point(when, epoch, value, ratios)
+                self._progress_point(when, epoch, value, ratios, {"world_size": world} if world > 1 else None)
             log.info(f"Model {self.model_id}: Epoch {epoch + 1}, Cost: {value:.4f}")
             if long_training:  # pragma: no cover - timing dependent
                 self._record_training_overall_progress(activations)
@@ -392,12 +400,12 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         if activations is not None:
             self._record_training_overall_progress(activations)
 
-    def _average_gradients(self, ctx) -> None:
-        """Mean of every parameter gradient over the ranks: one flat bucket, one all-reduce."""
+    def _average_gradients(self, ctx, weight: float) -> None:
+        """Global-batch mean of every parameter gradient: each rank's shard-mean gradient weighted
+        by its share of the sample, summed over the ranks in one flat all-reduce."""
         grads = [p.grad for p in self.params]
-        flat = torch.cat([g.reshape(-1) for g in grads])
+        flat = torch.cat([g.reshape(-1) for g in grads]) * weight
         ctx.wait_all([ctx.all_reduce_async(flat, exact=True)])
-        flat /= ctx.world_size
         off = 0
         for g in grads:
             g.copy_(flat[off:off + g.numel()].view_as(g))
@@ -406,7 +414,7 @@ class NeuralNetworkModel(MultiLayerPerceptron):
     def _fused_trainer(self):
         from ..engine.trainer import FusedTrainer, UnsupportedModel
         try:
-            return FusedTrainer(self)
+            return FusedTrainer(self, self._dp_context())
         except UnsupportedModel as e:
             log.info(f"Model {self.model_id}: fused engine unavailable ({e}); training under autograd")
             return None

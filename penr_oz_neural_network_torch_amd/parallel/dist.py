@@ -32,10 +32,17 @@ class DataParallelContext:
     world_size: int = 1
     group: object = None
     comm_dtype: torch.dtype | None = None   # e.g. bfloat16 to halve xGMI bytes (default: fp32)
+    # PZ_FORCE_COMM=1: run every collective even at world size 1 (a 1-rank RCCL communicator), so
+    # the comm-stream / wait ordering of the data-parallel step is exercised on a single GPU
+    force: bool = False
 
     @property
     def enabled(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self.force
+
+    @property
+    def backend(self) -> str | None:
+        return dist.get_backend(self.group) if dist.is_initialized() else None
 
     def all_reduce_async(self, t: torch.Tensor, exact: bool = False):
         """Start a SUM all-reduce of ``t`` in place. ``exact``: never through ``comm_dtype``
@@ -70,7 +77,7 @@ class DataParallelContext:
     def all_reduce_scalar(self, value: float, op=None) -> float:
         if not self.enabled:
             return value
-        dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(self.group) == "nccl" else "cpu"
+        dev = torch.device("cuda", torch.cuda.current_device()) if self.backend == "nccl" else "cpu"
         t = torch.tensor([value], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=op or dist.ReduceOp.SUM, group=self.group)
         return t.item()
@@ -86,11 +93,27 @@ class DataParallelContext:
 _CONTEXT: DataParallelContext | None = None
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def init_from_env(backend: str | None = None) -> DataParallelContext:
-    """Initialise the process group from torchrun's env vars (RANK / WORLD_SIZE / MASTER_*)."""
+    """Initialise the process group from torchrun's env vars (RANK / WORLD_SIZE / MASTER_*).
+
+    ``PZ_FORCE_COMM=1`` brings a group up even at world size 1 (rendezvous on 127.0.0.1) and
+    marks the context ``force``: every bucket all-reduce then really runs through RCCL."""
     global _CONTEXT
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world > 1 and not dist.is_initialized():
+    force = os.environ.get("PZ_FORCE_COMM", "0") == "1"
+    if force and world == 1 and not dist.is_initialized():
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
             # PZ_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
             backend = os.environ.get("PZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
@@ -105,7 +128,7 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
     comm = os.environ.get("PZ_GRAD_COMM_DTYPE")
     comm_dtype = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": None, None: None}.get(comm)
     if dist.is_initialized():
-        _CONTEXT = DataParallelContext(dist.get_rank(), dist.get_world_size(), None, comm_dtype)
+        _CONTEXT = DataParallelContext(dist.get_rank(), dist.get_world_size(), None, comm_dtype, force=force)
     else:
         _CONTEXT = DataParallelContext(0, 1, None, comm_dtype)
     return _CONTEXT

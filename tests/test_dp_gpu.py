@@ -89,3 +89,83 @@ def test_two_rank_step_equals_single_rank(tmp_path, optimizer, comm):
         assert d.mean().item() < (1e-5 if comm == "fp32" else 2e-4)
     else:
         assert d.max().item() < (1e-6 if comm == "fp32" else 1e-4), d.max().item()
+
+
+def _forced_main(rank, comm, out_path):
+    """World size 1 with PZ_FORCE_COMM=1: every gradient bucket goes through a real 1-rank RCCL
+    all-reduce on its comm stream, waited for by the optimizer's stream."""
+    os.environ.update(PZ_FORCE_COMM="1", PZ_GRAD_COMM_DTYPE=comm, MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(_free_port()))
+    if comm == "fp32":  # unchunked first-layer dW (chunks change the split-K choice = rounding)
+        os.environ["PZ_DW_CHUNKS"] = "1"
+    os.environ.pop("WORLD_SIZE", None)
+    from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
+    from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
+    ctx = init_from_env()
+    assert ctx.force and ctx.enabled and ctx.world_size == 1 and ctx.backend == "nccl", ctx
+    model = _build("adam", "bf16")
+    tr = FusedTrainer(model, ctx)
+    assert bool(tr.grads16) == (comm == "bf16")
+    x, y, idx = _data()
+    tr.load_tensors(x, y, seed=3)
+    tr.begin(3)
+    for e in range(3):
+        tr.step(e, 0.01, 2 * B, 0.2, 1e-3, want_ratios=True, record=False, indices=idx)
+    costs = [c for _, c, _, _ in tr.drain()]
+    torch.save({"flat": model._param_store.flat.cpu(), "costs": costs}, out_path)
+    shutdown()
+
+
+@pytest.mark.parametrize("comm", ["fp32", "bf16"])
+def test_forced_rccl_world1_matches_no_comm(tmp_path, comm):
+    out = str(tmp_path / "forced.pt")
+    mp.start_processes(_forced_main, args=(comm, out), nprocs=1, start_method="spawn")
+    got = torch.load(out, weights_only=True)
+    from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
+    from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
+    model = _build("adam", "bf16")
+    tr = FusedTrainer(model, DataParallelContext())
+    x, y, idx = _data()
+    tr.load_tensors(x, y, seed=3)
+    tr.begin(3)
+    for e in range(3):
+        tr.step(e, 0.01, 2 * B, 0.2, 1e-3, want_ratios=True, record=False, indices=idx)
+    costs = [c for _, c, _, _ in tr.drain()]
+    flat = model._param_store.flat.cpu()
+    if comm == "fp32":
+        # a 1-rank fp32 all-reduce is the identity; what remains is the run-to-run order of the
+        # bias-gradient column-sum atomics (fp32), which Adam turns into ~lr-sized flips only on
+        # near-zero gradients
+        for a, b in zip(got["costs"], costs):
+            assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (got["costs"], costs)
+        d = (got["flat"] - flat).abs()
+        frac = (d > 0).double().mean().item()
+        assert d.mean().item() < 1e-6 and (d > 1e-3).double().mean().item() < 1e-3, (d.max().item(), frac)
+    else:  # bf16 gradient buckets: one rounding of each dense weight gradient
+        for a, b in zip(got["costs"], costs):
+            assert abs(a - b) < 2e-3 * max(1.0, abs(b))
+        d = (got["flat"] - flat).abs()
+        assert d.mean().item() < 2e-4 and (d > 1e-3).double().mean().item() < 2e-2
+
+
+def test_bench_launches_its_own_ranks(tmp_path):
+    """`bench.py --gpus 2` with no launcher starts 2 rank processes itself (on a 1-GPU box they
+    rehearse over gloo, sharing the GPU) and reports the process group's real size."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--batch", "1024"], capture_output=True, text=True, timeout=300, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(line) == 1, r.stdout
+    out = json.loads(line[0])
+    assert out["n_gpus"] == 2 and out["config"]["dist_world_size"] == 2
+    assert out["config"]["dist_backend"] in ("gloo", "nccl") and out["config"]["launcher"] == "self"
+    assert out["config"]["global_batch"] == 2048 and out["value"] > 0
+    # a process group that does not hold --gpus ranks is an error, not a relabelled 1-GPU number
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
+                       capture_output=True, text=True, timeout=300, env=dict(env, WORLD_SIZE="1"), cwd=str(tmp_path))
+    assert r.returncode != 0 and "process group holds 1" in r.stderr

@@ -1,0 +1,61 @@
+"""The REST service's multi-rank train group (parallel/service.py) on the CPU: ``PUT /train/``
+drives a 2-rank gloo data-parallel training (this pytest process is rank 0, one worker process
+is started by the app's lifespan) — the code path an 8-GPU node runs over RCCL."""
+import time
+
+import pytest
+from fastapi.testclient import TestClient
+
+import main
+
+
+def _wait(client, model_id, want, timeout=120.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        r = client.get("/progress/", params={"model_id": model_id})
+        assert r.status_code == 200, r.text
+        if r.json()["status"] in want:
+            return r.json()
+        time.sleep(0.05)
+    raise AssertionError(f"{model_id} did not reach {want}")
+
+
+def _group_ready(client, timeout=120.0):
+    t0 = time.time()
+    while time.time() - t0 < timeout:
+        g = client.get("/health").json()["train_group"]
+        assert g is not None
+        if g["ready"]:
+            assert g["healthy"], g
+            return g
+        time.sleep(0.1)
+    raise AssertionError("train group did not come up")
+
+
+def test_train_route_runs_on_two_ranks(models_tmpdir, monkeypatch):
+    monkeypatch.setenv("PZ_SERVICE_GPUS", "2")
+    monkeypatch.setenv("PZ_DIST_BACKEND", "gloo")
+    with TestClient(main.app) as client:
+        g = _group_ready(client)
+        assert g["world_size"] == 2 and g["backend"] == "gloo"
+        r = client.post("/model/", json={"model_id": "dp", "layer_sizes": [4, 8, 2], "optimizer": "adam",
+                                         "activation_algos": ["tanh", "softmax"]})
+        assert r.status_code == 200
+        data = [{"activation_vector": [i % 3, 1, 0, -(i % 2)], "target_vector": [i % 2]} for i in range(64)]
+        r = client.put("/train/", json={"model_id": "dp", "training_data": data, "epochs": 8, "batch_size": 17,
+                                        "learning_rate": 0.05, "decay_rate": 1.0})
+        assert r.status_code == 202
+        prog = _wait(client, "dp", ("Trained", "Failed"))
+        assert prog["status"] == "Trained"
+        assert len(prog["progress"]) == 8 and all(p["world_size"] == 2 for p in prog["progress"])
+        assert client.get("/health").json()["train_group"]["trainings"] == 1
+        # a sample smaller than the group fails on every rank (no hang) and the group survives it
+        r = client.put("/train/", json={"model_id": "dp", "training_data": data, "epochs": 2, "batch_size": 1})
+        assert r.status_code == 202
+        assert _wait(client, "dp", ("Failed",))["status"] == "Failed"
+        g = client.get("/health").json()["train_group"]
+        assert g["healthy"] and g["trainings"] == 1
+        r = client.put("/train/", json={"model_id": "dp", "training_data": data, "epochs": 2, "batch_size": 8})
+        assert r.status_code == 202
+        assert _wait(client, "dp", ("Trained",))["status"] == "Trained"
+        assert client.get("/health").json()["train_group"]["trainings"] == 2
