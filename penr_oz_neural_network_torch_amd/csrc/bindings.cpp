@@ -393,7 +393,8 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
                        const optional<Tensor>& exp_avg_sq, const Tensor& segments, const Tensor& block_seg,
                        int64_t num_segments, int64_t total_blocks, bool adam, double lr, double beta1, double beta2,
                        double eps, double bias_c1, double bias_c2_sqrt, double grad_scale, double l2,
-                       const optional<Tensor>& stats, const optional<Tensor>& hp, const optional<Tensor>& epoch) {
+                       const optional<Tensor>& stats, const optional<Tensor>& hp, const optional<Tensor>& epoch,
+                       int64_t stats_every) {
   check_dev(params, "params");
   TORCH_CHECK(params.scalar_type() == at::kFloat && grads.scalar_type() == at::kFloat, "pz::optimizer_step: fp32 master");
   pz::OptArgs a{};
@@ -416,6 +417,9 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
   a.grad_scale = static_cast<float>(grad_scale);
   a.l2_lambda = static_cast<float>(l2);
   a.stats = ptr_or_null<double>(stats);
+  a.stats_every = static_cast<int>(stats_every);
+  if (stats_every > 1) TORCH_CHECK(epoch.has_value() && epoch->defined(), "pz::optimizer_step: stats_every > 1 needs the epoch counter");
+  if (epoch.has_value() && epoch->defined()) a.epoch_ptr = epoch_counter(epoch);
   if (hp.has_value() && hp->defined()) {
     TORCH_CHECK(hp->scalar_type() == at::kFloat && hp->is_contiguous() && hp->is_cuda(), "pz::optimizer_step: hp table");
     TORCH_CHECK(epoch.has_value(), "pz::optimizer_step: an hp table needs the epoch counter");
@@ -676,7 +680,7 @@ TORCH_LIBRARY(pz, m) {
   m.def("optimizer_step(Tensor(a!) params, Tensor(e!) grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
         "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
         "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats, Tensor? hp=None, "
-        "Tensor? epoch=None) -> ()");
+        "Tensor? epoch=None, int stats_every=1) -> ()");
   m.def("segment_stats(Tensor params, Tensor segments, Tensor block_seg, int num_segments, int total_blocks, "
         "Tensor(a!) stats) -> ()");
   m.def("tensor_moments(Tensor x, int row_len, int rule, float thr, Tensor(a!) out) -> ()");

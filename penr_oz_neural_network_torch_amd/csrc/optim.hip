@@ -10,6 +10,8 @@
 //   bf16 shadow refresh for the next step's MFMA GEMMs                    -> fused store
 // in ONE pass over (p, g, m, v): 16 B/param read + 12 B/param written (+2 B shadow) instead of
 // the reference's ~10 passes. Numerics follow torch.optim.Adam (foreach=False, capturable=False).
+#include <cstdlib>
+
 #include "pz_common.h"
 #include "pz_kernels.h"
 
@@ -28,8 +30,20 @@ PZ_DEV int find_segment(const int64_t* block_seg, int nseg, int block) {
   return lo;
 }
 
-PZ_DEV void block_reduce_add(double v[4], double* dst) {
+PZ_DEV void block_reduce_add(double v[4], double* dst, bool full = true) {
   __shared__ double red[4][kThreads / 64];
+  if (!full) {  // only sum(w^2): one wave reduction, one atomic
+    const double s = wave_sum_d(v[3]);
+    if ((threadIdx.x & 63) == 0) red[3][threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      double t = 0.0;
+#pragma unroll
+      for (int i = 0; i < kThreads / 64; ++i) t += red[3][i];
+      atomicAdd(dst + 3, t);
+    }
+    return;
+  }
 #pragma unroll
   for (int k = 0; k < 4; ++k) v[k] = wave_sum_d(v[k]);
   const int w = threadIdx.x >> 6;
@@ -71,25 +85,28 @@ PZ_DEV void block_amax_commit(float m, float* amax) {
   }
 }
 
-PZ_DEV void add_stats(double st[4], float p0, float p1) {
-  const double d = static_cast<double>(p1 - p0);
-  st[0] += d; st[1] += d * d; st[2] += p1; st[3] += static_cast<double>(p1) * p1;
+// full: the update-ratio sums too (progress epochs only); otherwise just sum(w^2), which the
+// next step's cost needs for its L2 term
+PZ_DEV void add_stats(double st[4], float p0, float p1, bool full) {
+  st[3] += static_cast<double>(p1) * p1;
+  if (full) {
+    const double d = static_cast<double>(p1 - p0);
+    st[0] += d; st[1] += d * d; st[2] += p1;
+  }
 }
 
 // Segments whose offset and length are multiples of 4 (every dense weight: ParamStore aligns
 // offsets to 64) move 16 B per lane per stream — p, g, m, v in and p, m, v, shadow out — so a
 // wave instruction covers 1 KiB; other segments (odd-sized biases) take the scalar loop.
+//
+// Grid: min(total_blocks, kOptMaxResident) workgroups loop over the 4096-element work blocks, so
+// a launch that overlaps the MFMA-bound GEMMs (side stream) gets all its workgroups resident
+// beside the GEMM's instead of queueing behind the GEMM's pending ones.
 template <bool ADAM>
-__global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
-  if (a.hp != nullptr) {
-    const float* h = a.hp + 4 * static_cast<int64_t>(*a.epoch_ptr);
-    a.lr = h[0];
-    a.bias_c1 = h[1];
-    a.bias_c2_sqrt = h[2];
-  }
-  const int seg_id = find_segment(a.block_seg, a.num_segments, blockIdx.x);
+PZ_DEV void optimizer_block(const OptArgs& a, int block, bool full) {
+  const int seg_id = find_segment(a.block_seg, a.num_segments, block);
   const OptSegment seg = a.segments[seg_id];
-  const int64_t local0 = (static_cast<int64_t>(blockIdx.x) - a.block_seg[seg_id]) * kOptElemsPerBlock;
+  const int64_t local0 = (static_cast<int64_t>(block) - a.block_seg[seg_id]) * kOptElemsPerBlock;
   const bool weight = seg.is_weight != 0;
   const float l2x2 = weight ? 2.f * a.l2_lambda : 0.f;
   const float step_size = a.lr / a.bias_c1;
@@ -136,7 +153,8 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
           *reinterpret_cast<float4*>(static_cast<float*>(seg.shadow) + li) = p1;
       }
       if (stats) {
-        add_stats(st, p0.x, p1.x); add_stats(st, p0.y, p1.y); add_stats(st, p0.z, p1.z); add_stats(st, p0.w, p1.w);
+        add_stats(st, p0.x, p1.x, full); add_stats(st, p0.y, p1.y, full);
+        add_stats(st, p0.z, p1.z, full); add_stats(st, p0.w, p1.w, full);
       }
       am = fmaxf(am, fmaxf(fmaxf(fabsf(p1.x), fabsf(p1.y)), fmaxf(fabsf(p1.z), fabsf(p1.w))));
     }
@@ -164,12 +182,29 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
         if (seg.shadow_dtype == DT_BF16) static_cast<uint16_t*>(seg.shadow)[li] = f2bf(p1);
         else static_cast<float*>(seg.shadow)[li] = p1;
       }
-      if (stats) add_stats(st, p0, p1);
+      if (stats) add_stats(st, p0, p1, full);
       am = fmaxf(am, fabsf(p1));
     }
   }
-  if (stats && a.stats != nullptr) block_reduce_add(st, a.stats + 4 * seg.stat_slot);
+  if (stats && a.stats != nullptr) block_reduce_add(st, a.stats + 4 * seg.stat_slot, full);
   if (seg.amax != nullptr) block_amax_commit(am, seg.amax);
+}
+
+template <bool ADAM>
+__global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
+  int epoch = -1;
+  if (a.epoch_ptr != nullptr) epoch = *a.epoch_ptr;
+  if (a.hp != nullptr) {
+    const float* h = a.hp + 4 * static_cast<int64_t>(epoch);
+    a.lr = h[0];
+    a.bias_c1 = h[1];
+    a.bias_c2_sqrt = h[2];
+  }
+  const bool full = a.stats_every == 1 || (a.stats_every > 1 && (epoch < 0 || epoch % a.stats_every == 0));
+  for (int b = blockIdx.x; b < a.total_blocks; b += gridDim.x) {
+    optimizer_block<ADAM>(a, b, full);
+    __syncthreads();  // the block reductions reuse their LDS slots
+  }
 }
 
 __global__ void __launch_bounds__(kThreads) segment_stats_kernel(const float* __restrict__ params,
@@ -242,8 +277,13 @@ hipError_t step_finalize(const FinalizeArgs& a, hipStream_t s) {
 
 hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
   if (a.total_blocks <= 0) return hipSuccess;
-  if (a.adam) hipLaunchKernelGGL(optimizer_kernel<true>, dim3(a.total_blocks), dim3(kThreads), 0, s, a);
-  else hipLaunchKernelGGL(optimizer_kernel<false>, dim3(a.total_blocks), dim3(kThreads), 0, s, a);
+  static const int max_grid = [] {  // PZ_OPT_GRID: resident workgroups (0 = one per work block)
+    const char* e = getenv("PZ_OPT_GRID");
+    return e ? atoi(e) : 0;
+  }();
+  const int grid = max_grid > 0 && max_grid < a.total_blocks ? max_grid : a.total_blocks;
+  if (a.adam) hipLaunchKernelGGL(optimizer_kernel<true>, dim3(grid), dim3(kThreads), 0, s, a);
+  else hipLaunchKernelGGL(optimizer_kernel<false>, dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError();
 }
 

@@ -114,6 +114,9 @@ struct OptArgs {
   // (filled on the host for the whole run, so eager and replayed steps use identical values)
   const float* hp;
   const int* epoch_ptr;
+  // update-ratio sums (sum dw, sum dw^2, sum w): 1 = this launch, 0 = not (only sum w^2, which the
+  // next step's L2 cost term needs), k > 1 = when the device epoch (*epoch_ptr) % k == 0
+  int stats_every;
 };
 
 constexpr int kOptElemsPerBlock = 4096;

@@ -147,6 +147,10 @@ class FusedOptimizer:
                 st["step"].fill_(float(self.step_count))
 
     # ------------------------------------------------------------------------------------
+    # update-ratio sums in the next launches: 1 = yes, 0 = no (sum(w^2) only), k > 1 = on device
+    # epochs divisible by k (graph capture; needs graph_tables)
+    stats_every = 1
+
     def init_stats(self) -> None:
         """sum(w^2) of the current weights into the 'previous' stats buffer (L2 term of step 0)."""
         prev = self.stats[1 - self.cur]
@@ -183,9 +187,12 @@ class FusedOptimizer:
     def _launch(self, grads, segments, block_seg, nseg, nblocks, l2: float, grad_scale: float) -> None:
         lr, b1, b2, eps, bc1, bc2s = self._hp
         hp, ctr = self.graph_tables or (None, None)
+        every = self.stats_every
+        if every > 1 and ctr is None:  # eager: the caller knows whether this is a progress epoch
+            every = 1
         torch.ops.pz.optimizer_step(self.store.flat, grads, self.exp_avg, self.exp_avg_sq, segments, block_seg, nseg,
                                     nblocks, self.adam, lr, b1, b2, eps, bc1, bc2s, grad_scale, l2,
-                                    self.stats[self.cur], hp, ctr)
+                                    self.stats[self.cur], hp, ctr, every)
 
     def finalize(self, loss: torch.Tensor | None, world: int, l2: float, costs: torch.Tensor, epoch: int,
                  ratios: torch.Tensor, ratio_row: int, epoch_ctr: torch.Tensor | None = None, every: int = 1) -> None:

@@ -231,7 +231,10 @@ class FusedTrainer:
         # bucket is complete (its dW GEMM on one GPU, its all-reduce under DP), while the rest of
         # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
         self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
-        self.opt_stream = torch.cuda.Stream(device=self.dev) if self.overlap else None
+        # PZ_OPT_PRIO=-1: the side stream at high priority (its workgroups are dispatched ahead of
+        # a GEMM's pending ones)
+        prio = int(os.environ.get("PZ_OPT_PRIO", "0"))
+        self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
         # one launch per GEMM weight except the first layer's, which comes last anyway and
         # shares the final launch with the small accumulated parameters (biases, BN, embedding)
         gemm_w = [st.seg_w.offset for st in self.stages if st.kind == "gemm"]
@@ -624,6 +627,8 @@ class FusedTrainer:
         ops = torch.ops.pz
         main = torch.cuda.current_stream(self.dev)
         overlap = self.overlap and not record
+        # update-ratio sums only on progress epochs (row >= 0; captured steps: decided on device)
+        self.opt.stats_every = (self._plan["every"] if self._plan else 1) if row == -2 else (1 if row >= 0 else 0)
         if overlap:
             if not capture:
                 self.opt.begin_step(lr)
