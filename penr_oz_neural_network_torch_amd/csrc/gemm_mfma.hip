@@ -34,16 +34,29 @@
 namespace pz {
 namespace {
 
-constexpr int kBK = 32;  // K depth of one ring slot
+constexpr int kBK = 32;  // K depth of one ring slot (BK64 variants: two of these per slot)
 
-// K-contiguous slot [rows][32]: 64-B rows = 4 chunks; chunk XOR for conflict-free ds_read_b128
-// under the gfx950 b128 lane grouping (row groups of 4 rows map to permutation {0,2,3,1})
-PZ_DEV int swz_kc(int row) { return (120 >> (2 * ((row >> 2) & 3))) & 3; }
+// Per-variant ring geometry: VAR 20/21 stage 64-deep K steps into two 64 KiB slots (one MFMA
+// interval = 64 MFMAs per wave, half the barriers per FLOP of the 32-deep ring)
+template <int VAR> constexpr int var_bk() { return (VAR == 20 || VAR == 21) ? 64 : 32; }
+template <int VAR> constexpr int var_ns() { return VAR == 5 ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4); }
+
+// K-contiguous slot [rows][BK]. BK 32: 64-B rows = 4 chunks; chunk XOR for conflict-free
+// ds_read_b128 under the gfx950 b128 lane grouping (row groups of 4 rows map to permutation
+// {0,2,3,1}). BK 64: 128-B rows = 8 chunks, chunk ^= (row >> 1) & 7: every b128 lane group (16
+// rows x one chunk column, two rows per 256-B bank row) hits 16 distinct 16-B bank slots, and an
+// LDS-DMA instruction's 8 lanes per row still fetch one whole 128-B line.
+template <int BK = 32>
+PZ_DEV int swz_kc(int row) {
+  if constexpr (BK == 64) return (row >> 1) & 7;
+  else return (120 >> (2 * ((row >> 2) & 3))) & 3;
+}
 // M/N-contiguous slot [32][R]: chunk XOR so a half-wave's transposed reads hit 16 distinct slots
 PZ_DEV int swz_mn(int krow) { return ((krow & 3) | (((krow >> 3) & 1) << 2)) << 1; }
 
-template <int BM, int BN, int WM, int WN, int NS_ = 4>
+template <int BM, int BN, int WM, int WN, int NS_ = 4, int BK_ = 32>
 struct Cfg {
+  static constexpr int BK = BK_;
   // ring depth in 32-deep K slots. Measured on the step's GEMMs: 5 slots for 256x256 (160 KiB)
   // and 6 for 256x128 are 2-4% SLOWER than 4 (the DMA stream is throughput-, not latency-bound),
   // and 5 slots for 128x128 drop it to one workgroup per CU (-20%).
@@ -54,16 +67,16 @@ struct Cfg {
   static constexpr int WTN = BN / WN;
   static constexpr int TM = WTM / 16;
   static constexpr int TN = WTN / 16;
-  static constexpr int A_BYTES = BM * kBK * 2;
-  static constexpr int B_BYTES = BN * kBK * 2;
+  static constexpr int A_BYTES = BM * BK * 2;
+  static constexpr int B_BYTES = BN * BK * 2;
   static constexpr int SLOT_BYTES = A_BYTES + B_BYTES;
-  static constexpr int LDS_BYTES = NS * SLOT_BYTES;
+  static constexpr int LDS_BYTES = NS * SLOT_BYTES + 256;  // + L2-prefetch sink (VAR 24)
   static constexpr int GA = A_BYTES / 1024 / NW;  // LDS-DMA instructions per wave per slot
   static constexpr int GB = B_BYTES / 1024 / NW;
   static constexpr int G = GA + GB;
   static_assert(TM >= 1 && TN >= 1, "wave tile must hold at least one 16x16 MFMA tile");
   static_assert(GA >= 1 && GB >= 1 && GA * 1024 * NW == A_BYTES && GB * 1024 * NW == B_BYTES, "stage split");
-  static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+  static_assert(LDS_BYTES <= 160 * 1024 + 256, "LDS budget");
 };
 
 // LDS-DMA of 16 B per lane into wave-uniform LDS byte address `lds` (+ lane*16).
@@ -84,18 +97,36 @@ PZ_DEV void glds16(const void* gsrc, uint32_t lds) {
 }
 
 // Same DMA through the buffer (MUBUF) path: `rs` = raw buffer resource of the operand, `voff`
-// = per-lane byte offset. Out-of-range offsets (>= num_records) read zeros.
+// = per-lane byte offset (loop-invariant: row / column position), `soff` = wave-uniform byte
+// offset of the K step (an SGPR: no per-step vector address math). The operand must span
+// < 4 GiB from its base (checked by the dispatcher).
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
-PZ_DEV void blds16(i32x4_t rs, uint32_t voff, uint32_t lds) {
+PZ_DEV void blds16(i32x4_t rs, uint32_t voff, uint32_t soff, uint32_t lds) {
   uint32_t keep;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
       "s_mov_b32 m0, %3\n\t"
       "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
       "s_mov_b32 m0, %0"
       : "=&s"(keep)
-      : "v"(voff), "s"(rs), "s"(lds)
+      : "v"(voff), "s"(rs), "s"(lds), "s"(soff)
+      : "memory");
+}
+
+// 4-byte LDS-DMA used as an L2 PREFETCH: touching one dword of a 128-B line brings the line into
+// the XCD's L2 several ring steps before the real staging DMA asks for it; the bytes land in a
+// 256-B dummy LDS area nobody reads (no VGPR is written, so nothing can be clobbered)
+PZ_DEV void glds4(const void* gsrc, uint32_t lds) {
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds)
       : "memory");
 }
 
@@ -113,35 +144,40 @@ PZ_DEV uint32_t lds_addr(const PZ_LDS char* p) {
   return __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(p)));
 }
 
-// K-contiguous operand rows [row0, row0+R) x k [k0, k0+32) -> slot [R][32]
-template <int R, int NW, bool BUF = false>
+// K-contiguous operand rows [row0, row0+R) x k [k0, k0+BK) -> slot [R][BK]; NW waves share it
+template <int R, int NW, int BK = 32, bool BUF = false>
 PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
                      PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
-  constexpr int INSTR = R / (16 * NW);  // 16 rows of 64 B per 1-KiB instruction
+  constexpr int CPR = BK / 8;             // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;           // rows per 1-KiB instruction
+  constexpr int INSTR = R / (RPI * NW);
+  static_assert(INSTR >= 1 && INSTR * RPI * NW == R, "K-contiguous stage split");
 #pragma unroll
   for (int i = 0; i < INSTR; ++i) {
-    const int rbase = (wave * INSTR + i) * 16;
-    const int r = rbase + (lane >> 2);
-    const int chunk = (lane & 3) ^ swz_kc(r);
+    const int rbase = (wave * INSTR + i) * RPI;
+    const int r = rbase + lane / CPR;
+    const int chunk = (lane % CPR) ^ swz_kc<BK>(r);
     int gr = row0 + r;
     gr = gr < rows_valid ? gr : rows_valid - 1;
     if constexpr (BUF) {
-      blds16(rs, static_cast<uint32_t>((static_cast<int64_t>(gr) * ld + k0 + chunk * 8) * 2), lds_addr(tile + rbase * 64));
+      const uint32_t voff = (static_cast<uint32_t>(gr) * static_cast<uint32_t>(ld) + chunk * 8) * 2u;
+      blds16(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * 2u), lds_addr(tile + rbase * BK * 2));
     } else {
       const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
-      glds16(src, lds_addr(tile + rbase * 64));
+      glds16(src, lds_addr(tile + rbase * BK * 2));
     }
   }
 }
 
-// M/N-contiguous operand: k rows [k0, k0+32) x cols [col0, col0+R) -> slot [32][R]
-template <int R, int NW, bool BUF = false>
+// M/N-contiguous operand: k rows [k0, k0+BK) x cols [col0, col0+R) -> slot [BK][R]
+template <int R, int NW, int BK = 32, bool BUF = false>
 PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int cols_valid, int k0,
                      PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
   constexpr int ROW_BYTES = R * 2;
   constexpr int CHUNKS = R / 8;
   constexpr int ROWS_PER = 1024 / ROW_BYTES;
-  constexpr int INSTR = (kBK * ROW_BYTES) / (1024 * NW);
+  constexpr int INSTR = (BK * ROW_BYTES) / (1024 * NW);
+  static_assert(INSTR >= 1 && INSTR * 1024 * NW == BK * ROW_BYTES, "M/N-contiguous stage split");
 #pragma unroll
   for (int i = 0; i < INSTR; ++i) {
     const int kbase = (wave * INSTR + i) * ROWS_PER;
@@ -150,7 +186,9 @@ PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int c
     int gc = col0 + chunk * 8;
     gc = gc < cols_valid ? gc : cols_valid - 8;
     if constexpr (BUF) {
-      blds16(rs, static_cast<uint32_t>((static_cast<int64_t>(k0 + kr) * ld + gc) * 2), lds_addr(tile + kbase * ROW_BYTES));
+      const uint32_t voff = (static_cast<uint32_t>(kr) * static_cast<uint32_t>(ld) + gc) * 2u;
+      blds16(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * static_cast<uint32_t>(ld) * 2u),
+             lds_addr(tile + kbase * ROW_BYTES));
     } else {
       const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
       glds16(src, lds_addr(tile + kbase * ROW_BYTES));
@@ -158,9 +196,10 @@ PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int c
   }
 }
 
+template <int BK = 32>
 PZ_DEV i16x8_t frag_kc(const PZ_LDS char* tile, int row, int chunk) {
-  const int slot = chunk ^ swz_kc(row);
-  return *reinterpret_cast<const PZ_LDS i16x8_t*>(tile + row * 64 + slot * 16);
+  const int slot = chunk ^ swz_kc<BK>(row);
+  return *reinterpret_cast<const PZ_LDS i16x8_t*>(tile + row * (BK * 2) + slot * 16);
 }
 
 typedef int i32x8_t __attribute__((ext_vector_type(8)));
@@ -188,6 +227,17 @@ PZ_DEV i16x8_t frag_mn(const PZ_LDS char* tile, int col16, int kbase, int lane) 
 template <int N>
 PZ_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+
+// as wait_newer, with ONE extra (prefetch) operation issued after each step's G stage DMAs
+template <int G, int MAXN>
+PZ_DEV void wait_newer_pf(int n) {
+  if constexpr (MAXN == 0) {
+    wait_vm<1>();
+  } else {
+    if (n >= MAXN) wait_vm<MAXN * G + 1>();
+    else wait_newer_pf<G, MAXN - 1>(n);
+  }
 }
 
 // wait until at most n (<= MAXN) younger ring steps of G LDS-DMA instructions each are in flight
@@ -277,7 +327,9 @@ PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int split, int& tm, i
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
-  using C = Cfg<BM, BN, WM, WN, VAR == 5 ? 3 : 4>;
+  constexpr int BK = var_bk<VAR>();
+  constexpr int KB = BK / 32;  // 32-deep MFMA K blocks per ring slot
+  using C = Cfg<BM, BN, WM, WN, var_ns<VAR>(), BK>;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
 
@@ -299,7 +351,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   constexpr bool F8 = VAR == 8;
   static_assert(!F8 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "fp8: K-contiguous in, bf16 out");
   constexpr int TM8 = C::WTM / 32, TN8 = C::WTN / 32;
-  struct Frags16 { i16x8_t a[C::TM]; i16x8_t b[C::TN]; };
+  struct Frags16 { i16x8_t a[KB][C::TM]; i16x8_t b[KB][C::TN]; };
   struct Frags8 { i32x8_t a[TM8]; i32x8_t b[TN8]; };
   using Frags = std::conditional_t<F8, Frags8, Frags16>;
   using AccT = std::conditional_t<F8, f32x16_t[TM8][TN8], f32x4_t[C::TM][C::TN]>;
@@ -326,11 +378,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
           acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[j], f.a[i], acc[i][j], 0, 0, 0, 127, 0, 127);
     } else {
 #pragma unroll
-      for (int i = 0; i < C::TM; ++i)
+      for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int j = 0; j < C::TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, f.b[j]),
-                                                              __builtin_bit_cast(bf16x8_t, f.a[i]), acc[i][j], 0, 0, 0);
+        for (int i = 0; i < C::TM; ++i)
+#pragma unroll
+          for (int j = 0; j < C::TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, f.b[kb][j]),
+                                                                __builtin_bit_cast(bf16x8_t, f.a[kb][i]), acc[i][j], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
   };
@@ -351,14 +405,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < C::TN; ++j) {
-        if constexpr (B_KC) f.b[j] = frag_kc(tb, wn * C::WTN + j * 16 + (lane & 15), lane >> 4);
-        else f.b[j] = frag_mn<BN>(tb, wn * C::WTN + j * 16, 8 * (lane >> 4), lane);
-      }
+      for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
-      for (int i = 0; i < C::TM; ++i) {
-        if constexpr (A_KC) f.a[i] = frag_kc(ta, wm * C::WTM + i * 16 + (lane & 15), lane >> 4);
-        else f.a[i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, 8 * (lane >> 4), lane);
+        for (int j = 0; j < C::TN; ++j) {
+          if constexpr (B_KC) f.b[kb][j] = frag_kc<BK>(tb, wn * C::WTN + j * 16 + (lane & 15), (lane >> 4) + 4 * kb);
+          else f.b[kb][j] = frag_mn<BN>(tb, wn * C::WTN + j * 16, 8 * (lane >> 4) + 32 * kb, lane);
+        }
+#pragma unroll
+        for (int i = 0; i < C::TM; ++i) {
+          if constexpr (A_KC) f.a[kb][i] = frag_kc<BK>(ta, wm * C::WTM + i * 16 + (lane & 15), (lane >> 4) + 4 * kb);
+          else f.a[kb][i] = frag_mn<BM>(ta, wm * C::WTM + i * 16, 8 * (lane >> 4) + 32 * kb, lane);
+        }
       }
     }
   };
@@ -368,29 +425,62 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  const int nk = p.K / (F8 ? 2 * kBK : kBK) / split;  // K steps of this slice
+  const int nk = p.K / (F8 ? 2 * kBK : BK) / split;  // K steps of this slice
   const int kt0 = slice * nk;
-  constexpr bool BUF = VAR == 6;
+  // LDS-DMA addressing per operand: buffer (MUBUF, 32-bit per-lane offsets from one descriptor)
+  // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
+  // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
+  // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
+  constexpr bool BUF_A = VAR == 6 || (VAR == 25 && !A_KC);
+  constexpr bool BUF_B = VAR == 6 || (VAR == 25 && !B_KC);
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
   const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;
   // (measured, not kept: DMA issued by waves 0-3 only, twice the instructions each: -2..4%)
   constexpr int NWD = C::NW;
-  constexpr int GD = C::G;
-  auto stage_a = [&](int kt) {
+  constexpr bool PF = VAR == 24;      // L2 prefetch kPfAhead steps beyond the staged one
+  constexpr int kPfAhead = 3;
+  constexpr int GD = C::G + (PF ? 1 : 0);
+  // TEAM waves (team-local index tw) issue one operand's DMA of a step
+  auto stage_a_t = [&](int kt, auto team, int tw) {
+    constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
-    if constexpr (A_KC) stage_kc<BM, NWD, BUF>(A, lda, m0, p.M, (kt0 + kt) * kBK, base, wave, lane, rs_a);
-    else stage_mn<BM, NWD, BUF>(A, lda, m0, p.M, (kt0 + kt) * kBK, base, wave, lane, rs_a);
+    if constexpr (A_KC) stage_kc<BM, TEAM, BK, BUF_A>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
+    else stage_mn<BM, TEAM, BK, BUF_A>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
   };
-  auto stage_b = [&](int kt) {
+  auto stage_b_t = [&](int kt, auto team, int tw) {
+    constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (B_KC) stage_kc<BN, NWD, BUF>(B, ldb, n0, p.N, (kt0 + kt) * kBK, base, wave, lane, rs_b);
-    else stage_mn<BN, NWD, BUF>(B, ldb, n0, p.N, (kt0 + kt) * kBK, base, wave, lane, rs_b);
+    if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
+    else stage_mn<BN, TEAM, BK, BUF_B>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
+  };
+  auto stage_a = [&](int kt) { stage_a_t(kt, std::integral_constant<int, NWD>{}, wave); };
+  auto stage_b = [&](int kt) { stage_b_t(kt, std::integral_constant<int, NWD>{}, wave); };
+  auto prefetch = [&](int kt) {  // one dword per 128-B line of step kt's A and B tiles
+    kt = min(kt, nk - 1);
+    const int k0 = (kt0 + kt) * BK;
+    uint32_t sink = lds_addr(smem + C::NS * C::SLOT_BYTES);
+    const int tid = wave * 64 + lane;  // 512 lanes: A lines first, then B lines
+    auto line = [&](const uint16_t* g, int64_t ld, bool kc, int R, int r0, int valid, int idx) -> const void* {
+      if (kc) {  // idx = row
+        int gr = min(r0 + idx, valid - 1);
+        return g + static_cast<int64_t>(gr) * ld + k0;
+      }
+      const int per = (R * 2) / 128;  // lines per k row
+      const int kr = idx / per, c = (idx % per) * 64;
+      return g + static_cast<int64_t>(k0 + kr) * ld + min(r0 + c, valid - 8);
+    };
+    const int na = A_KC ? BM : BK * (BM * 2 / 128);
+    const int nb = B_KC ? BN : BK * (BN * 2 / 128);
+    if (tid < na) glds4(line(A, lda, A_KC, BM, m0, p.M, tid), sink);
+    else if (tid < na + nb) glds4(line(B, ldb, B_KC, BN, n0, p.N, tid - na), sink);
+    else glds4(A, sink);
   };
   auto stage = [&](int kt, int slot) {  // slot == kt % NS
     (void)slot;
     stage_a(kt);
     stage_b(kt);
+    if constexpr (PF) prefetch(kt + kPfAhead);
   };
 
   constexpr int NS = C::NS;
@@ -398,6 +488,41 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // every 128-B line are requested back to back (halved L1->L2 requests, matched hipBLASLt's
   // request count) ran 2-4% SLOWER than the plain ring with DEFER below.
   constexpr bool DEFER = VAR != 4;  // group 0 waits for step t+1 at the END of M_t (+2..6%)
+  if constexpr (BK == 64) {
+    // Ping-pong over 64-deep steps in a 2-slot ring (VAR 20: waves 0-3 issue every DMA in their
+    // read interval; VAR 21: waves 0-3 stage A in their read interval R_t while waves 4-7 stage
+    // B of the same step t+1 at the head of their MFMA interval M_{t-1} — the same barrier
+    // interval). Interval 2t: G0 R_t | G1 M_{t-1}; interval 2t+1: G0 M_t | G1 R_t. Slot (t+1)%2
+    // was last read by G1 in interval 2t-1, so step t+1 is issued in interval 2t and awaited
+    // (vmcnt(0)) at the end of interval 2t+1 by every wave, before G0 reads it in 2t+2.
+    static_assert(C::NW == 8, "BK64 ping-pong needs 8 waves");
+    const int grp = wave >> 2, tw = wave & 3;
+    using T4 = std::integral_constant<int, 4>;
+    auto stage_g0 = [&](int kt) {
+      stage_a_t(kt, T4{}, tw);
+      if constexpr (VAR == 20) stage_b_t(kt, T4{}, tw);
+    };
+    stage(0, 0);
+    wait_vm<0>();
+    barrier();
+    if (grp == 1) {
+      if (VAR == 21 && nk > 1) stage_b_t(1, T4{}, tw);
+      barrier();
+    }
+    for (int t = 0; t < nk; ++t) {
+      if (grp == 0 && t + 1 < nk) stage_g0(t + 1);
+      Frags f;
+      read_frags(t % 2, f);
+      if (grp == 1) wait_vm<0>();  // step t+1 (issued in M_{t-1}) landed before interval 2t+2
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      barrier();
+      if (VAR == 21 && grp == 1 && t + 2 < nk) stage_b_t(t + 2, T4{}, tw);
+      mfma_step(f);
+      if (grp == 0) wait_vm<0>();
+      barrier();
+    }
+    if (grp == 0) barrier();
+  } else {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
     if (s < nk) stage(s, s);
@@ -414,18 +539,22 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     // (t+NS-1)%NS = (t-1)%NS was last read in R_{t-1} and every wave retired those reads
     // (lgkmcnt(0)) before the barrier that precedes R_t of either group.
     const int grp = wave >> 2;
-    wait_newer<GD, NS - 2>(min(nk, NS - 1) - 1);  // step 0 landed
+    auto wait_step = [&](int n) {
+      if constexpr (PF) wait_newer_pf<GD, NS - 2>(n);
+      else wait_newer<GD, NS - 2>(n);
+    };
+    wait_step(min(nk, NS - 1) - 1);  // step 0 landed
     barrier();
     if (grp == 1) barrier();
     for (int t = 0; t < nk; ++t) {
       if (VAR != 2 && t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
-      if (!DEFER || grp == 1) wait_newer<GD, NS - 2>(min(nk - 1, t + NS - 1) - (t + 1));  // step t+1 landed
+      if (!DEFER || grp == 1) wait_step(min(nk - 1, t + NS - 1) - (t + 1));  // step t+1 landed
       Frags f;
       if constexpr (VAR == 3) {  // perf probe: no fragment reads
 #pragma unroll
-        for (int i = 0; i < C::TM; ++i) f.a[i] = i16x8_t{(short)i, 1, 2, 3, 4, 5, 6, (short)t};
+        for (int i = 0; i < C::TM; ++i) f.a[0][i] = i16x8_t{(short)i, 1, 2, 3, 4, 5, 6, (short)t};
 #pragma unroll
-        for (int j = 0; j < C::TN; ++j) f.b[j] = i16x8_t{(short)j, 1, 2, 3, 4, 5, 6, (short)t};
+        for (int j = 0; j < C::TN; ++j) f.b[0][j] = i16x8_t{(short)j, 1, 2, 3, 4, 5, 6, (short)t};
       } else {
         read_frags(t % NS, f);
       }
@@ -435,12 +564,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
         mfma_step(f);
       } else {  // perf probe: no MFMAs (keep the fragments live)
 #pragma unroll
-        for (int i = 0; i < C::TM; ++i) acc[i][0][0] += static_cast<float>(f.a[i][0] + f.b[i % C::TN][1]);
+        for (int i = 0; i < C::TM; ++i) acc[i][0][0] += static_cast<float>(f.a[0][i][0] + f.b[0][i % C::TN][1]);
       }
-      if (DEFER && grp == 0) wait_newer<GD, NS - 2>(min(nk - 1, t + NS - 1) - (t + 1));
+      if (DEFER && grp == 0) wait_step(min(nk - 1, t + NS - 1) - (t + 1));
       barrier();
     }
     if (grp == 0) barrier();
+    if constexpr (PF) wait_vm<0>();  // no prefetch DMA may outlive the workgroup's LDS
   } else
   for (int t = 0; t < nk; ++t) {
     // slot t landed: everything newer than step t (at most NS-2 steps) may stay in flight
@@ -452,6 +582,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     read_frags(t % NS, f);
     mfma_step(f);
   }
+  }  // BK
 
   // ---------------------------------------------------------------- split-K reduction
   // (guide "In-launch split-K reduction": plain slab stores, vmcnt(0), barrier, ONE agent-scope
@@ -544,7 +675,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
-  using C = Cfg<BM, BN, WM, WN, VAR == 5 ? 3 : 4>;
+  using C = Cfg<BM, BN, WM, WN, var_ns<VAR>(), var_bk<VAR>()>;
   auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR>;
   static bool attr_set = false;
   if (!attr_set) {
@@ -566,30 +697,63 @@ hipError_t launch_layout(const GemmArgs& p, hipStream_t s) {
   return launch_cfg<BM, BN, WM, WN, false, false, OutT, AuxT, VAR>(p, s);
 }
 
+#ifndef PZ_GEMM_LAB  // tools/gemm_lab.hip instantiates only the variants it measures
+// buffer-addressed DMA (VAR 6) needs every staged byte within 4 GiB of the operand's base
+bool buffer_ok(const GemmArgs& p) {
+  static const bool off = [] {  // PZ_GEMM_BUF=0: flat-addressed DMA everywhere (A/B experiments)
+    const char* e = getenv("PZ_GEMM_BUF");
+    return e != nullptr && atoi(e) == 0;
+  }();
+  if (off) return false;
+  constexpr int64_t kLim = int64_t(1) << 32;
+  const int64_t ea = (p.a_kc ? static_cast<int64_t>(p.M) : static_cast<int64_t>(p.K)) * p.lda * 2;
+  const int64_t eb = (p.b_kc ? static_cast<int64_t>(p.N) : static_cast<int64_t>(p.K)) * p.ldb * 2;
+  return ea < kLim && eb < kLim;
+}
+
+// PZ_GEMM_P128=1: 128x128 tiles (two workgroups per CU) instead of split-K 256x256 when the
+// shape has at least two such tiles per CU. In isolation fwd [8192,1024] K=4096 runs 950 vs 855
+// TFLOP/s (tools/gemm_lab), but the mlp4 step is 0.9% SLOWER with it (same-box A/B x3), so off.
+bool prefer_128(const GemmArgs& p) {
+  static const bool on = [] {
+    const char* e = getenv("PZ_GEMM_P128");
+    return e != nullptr && atoi(e) == 1;
+  }();
+  if (!on) return false;
+  constexpr int kFill = 240;
+  const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  const int t128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
+  return t256 < kFill && t128 >= 2 * kFill;
+}
+
 template <typename OutT, typename AuxT>
 hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   auto tiles = [&](int bm, int bn) { return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
+  const bool buf = buffer_ok(p);
   constexpr int kFill = 240;  // ~ CU count: a config below this leaves CUs idle
-  static const int forced = [] {  // experiments: PZ_GEMM_TILE=1 (256x256) 2 (256x128) 3 (128x128)
+  // experiments (probe variants live in tools/gemm_lab.hip): PZ_GEMM_TILE=1 (256x256 flat DMA)
+  // 2 (256x128) 3 (128x128) 16 (256x256 buffer DMA)
+  static const int forced = [] {
     const char* e = getenv("PZ_GEMM_TILE");
     return e ? atoi(e) : 0;
   }();
-  if (p.split_k > 1) return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);  // slabs sized for 256x256
+  if (p.split_k > 1) {  // slabs sized for 256x256
+    if (buf) return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
+    return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
+  }
   switch (forced) {
-    case 11: return launch_layout<256, 256, 2, 4, OutT, AuxT, 1>(p, s);
-    case 12: return launch_layout<256, 256, 2, 4, OutT, AuxT, 2>(p, s);
-    case 13: return launch_layout<256, 256, 2, 4, OutT, AuxT, 3>(p, s);
-    case 14: return launch_layout<256, 256, 2, 4, OutT, AuxT, 4>(p, s);
-    case 15: return launch_layout<256, 128, 4, 2, OutT, AuxT, 5>(p, s);
     case 16: return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
     case 1: return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
     case 2: return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
     case 3: return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
     default: break;
   }
-  if (tiles(256, 256) >= kFill) return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
-  if (tiles(256, 128) >= kFill) return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
-  return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
+  // buffer-addressed LDS-DMA (VAR 6; +2..12% on the step's shapes, tools/gemm_lab)
+  if (tiles(256, 256) >= kFill)
+    return buf ? launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s) : launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
+  if (!prefer_128(p) && tiles(256, 128) >= kFill)
+    return buf ? launch_layout<256, 128, 4, 2, OutT, AuxT, 6>(p, s) : launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
+  return buf ? launch_layout<128, 128, 2, 2, OutT, AuxT, 6>(p, s) : launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
 }
 
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
@@ -598,8 +762,10 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   return launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
 }
 
+#endif  // PZ_GEMM_LAB
 }  // namespace
 
+#ifndef PZ_GEMM_LAB
 bool fp8_eligible(const GemmArgs& p) {
   if (p.force_generic || p.in_dtype != DT_FP8 || p.out_dtype != DT_BF16) return false;
   if (!p.a_kc || !p.b_kc || p.accumulate) return false;
@@ -657,7 +823,7 @@ int gemm_split(const GemmArgs& p) {
   if (mode == 0 || forced_tile || p.in_dtype == DT_FP8 || !mfma_eligible(p)) return 1;
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   constexpr int kFill = 240;
-  if (tiles >= kFill) return 1;
+  if (tiles >= kFill || prefer_128(p)) return 1;
   const int nk = p.K / (p.in_dtype == DT_FP8 ? 64 : kBK);
   for (int sp : {2, 4, 8})
     if (tiles * sp >= kFill && nk % sp == 0 && nk / sp >= 16) return sp;
@@ -676,5 +842,6 @@ hipError_t gemm_mfma(const GemmArgs& p, hipStream_t s) {
   if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);
   return launch_tiles<float, uint16_t>(p, s);
 }
+#endif  // PZ_GEMM_LAB
 
 }  // namespace pz
