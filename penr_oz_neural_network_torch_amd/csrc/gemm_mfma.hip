@@ -38,7 +38,7 @@ constexpr int kBK = 32;  // K depth of one ring slot (BK64 variants: two of thes
 
 // Per-variant ring geometry: VAR 20/21 stage 64-deep K steps into two 64 KiB slots (one MFMA
 // interval = 64 MFMAs per wave, half the barriers per FLOP of the 32-deep ring)
-template <int VAR> constexpr int var_bk() { return (VAR == 20 || VAR == 21) ? 64 : 32; }
+template <int VAR> constexpr int var_bk() { return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31) ? 64 : 32; }
 template <int VAR> constexpr int var_ns() { return VAR == 5 ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4); }
 
 // K-contiguous slot [rows][BK]. BK 32: 64-B rows = 4 chunks; chunk XOR for conflict-free
@@ -101,17 +101,25 @@ PZ_DEV void glds16(const void* gsrc, uint32_t lds) {
 // offset of the K step (an SGPR: no per-step vector address math). The operand must span
 // < 4 GiB from its base (checked by the dispatcher).
 typedef int i32x4_t __attribute__((ext_vector_type(4)));
+// POL: cache policy of the request (0 default, 1 nt, 2 sc1, 3 sc0 sc1) — experiments
+template <int POL = 0>
 PZ_DEV void blds16(i32x4_t rs, uint32_t voff, uint32_t soff, uint32_t lds) {
   uint32_t keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "buffer_load_dwordx4 %1, %2, %4 offen lds\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(rs), "s"(lds), "s"(soff)
-      : "memory");
+#define PZ_BLDS(POLICY)                                          \
+  asm volatile(                                                 \
+      "s_mov_b32 %0, m0\n\t"                                    \
+      "s_mov_b32 m0, %3\n\t"                                    \
+      "s_nop 0\n\t"                                             \
+      "buffer_load_dwordx4 %1, %2, %4 offen" POLICY " lds\n\t"  \
+      "s_mov_b32 m0, %0"                                        \
+      : "=&s"(keep)                                             \
+      : "v"(voff), "s"(rs), "s"(lds), "s"(soff)                 \
+      : "memory")
+  if constexpr (POL == 1) PZ_BLDS(" nt");
+  else if constexpr (POL == 2) PZ_BLDS(" sc1");
+  else if constexpr (POL == 3) PZ_BLDS(" sc0 sc1");
+  else PZ_BLDS("");
+#undef PZ_BLDS
 }
 
 // 4-byte LDS-DMA used as an L2 PREFETCH: touching one dword of a 128-B line brings the line into
@@ -145,7 +153,7 @@ PZ_DEV uint32_t lds_addr(const PZ_LDS char* p) {
 }
 
 // K-contiguous operand rows [row0, row0+R) x k [k0, k0+BK) -> slot [R][BK]; NW waves share it
-template <int R, int NW, int BK = 32, bool BUF = false>
+template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0>
 PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
                      PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
   constexpr int CPR = BK / 8;             // 16-B chunks per row
@@ -161,7 +169,7 @@ PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int r
     gr = gr < rows_valid ? gr : rows_valid - 1;
     if constexpr (BUF) {
       const uint32_t voff = (static_cast<uint32_t>(gr) * static_cast<uint32_t>(ld) + chunk * 8) * 2u;
-      blds16(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * 2u), lds_addr(tile + rbase * BK * 2));
+      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * 2u), lds_addr(tile + rbase * BK * 2));
     } else {
       const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
       glds16(src, lds_addr(tile + rbase * BK * 2));
@@ -170,7 +178,7 @@ PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int r
 }
 
 // M/N-contiguous operand: k rows [k0, k0+BK) x cols [col0, col0+R) -> slot [BK][R]
-template <int R, int NW, int BK = 32, bool BUF = false>
+template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0>
 PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int cols_valid, int k0,
                      PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
   constexpr int ROW_BYTES = R * 2;
@@ -187,7 +195,7 @@ PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int c
     gc = gc < cols_valid ? gc : cols_valid - 8;
     if constexpr (BUF) {
       const uint32_t voff = (static_cast<uint32_t>(kr) * static_cast<uint32_t>(ld) + gc) * 2u;
-      blds16(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * static_cast<uint32_t>(ld) * 2u),
+      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * static_cast<uint32_t>(ld) * 2u),
              lds_addr(tile + kbase * ROW_BYTES));
     } else {
       const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
@@ -431,8 +439,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
   // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
   // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
-  constexpr bool BUF_A = VAR == 6 || (VAR == 25 && !A_KC);
-  constexpr bool BUF_B = VAR == 6 || (VAR == 25 && !B_KC);
+  constexpr bool BUF_A = VAR == 6 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_B = VAR == 6 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
   const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;
@@ -445,14 +454,14 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   auto stage_a_t = [&](int kt, auto team, int tw) {
     constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
-    if constexpr (A_KC) stage_kc<BM, TEAM, BK, BUF_A>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
-    else stage_mn<BM, TEAM, BK, BUF_A>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
+    if constexpr (A_KC) stage_kc<BM, TEAM, BK, BUF_A, POL>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
+    else stage_mn<BM, TEAM, BK, BUF_A, POL>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
   };
   auto stage_b_t = [&](int kt, auto team, int tw) {
     constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
-    else stage_mn<BN, TEAM, BK, BUF_B>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
+    if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B, POL>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
+    else stage_mn<BN, TEAM, BK, BUF_B, POL>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
   };
   auto stage_a = [&](int kt) { stage_a_t(kt, std::integral_constant<int, NWD>{}, wave); };
   auto stage_b = [&](int kt) { stage_b_t(kt, std::integral_constant<int, NWD>{}, wave); };
@@ -500,13 +509,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     using T4 = std::integral_constant<int, 4>;
     auto stage_g0 = [&](int kt) {
       stage_a_t(kt, T4{}, tw);
-      if constexpr (VAR == 20) stage_b_t(kt, T4{}, tw);
+      if constexpr (VAR == 20 || VAR == 30) stage_b_t(kt, T4{}, tw);
     };
     stage(0, 0);
     wait_vm<0>();
     barrier();
     if (grp == 1) {
-      if (VAR == 21 && nk > 1) stage_b_t(1, T4{}, tw);
+      if ((VAR == 21 || VAR == 31) && nk > 1) stage_b_t(1, T4{}, tw);
       barrier();
     }
     for (int t = 0; t < nk; ++t) {
@@ -516,7 +525,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
       if (grp == 1) wait_vm<0>();  // step t+1 (issued in M_{t-1}) landed before interval 2t+2
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       barrier();
-      if (VAR == 21 && grp == 1 && t + 2 < nk) stage_b_t(t + 2, T4{}, tw);
+      if ((VAR == 21 || VAR == 31) && grp == 1 && t + 2 < nk) stage_b_t(t + 2, T4{}, tw);
       mfma_step(f);
       if (grp == 0) wait_vm<0>();
       barrier();
@@ -726,10 +735,24 @@ bool prefer_128(const GemmArgs& p) {
   return t256 < kFill && t128 >= 2 * kFill;
 }
 
+// 64-deep ring steps (VAR 30: 2 x 64 KiB slots, one MFMA interval = 64 MFMAs per wave, the
+// staging waves fetch whole 128-B lines of K-contiguous rows) for layouts with an M/N-contiguous
+// operand: fwd [8192,4096]x[4096,4096] +6%, dW +4%, fwd K=1024 +4% (tools/gemm_lab, same box).
+// Both operands K-contiguous (dX) stay on the 32-deep ring: the BK64 form spills there (-11%).
+bool use_bk64(const GemmArgs& p, bool buf) {
+  static const bool off = [] {  // PZ_GEMM_BK64=0: 32-deep ring everywhere (A/B experiments)
+    const char* e = getenv("PZ_GEMM_BK64");
+    return e != nullptr && atoi(e) == 0;
+  }();
+  const int split = p.split_k > 1 ? p.split_k : 1;
+  return !off && buf && !(p.a_kc && p.b_kc) && p.K % 64 == 0 && (p.K / 64) % split == 0;
+}
+
 template <typename OutT, typename AuxT>
 hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   auto tiles = [&](int bm, int bn) { return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
   const bool buf = buffer_ok(p);
+  const bool bk64 = use_bk64(p, buf);
   constexpr int kFill = 240;  // ~ CU count: a config below this leaves CUs idle
   // experiments (probe variants live in tools/gemm_lab.hip): PZ_GEMM_TILE=1 (256x256 flat DMA)
   // 2 (256x128) 3 (128x128) 16 (256x256 buffer DMA)
@@ -738,6 +761,7 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     return e ? atoi(e) : 0;
   }();
   if (p.split_k > 1) {  // slabs sized for 256x256
+    if (bk64) return launch_layout<256, 256, 2, 4, OutT, AuxT, 30>(p, s);
     if (buf) return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
     return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
   }
@@ -749,8 +773,10 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     default: break;
   }
   // buffer-addressed LDS-DMA (VAR 6; +2..12% on the step's shapes, tools/gemm_lab)
-  if (tiles(256, 256) >= kFill)
+  if (tiles(256, 256) >= kFill) {
+    if (bk64) return launch_layout<256, 256, 2, 4, OutT, AuxT, 30>(p, s);
     return buf ? launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s) : launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
+  }
   if (!prefer_128(p) && tiles(256, 128) >= kFill)
     return buf ? launch_layout<256, 128, 4, 2, OutT, AuxT, 6>(p, s) : launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
   return buf ? launch_layout<128, 128, 2, 2, OutT, AuxT, 6>(p, s) : launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);

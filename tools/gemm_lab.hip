@@ -57,9 +57,9 @@ struct Variant {
 
 #define PZ_VARIANTS(AKC, BKC, OUT)                                                   \
   {                                                                                  \
-    {"bk32", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 0>},                \
-        {"buf_all", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 6>},         \
-        {"buf_mn", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 25>},         \
+    {"buf", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 6>},                 \
+        {"bk64g0buf", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 30>},      \
+        {"bk64spbuf", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 31>},      \
   }
 
 struct Case {
