@@ -447,10 +447,11 @@ void tensor_moments_op(const Tensor& x, int64_t row_len, int64_t rule, double th
 
 void histogram_op(const Tensor& x, const Tensor& range, int64_t bins, const Tensor& counts) {
   check_dev(x, "x");
-  TORCH_CHECK(x.is_contiguous() && range.scalar_type() == at::kDouble && counts.scalar_type() == at::kFloat,
-              "pz::histogram");
+  TORCH_CHECK(x.is_contiguous() && range.scalar_type() == at::kDouble && counts.scalar_type() == at::kLong &&
+                  counts.is_contiguous() && counts.numel() >= bins,
+              "pz::histogram: counts must be a contiguous int64 tensor of >= bins elements");
   PZ_HIP_CHECK(pz::histogram(x.data_ptr(), dt_of(x), x.numel(), range.data_ptr<double>(), static_cast<int>(bins),
-                             counts.data_ptr<float>(), cur_stream(x)));
+                             counts.data_ptr<int64_t>(), cur_stream(x)));
 }
 
 // ------------------------------------------------------------------------------- batchnorm
@@ -530,8 +531,8 @@ void embedding_fwd_op(const Tensor& table, const Tensor& idx, const Tensor& out)
   TORCH_CHECK(idx.is_contiguous() && out.is_contiguous() && table.is_contiguous(), "pz::embedding_fwd: contiguous");
   const int dim = static_cast<int>(table.size(1));
   TORCH_CHECK(out.numel() == idx.numel() * dim, "pz::embedding_fwd: out shape");
-  PZ_HIP_CHECK(pz::embedding_fwd(table.data_ptr(), dt_of(table), idx.data_ptr(), idx_type(idx), idx.numel(), dim,
-                                 out.data_ptr(), dt_of(out), cur_stream(table)));
+  PZ_HIP_CHECK(pz::embedding_fwd(table.data_ptr(), dt_of(table), table.size(0), idx.data_ptr(), idx_type(idx),
+                                 idx.numel(), dim, out.data_ptr(), dt_of(out), cur_stream(table)));
 }
 
 void embedding_bwd_op(const Tensor& dout, const Tensor& idx, const Tensor& dtable) {
@@ -539,7 +540,7 @@ void embedding_bwd_op(const Tensor& dout, const Tensor& idx, const Tensor& dtabl
   TORCH_CHECK(idx.is_contiguous() && dout.is_contiguous() && dtable.is_contiguous(), "pz::embedding_bwd: contiguous");
   const int dim = static_cast<int>(dtable.size(1));
   PZ_HIP_CHECK(pz::embedding_bwd(dout.data_ptr(), dt_of(dout), idx.data_ptr(), idx_type(idx), idx.numel(), dim,
-                                 dtable.data_ptr(), dt_of(dtable), cur_stream(dout)));
+                                 dtable.size(0), dtable.data_ptr(), dt_of(dtable), cur_stream(dout)));
 }
 
 // ------------------------------------------------------------------------------------ fp8

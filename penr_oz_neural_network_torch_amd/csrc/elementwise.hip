@@ -107,7 +107,11 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
       const int64_t label = a.labels[row];
       const F lse = mx + log(se);
       const F inv = F(1) / se;
-      if (lane == 0) loss_acc += static_cast<float>((lse - static_cast<F>(ldd<T>(lr, label))) * static_cast<F>(a.loss_scale));
+      // the host rejects labels outside [0, cols) (IndexError); a bad one only ever yields a NaN
+      // loss here, never an out-of-row read
+      const bool lab_ok = label >= 0 && label < a.cols;
+      const F xlab = lab_ok ? static_cast<F>(ldd<T>(lr, label)) : static_cast<F>(NAN);
+      if (lane == 0) loss_acc += static_cast<float>((lse - xlab) * static_cast<F>(a.loss_scale));
       for (int c = lane; c < a.cols; c += 64) {
         const F pr = fexp(static_cast<F>(ldd<T>(lr, c)) - mx) * inv;
         if (probs != nullptr) std_<T>(probs, static_cast<int64_t>(row) * a.ld_probs + c, static_cast<double>(pr));

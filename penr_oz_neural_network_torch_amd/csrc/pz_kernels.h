@@ -150,8 +150,8 @@ enum SatRule : int { SAT_NONE = 0, SAT_ABS_GT = 1, SAT_LE = 2, SAT_ROW_NORM_GT =
 // out (double[8]): min, max, sum, sumsq, saturated_count, count, row_count, -
 hipError_t tensor_moments(const void* x, int dtype, int64_t n, int64_t row_len, int sat_rule, float sat_thr,
                           double* out, hipStream_t s);
-// counts[bins] (float) of x over [lo, hi] read from range (double[2] on device: lo, hi)
-hipError_t histogram(const void* x, int dtype, int64_t n, const double* range, int bins, float* counts, hipStream_t s);
+// counts[bins] (int64, exact) of x over [lo, hi] read from range (double[2] on device: lo, hi)
+hipError_t histogram(const void* x, int dtype, int64_t n, const double* range, int bins, int64_t* counts, hipStream_t s);
 
 // ------------------------------------------------------------------ batchnorm (N4)
 struct BnArgs {
@@ -196,10 +196,12 @@ hipError_t batchnorm_bwd(const BnBwdArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ embedding (N5)
 enum IdxType : int { IDX_I64 = 0, IDX_F32 = 1, IDX_F64 = 2 };
-hipError_t embedding_fwd(const void* table, int table_dtype, const void* idx, int idx_dtype, int64_t n_idx, int dim,
-                         void* out, int out_dtype, hipStream_t s);
+// ids follow Python indexing (negative = from the end); ids outside [-vocab, vocab) read zeros /
+// drop their gradient (the host raises IndexError before launching with such ids)
+hipError_t embedding_fwd(const void* table, int table_dtype, int64_t vocab, const void* idx, int idx_dtype, int64_t n_idx,
+                         int dim, void* out, int out_dtype, hipStream_t s);
 hipError_t embedding_bwd(const void* dout, int dout_dtype, const void* idx, int idx_dtype, int64_t n_idx, int dim,
-                         void* dtable, int dtable_dtype, hipStream_t s);
+                         int64_t vocab, void* dtable, int dtable_dtype, hipStream_t s);
 
 // ------------------------------------------------------------------ fp8 quantisation
 // qs records are {q, s}: T8 = sat(T * q), T ~= T8 * s

@@ -93,9 +93,11 @@ __global__ void decode_moments_kernel(double* out) {
   }
 }
 
+// Exact integer counts: u32 per block in LDS, u64 device totals (an fp32 count stops being exact
+// past 2^24, which the ReLU-zero bin of one [8192, 8192] activation already exceeds)
 template <typename T>
 __global__ void __launch_bounds__(256) histogram_kernel(const T* __restrict__ x, int64_t n, const double* range, int bins,
-                                                        float* counts) {
+                                                        unsigned long long* counts) {
   extern __shared__ unsigned int hist_lds[];
   for (int b = threadIdx.x; b < bins; b += 256) hist_lds[b] = 0u;
   __syncthreads();
@@ -111,7 +113,7 @@ __global__ void __launch_bounds__(256) histogram_kernel(const T* __restrict__ x,
   }
   __syncthreads();
   for (int b = threadIdx.x; b < bins; b += 256)
-    if (hist_lds[b]) atomicAdd(counts + b, static_cast<float>(hist_lds[b]));
+    if (hist_lds[b]) atomicAdd(counts + b, static_cast<unsigned long long>(hist_lds[b]));
 }
 
 int grid_stride_blocks(int64_t n) {
@@ -147,11 +149,11 @@ hipError_t tensor_moments(const void* x, int dtype, int64_t n, int64_t row_len, 
   return hipGetLastError();
 }
 
-hipError_t histogram(const void* x, int dtype, int64_t n, const double* range, int bins, float* counts, hipStream_t s) {
+hipError_t histogram(const void* x, int dtype, int64_t n, const double* range, int bins, int64_t* counts, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   PZ_STATS_DISPATCH(dtype, T, {
     hipLaunchKernelGGL((histogram_kernel<T>), dim3(grid_stride_blocks(n)), dim3(256), bins * sizeof(unsigned int), s,
-                       static_cast<const T*>(x), n, range, bins, counts);
+                       static_cast<const T*>(x), n, range, bins, reinterpret_cast<unsigned long long*>(counts));
   });
   return hipGetLastError();
 }

@@ -288,9 +288,11 @@ class FusedTrainer:
         else:
             x = torch.tensor(inputs, dtype=torch.float32).reshape(len(inputs), -1)
             self.block = 1
+        lab = torch.tensor([int(t[0]) for t in targets], dtype=torch.int64) if self.head == "softmax" else None
+        self._validate(x, lab)
         self.data = self._table(x)
         if self.head == "softmax":
-            self.labels = torch.tensor([int(t[0]) for t in targets], dtype=torch.int64, device=self.dev)
+            self.labels = lab.to(self.dev)
             self.targets = None
         else:
             self.targets = torch.tensor(targets, dtype=torch.float32).reshape(len(targets), -1).to(self.dev)
@@ -299,6 +301,15 @@ class FusedTrainer:
         self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
         self._rows = None
         self._invalidate_graphs()
+
+    def _validate(self, x: torch.Tensor, labels: torch.Tensor | None) -> None:
+        """Reject class labels / token ids the kernels cannot index, once per dataset (IndexError,
+        as the reference's cross_entropy / `weights[ids]` raise), instead of per step."""
+        if labels is not None:
+            PF.check_index_range(labels, 0, self.stages[-1].out_width, "Target")
+        if self.stages[0].kind == "embed":
+            vocab = self.stages[0].seg_w.shape[0]
+            PF.check_index_range(x.reshape(-1), -vocab, vocab, "index", vocab)
 
     def _table(self, x: torch.Tensor) -> torch.Tensor:
         """Device-resident dataset. Dense inputs are kept in the GEMM operand dtype (the gather
@@ -313,6 +324,7 @@ class FusedTrainer:
         ``inputs``: ``[N, in]`` (or ``[N, T]`` token ids); ``targets``: ``[N]`` class labels for a
         softmax head, ``[N, out]`` regression targets otherwise.
         """
+        self._validate(inputs, targets.reshape(-1) if self.head == "softmax" else None)
         self.data = self._table(inputs.to(dtype=torch.float32))
         self.block = self.data.shape[1] if self.stages[0].kind == "embed" else 1
         if self.head == "softmax":

@@ -239,11 +239,25 @@ def softmax(x: Tensor) -> Tensor:
     return _Softmax.apply(x)
 
 
+def check_index_range(idx: Tensor, lo: int, hi: int, what: str, size: int | None = None) -> None:
+    """Raise IndexError (as ATen / Python indexing do) unless every id is in ``[lo, hi)``.
+    The HIP kernels never read outside their tables either way, but a bad id must surface as an
+    error, not as a silently wrong loss. A GPU tensor costs one small reduction + sync."""
+    if idx.numel() == 0:
+        return
+    v = idx if idx.dtype == torch.int64 else idx.long()
+    mn, mx = (int(t) for t in torch.aminmax(v))
+    if mn < lo or mx >= hi:
+        bad = mn if mn < lo else mx
+        raise IndexError(f"{what} {bad} is out of bounds for size {hi if size is None else size}")
+
+
 class _CrossEntropy(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits: Tensor, labels: Tensor):
         squeeze = logits.dim() == 1
         l2 = (logits.unsqueeze(0) if squeeze else logits).contiguous()
+        check_index_range(labels.reshape(-1), 0, l2.shape[-1], "Target")
         lab = labels.reshape(-1).to(device=l2.device, dtype=torch.int64).contiguous()
         rows = l2.shape[0]
         loss = torch.zeros(1, device=l2.device, dtype=torch.float32)
@@ -340,6 +354,8 @@ def batchnorm(x: Tensor, gain: Tensor, bias: Tensor, rmean: Tensor, rvar: Tensor
 class _Embedding(torch.autograd.Function):
     @staticmethod
     def forward(ctx, idx: Tensor, table: Tensor):
+        vocab = table.shape[0]
+        check_index_range(idx.reshape(-1), -vocab, vocab, "index", vocab)  # negative ids wrap (Python indexing)
         ids = idx.to(device=table.device, dtype=torch.int64).contiguous()
         out = torch.empty(*ids.shape, table.shape[1], device=table.device, dtype=table.dtype)
         _ops().embedding_fwd(table.detach().contiguous(), ids, out)
@@ -377,7 +393,7 @@ def tensor_summary(t: Tensor, algo: str | None, bins: int) -> dict:
     _ops().tensor_moments(x, row_len, SAT_CODES[rule] if algo is not None else 0, thr, moments)
     counts = None
     if bins > 0:
-        counts = torch.zeros(bins, device=dev, dtype=torch.float32)
+        counts = torch.zeros(bins, device=dev, dtype=torch.int64)  # exact counts (u64 atomics)
         _ops().histogram(x, moments[:2], bins, counts)
     host = torch.cat([moments, counts.double()]) if counts is not None else moments
     host = host.cpu().tolist()
