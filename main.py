@@ -230,7 +230,7 @@ async def train_model(body: TrainingRequest = Body(...)):
 @app.get("/progress/")
 def model_progress(model_id: str = ModelIdQuery(...)):
     log.info(f"Requesting progress for model {model_id}")
-    model = NeuralNetworkModel.deserialize(model_id)
+    model = NeuralNetworkModel.deserialize(model_id, meta_only=True)  # no parameters, no GPU
     return {"progress": model.progress, "average_cost": model.avg_cost,
             "average_cost_history": model.avg_cost_history, "status": model.status}
 
@@ -238,7 +238,7 @@ def model_progress(model_id: str = ModelIdQuery(...)):
 @app.get("/stats/")
 def model_stats(model_id: str = ModelIdQuery(...)):
     log.info(f"Requesting stats for model {model_id}")
-    return NeuralNetworkModel.deserialize(model_id).stats
+    return NeuralNetworkModel.deserialize(model_id, meta_only=True).stats
 
 
 @app.delete("/model/")

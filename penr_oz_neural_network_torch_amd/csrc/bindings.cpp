@@ -3,6 +3,10 @@
 // Device ops are registered for the CUDA dispatch key (which is the HIP device on ROCm builds of
 // PyTorch) and launch on PyTorch's current HIP stream, so they order correctly with the caching
 // allocator, RCCL collectives issued through torch.distributed, and hipGraph capture.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 #include <ATen/ATen.h>
 #include <c10/hip/HIPStream.h>
 #include <map>
@@ -656,6 +660,36 @@ std::tuple<std::string, Tensor, Tensor> scan_json_arrays_op(const std::string& p
   return {std::move(skeleton), v, s};
 }
 
+// metadata reader: top-level JSON object of `path` with the named members' values nulled (mmap'd,
+// skipped structurally: the REST progress / stats polls never parse parameter arrays)
+std::string json_skip_keys_op(const std::string& path, const std::vector<std::string>& keys) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  TORCH_CHECK(fd >= 0, "pz::json_skip_keys: cannot open ", path);
+  struct stat st;
+  if (::fstat(fd, &st) != 0) {
+    ::close(fd);
+    TORCH_CHECK(false, "pz::json_skip_keys: cannot stat ", path);
+  }
+  const size_t n = static_cast<size_t>(st.st_size);
+  if (n == 0) {
+    ::close(fd);
+    TORCH_CHECK(false, "pz::json_skip_keys: empty file ", path);
+  }
+  void* m = ::mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+  ::close(fd);
+  TORCH_CHECK(m != MAP_FAILED, "pz::json_skip_keys: mmap failed for ", path);
+  ::madvise(m, n, MADV_SEQUENTIAL);
+  std::string out;
+  try {
+    out = pz::json_null_keys(static_cast<const char*>(m), n, keys);
+  } catch (const std::exception& e) {
+    ::munmap(m, n);
+    TORCH_CHECK(false, e.what());
+  }
+  ::munmap(m, n);
+  return out;
+}
+
 }  // namespace
 
 TORCH_LIBRARY(pz, m) {
@@ -704,6 +738,7 @@ TORCH_LIBRARY(pz, m) {
   m.def("format_json_array(Tensor t, int level) -> str");
   m.def("repr_double(float x) -> str");
   m.def("scan_json_arrays(str path, str key) -> (str, Tensor, Tensor)");
+  m.def("json_skip_keys(str path, str[] keys) -> str");
 }
 
 TORCH_LIBRARY_IMPL(pz, CUDA, m) {
@@ -740,4 +775,5 @@ TORCH_LIBRARY_IMPL(pz, CompositeExplicitAutograd, m) {
   m.impl("pack_segments", TORCH_FN(pack_segments_op));
   m.impl("repr_double", TORCH_FN(repr_double_op));
   m.impl("scan_json_arrays", TORCH_FN(scan_json_arrays_op));
+  m.impl("json_skip_keys", TORCH_FN(json_skip_keys_op));
 }

@@ -251,4 +251,83 @@ void scan_json_arrays(const std::string& text, const std::string& key, std::stri
   sc.object(Scanner::COPY, true);
 }
 
+namespace {
+
+// end of the JSON string starting at p (p points at the opening quote)
+const char* skip_string(const char* p, const char* end) {
+  ++p;
+  while (true) {
+    const void* q = std::memchr(p, '"', static_cast<size_t>(end - p));
+    if (q == nullptr) throw std::runtime_error("pz::json_null_keys: unterminated string");
+    const char* e = static_cast<const char*>(q);
+    size_t bs = 0;  // an odd run of backslashes before the quote escapes it
+    for (const char* b = e - 1; b >= p && *b == '\\'; --b) ++bs;
+    if ((bs & 1) == 0) return e + 1;
+    p = e + 1;
+  }
+}
+
+// end of the JSON value starting at p (after whitespace)
+const char* skip_value(const char* p, const char* end) {
+  if (p >= end) throw std::runtime_error("pz::json_null_keys: unexpected end");
+  if (*p == '"') return skip_string(p, end);
+  if (*p != '[' && *p != '{') {
+    while (p < end && *p != ',' && *p != ']' && *p != '}' && *p != ' ' && *p != '\n' && *p != '\r' && *p != '\t') ++p;
+    return p;
+  }
+  int depth = 0;
+  while (p < end) {
+    const char c = *p;
+    if (c == '"') { p = skip_string(p, end); continue; }
+    if (c == '[' || c == '{') ++depth;
+    else if (c == ']' || c == '}') {
+      if (--depth == 0) return p + 1;
+    }
+    ++p;
+  }
+  throw std::runtime_error("pz::json_null_keys: unterminated container");
+}
+
+}  // namespace
+
+std::string json_null_keys(const char* data, size_t n, const std::vector<std::string>& keys) {
+  const char* p = data;
+  const char* end = data + n;
+  auto ws = [&] { while (p < end && (*p == ' ' || *p == '\n' || *p == '\r' || *p == '\t')) ++p; };
+  ws();
+  if (p >= end || *p != '{') throw std::runtime_error("pz::json_null_keys: top level must be an object");
+  std::string out;
+  out.reserve(4096);
+  out += '{';
+  ++p;
+  bool first = true;
+  while (true) {
+    ws();
+    if (p < end && *p == '}') break;
+    if (p >= end || *p != '"') throw std::runtime_error("pz::json_null_keys: expected a key");
+    const char* k0 = p;
+    p = skip_string(p, end);
+    const std::string key(k0 + 1, p - 1 - (k0 + 1));
+    ws();
+    if (p >= end || *p != ':') throw std::runtime_error("pz::json_null_keys: expected ':'");
+    ++p;
+    ws();
+    const char* v0 = p;
+    p = skip_value(p, end);
+    if (!first) out += ", ";
+    first = false;
+    out.append(k0, static_cast<size_t>(v0 - k0) - 0);  // "key": (+ any whitespace)
+    bool drop = false;
+    for (const auto& k : keys) drop |= k == key;
+    if (drop) out += "null";
+    else out.append(v0, static_cast<size_t>(p - v0));
+    ws();
+    if (p < end && *p == ',') { ++p; continue; }
+    if (p < end && *p == '}') break;
+    throw std::runtime_error("pz::json_null_keys: bad object");
+  }
+  out += '}';
+  return out;
+}
+
 }  // namespace pz

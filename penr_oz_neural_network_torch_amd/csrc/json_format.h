@@ -16,4 +16,8 @@ std::string repr_double(double x);
 // `values`; `shapes` receives [ndim, d0, d1, ...] per lifted array. Throws on malformed input.
 void scan_json_arrays(const std::string& text, const std::string& key, std::string& skeleton,
                       std::vector<double>& values, std::vector<int64_t>& shapes);
+// Metadata reader: the top-level object of [data, data+n) with the VALUES of the top-level
+// members named in `keys` replaced by null — skipped structurally (bracket depth, string
+// escapes), never parsed, so a multi-GB "layers" member costs one linear byte scan.
+std::string json_null_keys(const char* data, size_t n, const std::vector<std::string>& keys);
 }  // namespace pz

@@ -50,6 +50,20 @@ def _effective_device(device) -> torch.device:
     return dev
 
 
+class ModelMeta:
+    """Checkpoint metadata under the attribute names of :class:`NeuralNetworkModel`."""
+
+    def __init__(self, model_id: str, meta: dict):
+        self.model_id = model_id
+        self.algos = meta.get("algos")
+        self.progress = meta.get("progress", [])
+        self.avg_cost = meta.get("average_cost")
+        self.avg_cost_history = meta.get("average_cost_history", [])
+        self.stats = meta.get("stats")
+        self.status = meta.get("status")
+        self.runtime = meta.get("runtime")
+
+
 class NeuralNetworkModel(MultiLayerPerceptron):
     def __init__(self, model_id, layer_sizes: list[int] = None, weight_algo="xavier", bias_algo="zeros",
                  activation_algos=None, optimizer_algo="adam", batchnorm=(1e-5, 0.1), confidence=1.0,
@@ -174,7 +188,17 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         return True
 
     @classmethod
-    def deserialize(cls, model_id: str):
+    def deserialize(cls, model_id: str, meta_only: bool = False):
+        """Load a model. ``meta_only=True`` (the REST ``/progress/`` / ``/stats/`` polls; the
+        reference deserialises the whole model for each, ``main.py:303-318``): a :class:`ModelMeta`
+        with the progress / cost / status / stats attributes only — no parameter is parsed and
+        nothing is placed on a GPU."""
+        if meta_only:
+            try:
+                return ModelMeta(model_id, ckpt.load_meta(model_id))
+            except FileNotFoundError as e:
+                log.error(f"File not found error occurred: {str(e)}")
+                raise KeyError(f"Model {model_id} not created yet.")
         try:
             model_data, opt_state = ckpt.load(model_id)
         except FileNotFoundError as e:

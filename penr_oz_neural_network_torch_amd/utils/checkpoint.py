@@ -19,6 +19,13 @@ What is new here (format unchanged, files are interchangeable with the reference
   same bytes.
 * **Atomic replace.** Files are written to a temporary sibling and ``os.replace``-d, so a
   concurrent ``/progress/`` poll never reads a torn file (reference race).
+* **Metadata reads without parameters.** ``/progress/`` and ``/stats/`` need a few small members,
+  not the (possibly multi-GB) ``layers`` / ``training_data_buffer``. :func:`load_meta` reads them
+  from a sidecar ``model_<id>.meta.json`` written next to every checkpoint (stamped with the main
+  file's size + mtime, so a stale sidecar is never trusted), else by a native structural skip of
+  the big members (``torch.ops.pz.json_skip_keys``: one mmap'd byte scan, nothing parsed), else
+  by ``json.load``. No model object is built, nothing touches the GPU. The main file format is
+  unchanged; the sidecar is an extra cache file (deleted with the model).
 """
 from __future__ import annotations
 
@@ -41,6 +48,15 @@ def models_dir() -> str:
 
 def model_path(model_id: str) -> str:
     return os.path.join(models_dir(), f"model_{model_id}.json")
+
+
+def meta_path(model_id: str) -> str:
+    return os.path.join(models_dir(), f"model_{model_id}.meta.json")
+
+
+# members of the checkpoint a metadata read returns (everything but the parameters / data buffer)
+META_KEYS = ("algos", "progress", "average_cost", "average_cost_history", "stats", "status", "runtime")
+BIG_KEYS = ("layers", "training_data_buffer")
 
 
 def optimizer_path(model_id: str) -> str:
@@ -157,11 +173,19 @@ def _to_cpu(obj):
     return obj
 
 
+def _stamp(path: str) -> list[int]:
+    st = os.stat(path)
+    return [st.st_size, st.st_mtime_ns]
+
+
 def save(model_id: str, skeleton: dict, optimizer_state: dict | None) -> None:
     os.makedirs(models_dir(), exist_ok=True)
     path = model_path(model_id)
     _atomic_write_text(path, render_json(skeleton))
     log.info(f"Model saved successfully: {path}")
+    meta = {k: skeleton[k] for k in META_KEYS if k in skeleton}
+    meta["main_stamp"] = _stamp(path)
+    _atomic_write_text(meta_path(model_id), json.dumps(meta))
     if optimizer_state is not None:
         opath = optimizer_path(model_id)
         _atomic_torch_save(_to_cpu(optimizer_state), opath)
@@ -271,7 +295,30 @@ def load(model_id: str) -> tuple[dict, dict | None]:
     return data, opt_state
 
 
+def load_meta(model_id: str) -> dict:
+    """The checkpoint's small members (:data:`META_KEYS`) without reading any parameter; missing
+    model → ``FileNotFoundError``."""
+    path = model_path(model_id)
+    stamp = _stamp(path)  # FileNotFoundError for an unknown model
+    try:
+        with open(meta_path(model_id), "r", encoding="utf-8") as f:
+            meta = json.load(f)
+        if meta.get("main_stamp") == stamp:
+            return meta
+    except (OSError, ValueError):
+        pass
+    from ..ops import native
+    if native.has_host_ops() and os.environ.get("PZ_NATIVE_JSON", "1") != "0":
+        return json.loads(torch.ops.pz.json_skip_keys(path, list(BIG_KEYS)))
+    with open(path, "r", encoding="utf-8") as f:
+        data = json.load(f)
+    return {k: data[k] for k in META_KEYS if k in data}
+
+
 def delete(model_id: str) -> None:
+    mpath = meta_path(model_id)
+    if os.path.exists(mpath):
+        os.remove(mpath)
     os.remove(model_path(model_id))
     opath = optimizer_path(model_id)
     if os.path.exists(opath):
