@@ -134,7 +134,7 @@ __global__ void __launch_bounds__(256) bn_dx_kernel(BnBwdArgs a) {
   T* __restrict__ dx = static_cast<T*>(a.dx);
   const P* gain = static_cast<const P*>(a.gain);
   const int64_t n = static_cast<int64_t>(a.rows) * a.cols;
-  const double B = a.rows_valid;
+  const double B = a.n_total > 0 ? static_cast<double>(a.n_total) : static_cast<double>(a.rows_valid);
   for (int64_t i = blockIdx.x * int64_t(256) + threadIdx.x; i < n; i += int64_t(gridDim.x) * 256) {
     const int64_t r = i / a.cols;
     const int c = static_cast<int>(i - r * a.cols);
@@ -180,17 +180,20 @@ int blocks_for(int64_t n) {
 
 hipError_t batchnorm_fwd(const BnArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
+  const int n = a.n_total > 0 ? static_cast<int>(a.n_total) : a.rows_valid;
   PZ_BN_DISPATCH(a.dtype, a.param_dtype, T, P, {
-    if (a.training) {
+    if (a.training && a.phase != 2) {
       hipMemsetAsync(a.partial, 0, sizeof(double) * 2 * a.cols, s);
       dim3 grid((a.cols + 63) / 64, (a.rows_valid + kRowsPerChunk - 1) / kRowsPerChunk);
       hipLaunchKernelGGL((bn_col_sums_kernel<T>), grid, dim3(256), 0, s, static_cast<const T*>(a.x), a.rows_valid,
                          a.cols, a.partial);
     }
-    hipLaunchKernelGGL((bn_finalize_kernel<P>), dim3((a.cols + 255) / 256), dim3(256), 0, s, a.partial, a.rows_valid,
-                       a.cols, static_cast<P*>(a.running_mean), static_cast<P*>(a.running_var), a.eps, a.momentum,
-                       a.training, a.save_mean, a.save_invstd);
-    hipLaunchKernelGGL((bn_normalize_kernel<T, P>), dim3(blocks_for(int64_t(a.rows) * a.cols)), dim3(256), 0, s, a);
+    if (a.phase != 1) {
+      hipLaunchKernelGGL((bn_finalize_kernel<P>), dim3((a.cols + 255) / 256), dim3(256), 0, s, a.partial, n, a.cols,
+                         static_cast<P*>(a.running_mean), static_cast<P*>(a.running_var), a.eps, a.momentum,
+                         a.training, a.save_mean, a.save_invstd);
+      hipLaunchKernelGGL((bn_normalize_kernel<T, P>), dim3(blocks_for(int64_t(a.rows) * a.cols)), dim3(256), 0, s, a);
+    }
   });
   return hipGetLastError();
 }
@@ -198,12 +201,14 @@ hipError_t batchnorm_fwd(const BnArgs& a, hipStream_t s) {
 hipError_t batchnorm_bwd(const BnBwdArgs& a, hipStream_t s) {
   if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
   PZ_BN_DISPATCH(a.dtype, a.param_dtype, T, P, {
-    hipMemsetAsync(a.partial, 0, sizeof(double) * 2 * a.cols, s);
-    dim3 grid((a.cols + 63) / 64, (a.rows_valid + kRowsPerChunk - 1) / kRowsPerChunk);
-    hipLaunchKernelGGL((bn_bwd_sums_kernel<T>), grid, dim3(256), 0, s, a);
-    hipLaunchKernelGGL((bn_param_grads_kernel<P>), dim3((a.cols + 255) / 256), dim3(256), 0, s, a.partial, a.cols,
-                       static_cast<P*>(a.dgain), static_cast<P*>(a.dbias));
-    if (a.dx != nullptr)
+    if (a.phase != 2) {
+      hipMemsetAsync(a.partial, 0, sizeof(double) * 2 * a.cols, s);
+      dim3 grid((a.cols + 63) / 64, (a.rows_valid + kRowsPerChunk - 1) / kRowsPerChunk);
+      hipLaunchKernelGGL((bn_bwd_sums_kernel<T>), grid, dim3(256), 0, s, a);
+      hipLaunchKernelGGL((bn_param_grads_kernel<P>), dim3((a.cols + 255) / 256), dim3(256), 0, s, a.partial, a.cols,
+                         static_cast<P*>(a.dgain), static_cast<P*>(a.dbias));
+    }
+    if (a.dx != nullptr && a.phase != 1)
       hipLaunchKernelGGL((bn_dx_kernel<T, P>), dim3(blocks_for(int64_t(a.rows) * a.cols)), dim3(256), 0, s, a);
   });
   return hipGetLastError();

@@ -462,7 +462,7 @@ void histogram_op(const Tensor& x, const Tensor& range, int64_t bins, const Tens
 void batchnorm_fwd_op(const Tensor& x, const Tensor& y, const Tensor& gain, const Tensor& bias,
                       const Tensor& running_mean, const Tensor& running_var, double eps, double momentum, bool training,
                       int64_t rows_valid, const Tensor& save_mean, const Tensor& save_invstd, const Tensor& partial,
-                      at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld) {
+                      at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld, int64_t phase, int64_t n_total) {
   check_dev(x, "x");
   TORCH_CHECK(x.is_contiguous() && y.is_contiguous(), "pz::batchnorm_fwd: contiguous");
   TORCH_CHECK(gain.scalar_type() == bias.scalar_type() && gain.scalar_type() == running_mean.scalar_type() &&
@@ -488,13 +488,15 @@ void batchnorm_fwd_op(const Tensor& x, const Tensor& y, const Tensor& gain, cons
   a.partial = partial.data_ptr<double>();
   a.epi = make_epi(ei, ef);
   a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
+  a.phase = static_cast<int>(phase);
+  a.n_total = n_total;
   PZ_HIP_CHECK(pz::batchnorm_fwd(a, cur_stream(x)));
 }
 
 void batchnorm_bwd_op(const Tensor& g, const Tensor& y, const Tensor& x, const optional<Tensor>& dx, const Tensor& gain,
                       const Tensor& bias, const Tensor& save_mean, const Tensor& save_invstd,
                       const optional<Tensor>& dgain, const optional<Tensor>& dbias, const Tensor& partial,
-                      int64_t rows_valid, at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld) {
+                      int64_t rows_valid, at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld, int64_t phase, int64_t n_total) {
   check_dev(g, "g");
   TORCH_CHECK(g.is_contiguous() && y.is_contiguous() && x.is_contiguous(), "pz::batchnorm_bwd: contiguous");
   pz::BnBwdArgs a{};
@@ -516,6 +518,8 @@ void batchnorm_bwd_op(const Tensor& g, const Tensor& y, const Tensor& x, const o
   a.partial = partial.data_ptr<double>();
   a.epi = make_epi(ei, ef);
   a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
+  a.phase = static_cast<int>(phase);
+  a.n_total = n_total;
   PZ_HIP_CHECK(pz::batchnorm_bwd(a, cur_stream(g)));
 }
 
@@ -722,10 +726,10 @@ TORCH_LIBRARY(pz, m) {
   m.def("histogram(Tensor x, Tensor range, int bins, Tensor(a!) counts) -> ()");
   m.def("batchnorm_fwd(Tensor x, Tensor(a!) y, Tensor gain, Tensor bias, Tensor(b!) running_mean, "
         "Tensor(c!) running_var, float eps, float momentum, bool training, int rows_valid, Tensor(d!) save_mean, "
-        "Tensor(e!) save_invstd, Tensor(f!) partial, int[] epi_i, float[] epi_f, int idx_ld) -> ()");
+        "Tensor(e!) save_invstd, Tensor(f!) partial, int[] epi_i, float[] epi_f, int idx_ld, int phase=0, int n_total=0) -> ()");
   m.def("batchnorm_bwd(Tensor g, Tensor y, Tensor x, Tensor(a!)? dx, Tensor gain, Tensor bias, Tensor save_mean, "
         "Tensor save_invstd, Tensor(b!)? dgain, Tensor(c!)? dbias, Tensor(d!) partial, int rows_valid, int[] epi_i, "
-        "float[] epi_f, int idx_ld) -> ()");
+        "float[] epi_f, int idx_ld, int phase=0, int n_total=0) -> ()");
   m.def("embedding_fwd(Tensor table, Tensor idx, Tensor(a!) out) -> ()");
   m.def("embedding_bwd(Tensor dout, Tensor idx, Tensor(a!) dtable) -> ()");
   m.def("step_finalize(Tensor(e!)? loss, float loss_div, Tensor(a!) stats_prev, Tensor stats_cur, Tensor slot_numel, "

@@ -171,6 +171,11 @@ struct BnArgs {
   double* partial;        // workspace [2][cols] (sum, sumsq)
   EpiSpec epi;            // fused stage epilogue after the affine transform
   int64_t idx_ld;
+  // Synchronised batchnorm under data parallelism: phase 1 = column sums into `partial` only;
+  // the caller all-reduces partial; phase 2 = statistics from the reduced partial over n_total
+  // rows (the global batch) + normalise. phase 0 = both (single process).
+  int phase;
+  int64_t n_total;        // rows behind `partial` (0: rows_valid)
 };
 hipError_t batchnorm_fwd(const BnArgs& a, hipStream_t s);
 struct BnBwdArgs {
@@ -191,6 +196,11 @@ struct BnBwdArgs {
   void* dxhat_buf;        // optional workspace [rows][cols] (same dtype as x) for the epilogue grads
   EpiSpec epi;
   int64_t idx_ld;
+  // phase 1 = sum(dy), sum(dy*xhat) into `partial` + the LOCAL parameter gradients (the data-
+  // parallel gradient all-reduce sums those); the caller all-reduces partial; phase 2 = dx from
+  // the reduced partial over n_total rows. phase 0 = both.
+  int phase;
+  int64_t n_total;
 };
 hipError_t batchnorm_bwd(const BnBwdArgs& a, hipStream_t s);
 

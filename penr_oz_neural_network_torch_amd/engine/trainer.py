@@ -191,6 +191,12 @@ class FusedTrainer:
         # all-reduced in bf16 (half the xGMI bytes of fp32 — rings over xGMI are per-link bound,
         # SURVEY §5.8); the fused optimizer reads them back as fp32. Biases, BN, embeddings and
         # the loss stay in the exact fp32 bucket. PZ_GRAD_COMM_DTYPE=fp32 keeps fp32 gradients.
+        # Why bf16 is the default (tests/test_dp_gpu.py, measured on MI355X against one rank on the
+        # concatenated batch, 2 steps): the bf16 rounding of each rank's gradient plus the ring's
+        # bf16 partial sums cost 5e-5 (2 ranks) / 1e-4 (8 ranks) relative cost error and SGD weight
+        # deltas of 1.3e-5 / 1.8e-5 — a few bf16 ulps of the update, far below minibatch noise —
+        # while the fp32 L2 bucket of the headline model (67 MB) would no longer hide behind the
+        # remaining backward (dX L2 + dW L1, ~0.3 ms) at a ~300 GB/s ring over xGMI.
         self.grads16: dict[int, torch.Tensor] = {}
         policy = os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower()
         if self.ctx.enabled and self.compute == torch.bfloat16 and policy in ("bf16", "bfloat16"):
@@ -827,11 +833,20 @@ class FusedTrainer:
         return y
 
     def _bn_fwd(self, st: Stage, x, y, batch, ei, ef):
+        """Batchnorm forward. Under data parallelism the statistics are SYNCHRONISED: column
+        sums (phase 1) -> all-reduce over the ranks -> mean / variance of the global batch and
+        normalise (phase 2), so every rank normalises with, and keeps, the same running stats
+        (one process training on the whole batch)."""
         layer = st.layer
-        torch.ops.pz.batchnorm_fwd(x, y, self.store.view(st.seg_w), self.store.view(st.seg_b), layer.mean,
-                                   layer.variance, float(layer.eps), float(layer.momentum), True,
-                                   batch * st.pos_out, st.buffers["mean"], st.buffers["invstd"],
-                                   st.buffers["partial"], ei, ef, 0)
+        args = (x, y, self.store.view(st.seg_w), self.store.view(st.seg_b), layer.mean, layer.variance,
+                float(layer.eps), float(layer.momentum), True, batch * st.pos_out, st.buffers["mean"],
+                st.buffers["invstd"], st.buffers["partial"], ei, ef, 0)
+        if not self.ctx.enabled:
+            torch.ops.pz.batchnorm_fwd(*args)
+            return
+        torch.ops.pz.batchnorm_fwd(*args, 1, 0)
+        self.ctx.all_reduce_(st.buffers["partial"])
+        torch.ops.pz.batchnorm_fwd(*args, 2, batch * st.pos_out * self.ctx.world_size)
 
     def _scratch(self, key, like):
         buf = getattr(self, "_scratch_bufs", None)
@@ -891,11 +906,16 @@ class FusedTrainer:
             dx = st.buffers["bn_in_grad"] if before is not None else None
             layer = st.layer
             none = PF.epi_spec()
-            ops.batchnorm_bwd(g, st.buffers["y"] if rec is None else rec[("z", st.first)], x_in, dx,
-                              self.store.view(st.seg_w), self.store.view(st.seg_b), st.buffers["mean"],
-                              st.buffers["invstd"], self.store.view(st.seg_w, self.grads),
-                              self.store.view(st.seg_b, self.grads), st.buffers["partial"], rows_valid,
-                              *none, 0)
+            bargs = (g, st.buffers["y"] if rec is None else rec[("z", st.first)], x_in, dx,
+                     self.store.view(st.seg_w), self.store.view(st.seg_b), st.buffers["mean"],
+                     st.buffers["invstd"], self.store.view(st.seg_w, self.grads),
+                     self.store.view(st.seg_b, self.grads), st.buffers["partial"], rows_valid, *none, 0)
+            if not self.ctx.enabled:
+                ops.batchnorm_bwd(*bargs)
+            else:  # synchronised: local parameter grads, then dx from the global sums
+                ops.batchnorm_bwd(*bargs, 1, 0)
+                self.ctx.all_reduce_(st.buffers["partial"])
+                ops.batchnorm_bwd(*bargs, 2, rows_valid * self.ctx.world_size)
             del layer
             if rec is not None and before is not None:
                 rec[("grad", before.layers[-1])] = dx[:batch * st.pos_in]

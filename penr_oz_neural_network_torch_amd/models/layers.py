@@ -27,6 +27,16 @@ def _on_gpu(t: Tensor | None) -> bool:
     return t is not None and t.is_cuda
 
 
+# Data-parallel context whose ranks SHARE batchnorm statistics while set (``_train_autograd``
+# sets it for world size > 1): synchronised batchnorm, the global batch is normalised as one
+_BN_SYNC = None
+
+
+def set_bn_sync(ctx) -> None:
+    global _BN_SYNC
+    _BN_SYNC = ctx if ctx is not None and ctx.enabled else None
+
+
 def _pf():
     from ..ops import functional as PF
     return PF
@@ -192,12 +202,29 @@ class BatchNormLayer(Layer):
         return {"params": [ref(p) for p in self.params], "eps": self.eps, "momentum": self.momentum}
 
     def forward(self, input_tensor: Tensor) -> Tensor:
+        sync = _BN_SYNC if self.training else None
         if _on_gpu(self.gain):
             y, rm, rv = _pf().batchnorm(input_tensor, self.gain, self.bias, self.mean, self.variance, self.eps,
-                                        self.momentum, self.training)
+                                        self.momentum, self.training, sync=sync)
             if self.training:
                 self.mean, self.variance = rm, rv
             return y
+        if sync is not None:  # global-batch statistics through a differentiable all-reduce
+            from torch.distributed.nn.functional import all_reduce
+            dims = tuple(range(input_tensor.ndim - 1))
+            n = torch.tensor([float(input_tensor.numel() // input_tensor.shape[-1])], dtype=input_tensor.dtype)
+            sums = all_reduce(torch.cat([input_tensor.sum(dims), (input_tensor * input_tensor).sum(dims), n]),
+                              group=sync.group)
+            c = input_tensor.shape[-1]
+            total = sums[2 * c]
+            keep = [1] * (input_tensor.ndim - 1) + [c]  # keepdim shape, as the reference's mean / var
+            mean = (sums[:c] / total).view(keep)
+            variance = ((sums[c:2 * c] - total * sums[:c] / total * sums[:c] / total) / (total - 1)).view(keep)
+            with torch.no_grad():
+                m = self.momentum
+                self.mean = (1 - m) * self.mean + m * mean.detach()
+                self.variance = (1 - m) * self.variance + m * variance.detach()
+            return self.gain * (input_tensor - mean) / torch.sqrt(variance + self.eps) + self.bias
         if self.training:
             dims = tuple(range(input_tensor.ndim - 1))
             mean = input_tensor.mean(dims, keepdim=True)

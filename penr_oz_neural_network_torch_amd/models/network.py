@@ -357,6 +357,17 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         (identical) optimizer step — equivalent to one process training on the whole sample."""
         ctx = context or self._dp_context()
         world, rank = ctx.world_size, ctx.rank
+        from . import layers as _layers
+        _layers.set_bn_sync(ctx if world > 1 else None)  # synchronised batchnorm statistics
+        try:
+            self._autograd_epochs(data, epochs, learning_rate, sample_size, decay_rate, dropout_rate, l2_lambda,
+                                  ctx, sampler)
+        finally:
+            _layers.set_bn_sync(None)
+
+    def _autograd_epochs(self, data, epochs, learning_rate, sample_size, decay_rate, dropout_rate, l2_lambda, ctx,
+                         sampler):
+        world, rank = ctx.world_size, ctx.rank
         if world > 1:
             dev = self.params[0].device if self.params else torch.device("cpu")
             with torch.no_grad():
@@ -400,9 +411,13 @@ class NeuralNetworkModel(MultiLayerPerceptron):
             if epoch + 1 == epochs or long_training:
                 for a in activations:
                     a.retain_grad()
-            cost.backward()
             if world > 1:
-                self._average_gradients(ctx, weight)
+                # the rank's share of the global objective: gradients then simply SUM over the ranks
+                # (and a synchronised batchnorm's all-reduce backward combines the shares correctly)
+                (cost * weight).backward()
+                self._average_gradients(ctx, 1.0)
+            else:
+                cost.backward()
             if self.optimizer is not None:
                 self.optimizer.step()
             else:

@@ -307,7 +307,7 @@ def mse_loss(y: Tensor, target: Tensor) -> Tensor:
 # --------------------------------------------------------------------------------------------
 class _BatchNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gain, bias, rmean, rvar, eps, momentum, training):
+    def forward(ctx, x, gain, bias, rmean, rvar, eps, momentum, training, sync):
         cols = x.shape[-1]
         xc = x.contiguous()
         y = torch.empty_like(xc)
@@ -316,11 +316,21 @@ class _BatchNorm(torch.autograd.Function):
         save_inv = torch.empty(cols, device=dev, dtype=torch.float64)
         partial = torch.empty(2 * cols, device=dev, dtype=torch.float64)
         rows = xc.numel() // max(cols, 1)
-        _ops().batchnorm_fwd(xc, y, gain.detach().contiguous(), bias.detach().contiguous(), rmean, rvar, eps,
-                             momentum, training, rows, save_mean, save_inv, partial, NO_EPI[0], NO_EPI[1], 0)
+        args = (xc, y, gain.detach().contiguous(), bias.detach().contiguous(), rmean, rvar, eps, momentum, training,
+                rows, save_mean, save_inv, partial, NO_EPI[0], NO_EPI[1], 0)
+        total = rows
+        if sync is not None and training:  # synchronised statistics: sums -> all-reduce -> finalise
+            _ops().batchnorm_fwd(*args, 1, 0)
+            sync.all_reduce_(partial)
+            total = int(sync.all_reduce_scalar(float(rows)))
+            _ops().batchnorm_fwd(*args, 2, total)
+        else:
+            _ops().batchnorm_fwd(*args)
         ctx.save_for_backward(xc, y, gain, bias, save_mean, save_inv)
         ctx.rows = rows
         ctx.training = training
+        ctx.sync = sync if training else None
+        ctx.total = total
         return y
 
     @staticmethod
@@ -336,18 +346,24 @@ class _BatchNorm(torch.autograd.Function):
         dgain = torch.zeros_like(gain)
         dbias = torch.zeros_like(bias)
         partial = torch.empty(2 * xc.shape[-1], device=xc.device, dtype=torch.float64)
-        _ops().batchnorm_bwd(g.contiguous().to(xc.dtype), y, xc, dx, gain.detach().contiguous(),
-                             bias.detach().contiguous(), save_mean, save_inv, dgain, dbias, partial, ctx.rows,
-                             NO_EPI[0], NO_EPI[1], 0)
-        return dx, dgain, dbias, None, None, None, None, None
+        args = (g.contiguous().to(xc.dtype), y, xc, dx, gain.detach().contiguous(), bias.detach().contiguous(),
+                save_mean, save_inv, dgain, dbias, partial, ctx.rows, NO_EPI[0], NO_EPI[1], 0)
+        if ctx.sync is not None:  # local parameter grads; dx from the global sums
+            _ops().batchnorm_bwd(*args, 1, 0)
+            ctx.sync.all_reduce_(partial)
+            _ops().batchnorm_bwd(*args, 2, ctx.total)
+        else:
+            _ops().batchnorm_bwd(*args)
+        return dx, dgain, dbias, None, None, None, None, None, None
 
 
 def batchnorm(x: Tensor, gain: Tensor, bias: Tensor, rmean: Tensor, rvar: Tensor, eps: float, momentum: float,
-              training: bool) -> tuple[Tensor, Tensor, Tensor]:
-    """Returns ``(y, running_mean, running_var)``; running stats are fresh tensors like the reference."""
+              training: bool, sync=None) -> tuple[Tensor, Tensor, Tensor]:
+    """Returns ``(y, running_mean, running_var)``; running stats are fresh tensors like the reference.
+    ``sync``: a data-parallel context whose ranks share the batch statistics (synchronised BN)."""
     rm = rmean.detach().reshape(-1).to(gain.dtype).clone()
     rv = rvar.detach().reshape(-1).to(gain.dtype).clone()
-    y = _BatchNorm.apply(x, gain, bias, rm, rv, float(eps), float(momentum), bool(training))
+    y = _BatchNorm.apply(x, gain, bias, rm, rv, float(eps), float(momentum), bool(training), sync)
     return y, rm, rv
 
 

@@ -55,6 +55,11 @@ class DataParallelContext:
             return (work, low, t)
         return (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), None, None)
 
+    def all_reduce_(self, t: torch.Tensor) -> None:
+        """Blocking exact SUM all-reduce in place (stream-ordered under RCCL): the synchronised
+        batchnorm statistics, which the next kernel needs right away."""
+        self.wait_one(self.all_reduce_async(t, exact=True))
+
     def wait_all(self, handles) -> None:
         for h in handles:
             self.wait_one(h)

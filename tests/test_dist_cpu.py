@@ -49,24 +49,32 @@ def test_gloo_two_rank_communicator(tmp_path):
         assert torch.allclose(got["bf16"], torch.full((64,), 1.5))
 
 
-def _train_rank(rank, world, port, optimizer, out_dir):
+def _train_rank(rank, world, port, optimizer, out_dir, bn=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
     init_from_env("gloo")
-    model, data = _dp_model(optimizer)
+    model, data = _dp_model(optimizer, bn)
     torch.manual_seed(100 + rank)  # ranks' own RNG streams differ; the shared sampler decides the data
     model._train_autograd(data, 4, 0.05, 32, 0.9, 0.0, 1e-3, sampler=torch.Generator().manual_seed(21))
     if rank == 0:
-        torch.save({"params": [p.detach() for p in model.params], "costs": [p["cost"] for p in model.progress]},
-                   os.path.join(out_dir, "dp.pt"))
+        torch.save({"params": [p.detach() for p in model.params], "costs": [p["cost"] for p in model.progress],
+                    "bn": _bn_running(model)}, os.path.join(out_dir, "dp.pt"))
+    else:
+        torch.save({"bn": _bn_running(model)}, os.path.join(out_dir, f"bn{rank}.pt"))
     shutdown()
 
 
-def _dp_model(optimizer):
+def _bn_running(model):
+    return [(l.mean.detach().clone(), l.variance.detach().clone()) for l in model.layers if l.algo == "batchnorm"]
+
+
+def _dp_model(optimizer, bn=False):
     from neural_net_model import NeuralNetworkModel
     torch.manual_seed(3)
-    model = NeuralNetworkModel("dp", [6, 16, 4], "xavier", "random", ["tanh", "softmax"], optimizer)
+    algos = ["linear", "batchnorm", "tanh", "softmax"] if bn else ["tanh", "softmax"]
+    model = NeuralNetworkModel("dp", [6, 16, 4], "xavier", "random", algos, optimizer)
     g = torch.Generator().manual_seed(8)
     x = torch.randn(200, 6, generator=g, dtype=torch.float64)
     y = torch.randint(0, 4, (200,), generator=g)
@@ -76,16 +84,30 @@ def _dp_model(optimizer):
 import pytest  # noqa: E402
 
 
-@pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
-def test_gloo_data_parallel_training_equals_single_process(tmp_path, optimizer):
-    """CPU data parallelism (reference fp64 path): 2 ranks x 16 samples == 1 process x 32."""
-    mp.start_processes(_train_rank, args=(2, _free_port(), optimizer, str(tmp_path)), nprocs=2, start_method="spawn")
+@pytest.mark.parametrize("world,optimizer,bn", [(2, "adam", False), (2, "stochastic", False), (2, "adam", True),
+                                                (8, "adam", False), (8, "stochastic", True)])
+def test_gloo_data_parallel_training_equals_single_process(tmp_path, world, optimizer, bn):
+    """CPU data parallelism (reference fp64 path): W ranks x 32/W samples == 1 process x 32, to
+    fp64 rounding — at world 8 too, and for batchnorm models, whose statistics are synchronised
+    over the ranks (every rank ends with the single process's running mean / variance)."""
+    mp.start_processes(_train_rank, args=(world, _free_port(), optimizer, str(tmp_path), bn), nprocs=world,
+                       start_method="spawn")
     dp = torch.load(tmp_path / "dp.pt", weights_only=True)
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
-    model, data = _dp_model(optimizer)
+    model, data = _dp_model(optimizer, bn)
     model._train_autograd(data, 4, 0.05, 32, 0.9, 0.0, 1e-3, context=DataParallelContext(),
                           sampler=torch.Generator().manual_seed(21))
+    # batchnorm: the ranks form the statistics from all-reduced sums / sums of squares where the
+    # single process uses torch.var's two-pass form — equal up to fp64 cancellation (~1e-9)
+    tol = 1e-7 if bn else 1e-10
     for a, b in zip(dp["params"], model.params):
-        torch.testing.assert_close(a, b.detach(), rtol=1e-12, atol=1e-12)
+        torch.testing.assert_close(a, b.detach(), rtol=tol, atol=tol * 1e-2)
     for a, b in zip(dp["costs"], [p["cost"] for p in model.progress]):
-        assert abs(a - b) < 1e-12 * max(1.0, abs(b))
+        assert abs(a - b) < tol * max(1.0, abs(b))
+    want = _bn_running(model)
+    for r in range(1, world):
+        dp[f"r{r}"] = torch.load(tmp_path / f"bn{r}.pt", weights_only=True)["bn"]
+    for stats in [dp["bn"]] + [dp[f"r{r}"] for r in range(1, world)]:
+        for (m, v), (wm, wv) in zip(stats, want):
+            torch.testing.assert_close(m, wm, rtol=tol, atol=tol * 1e-2)
+            torch.testing.assert_close(v, wv, rtol=tol, atol=tol * 1e-2)
