@@ -1,9 +1,8 @@
 // N1b — shape-agnostic GEMM for gfx950: any M/N/K, any operand layout, bf16 / fp32 / fp64.
 //
-// Covers everything the MFMA fast path does not: tiny layers (the reference's [4,8,2]-style
-// models, vocab 27 embeddings), ragged shapes, and fp32 / fp64 models (f32-input MFMA has the
-// same rate as the f32 VALU on gfx950, so a VALU tile loses nothing there; fp64 keeps the
-// reference's precision on the GPU). Same fused epilogue contract as the MFMA kernel.
+// Covers everything the matrix-core paths do not: tiny layers (the reference's [4,8,2]-style
+// models, vocab 27 embeddings) and ragged bf16 shapes; fp32 / fp64 GEMMs of any real size run on
+// the f32 / f64 MFMA kernel (gemm_wide.hip). Same fused epilogue contract as the MFMA kernels.
 //
 // 64x64 output tile, BK = 16, 256 threads (4 waves), 4x4 outputs per thread, operands staged
 // through padded LDS ([k][m+1]) so both K-major and M-major global reads coalesce.
@@ -127,6 +126,8 @@ hipError_t launch_generic_in(const GemmArgs& p, hipStream_t s) {
 
 bool mfma_eligible(const GemmArgs& p);
 hipError_t gemm_mfma(const GemmArgs& p, hipStream_t s);
+bool wide_eligible(const GemmArgs& p);
+hipError_t gemm_wide(const GemmArgs& p, hipStream_t s);
 
 hipError_t gemm_generic(const GemmArgs& p, hipStream_t s) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
@@ -138,10 +139,11 @@ hipError_t gemm_generic(const GemmArgs& p, hipStream_t s) {
   }
 }
 
-int gemm_path(const GemmArgs& p) { return mfma_eligible(p) ? 1 : 0; }
+int gemm_path(const GemmArgs& p) { return mfma_eligible(p) ? 1 : (wide_eligible(p) ? 2 : 0); }
 
 hipError_t gemm(const GemmArgs& p, hipStream_t s) {
   if (mfma_eligible(p)) return gemm_mfma(p, s);
+  if (wide_eligible(p)) return gemm_wide(p, s);
   // bitmask / e4m3 epilogues and e4m3 operands exist on the MFMA path only
   if (p.mask != nullptr || p.out8 != nullptr || p.in_dtype == DT_FP8) return hipErrorInvalidValue;
   return gemm_generic(p, s);

@@ -70,6 +70,6 @@ int64_t gemm_split_ws_floats(const GemmArgs& args);
 // returns hipSuccess or an error; chooses the MFMA path when the shape allows
 hipError_t gemm(const GemmArgs& args, hipStream_t stream);
 // exposed for tests / benchmarks: which path gemm() would take
-int gemm_path(const GemmArgs& args);  // 0 = generic VALU, 1 = MFMA bf16
+int gemm_path(const GemmArgs& args);  // 0 = generic VALU, 1 = MFMA bf16 / fp8, 2 = MFMA fp32 / fp64
 
 }  // namespace pz

@@ -124,7 +124,8 @@ def relu_mask_cols(n: int) -> int:
 def gemm_path(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor) -> str:
     M, N = out.shape
     K = a.shape[1] if a_kc else a.shape[0]
-    return "mfma" if _ops().gemm_path(a, a_kc, b, b_kc, out, M, N, K) == 1 else "generic"
+    path = _ops().gemm_path(a, a_kc, b, b_kc, out, M, N, K)
+    return {1: "mfma", 2: "mfma_wide"}.get(path, "generic")  # mfma_wide: fp32 / fp64 matrix cores
 
 
 def _as_2d(x: Tensor) -> tuple[Tensor, tuple]:
