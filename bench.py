@@ -38,6 +38,8 @@ import torch.distributed as dist
 
 REFERENCE_SAMPLES_PER_S = {  # BASELINE.md, reference on CPU fp64 (no published numbers exist)
     "mlp4": 2064.0,
+    "mlp4_fp32": 2064.0,
+    "mlp4_fp64": 2064.0,
     "deep16x8192": 22.8,
     "mlp8192": 3095.0,
     "mlp8192_bf16": 3095.0,
@@ -53,8 +55,19 @@ CONFIGS = {
                     optimizer="adam", name="mlp[1024,8192,1024] relu,softmax (16.8M params), fp8 e4m3 fwd GEMMs"),
     "mlp8192_bf16": dict(sizes=[1024, 8192, 1024], algos=["relu", "softmax"], batch=8192, dtype="bfloat16",
                          optimizer="adam", name="mlp[1024,8192,1024] relu,softmax (16.8M params)"),
+    # the other reading of the metric name "4x8192 MLP": four 8192-wide layers, Adam (268M params)
+    "mlp4x8192": dict(sizes=[8192] * 5, algos=["relu"] * 3 + ["softmax"], batch=8192, dtype="bfloat16",
+                      optimizer="adam", name="mlp[8192]x5 (4 layers 8192-wide, 268M params)"),
+    # the headline model at the reference's own precisions: fp32 on the fused engine (f32 MFMA
+    # GEMMs), fp64 through the autograd engine (f64 MFMA GEMMs, HIP loss / stage kernels,
+    # torch.optim.Adam) — the reference epoch body (BASELINE.md method C) on the GPU
+    "mlp4_fp32": dict(sizes=[1024, 4096, 4096, 1024], algos=["relu", "relu", "softmax"], batch=8192,
+                      dtype="float32", optimizer="adam", name="mlp[1024,4096,4096,1024] relu,relu,softmax fp32"),
+    "mlp4_fp64": dict(sizes=[1024, 4096, 4096, 1024], algos=["relu", "relu", "softmax"], batch=8192,
+                      dtype="float64", optimizer="adam", engine="autograd",
+                      name="mlp[1024,4096,4096,1024] relu,relu,softmax fp64 (autograd engine)"),
 }
-DTYPE_LABEL = {"bfloat16": "bf16", "fp8": "fp8", "float32": "fp32"}
+DTYPE_LABEL = {"bfloat16": "bf16", "fp8": "fp8", "float32": "fp32", "float64": "fp64"}
 
 
 def log(msg: str) -> None:
@@ -98,6 +111,84 @@ def _launch_ranks(n: int, argv: list[str]) -> int:
     return rc
 
 
+def _emit(args, cfg, world, elapsed, costs, batch, ctx) -> None:
+    finite = all(c == c and abs(c) != float("inf") for c in costs)
+    ms = elapsed * 1e3 / args.steps
+    global_batch = batch * world
+    value = global_batch * args.steps / elapsed
+    ref = REFERENCE_SAMPLES_PER_S.get(args.config)
+    if ctx.rank != 0:
+        return
+    log(f"cost first/last = {costs[0]:.4f} / {costs[-1]:.4f}, finite={finite}")
+    print(json.dumps({
+        "metric": "training samples/sec (whole node), 4x8192 MLP bf16 at 1/2/4/8 MI355X",
+        "value": round(value, 1),
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / ref, 2) if ref else None,
+        "dtype": DTYPE_LABEL[cfg["dtype"]],
+        "data": "synthetic (random inputs/labels, random-init weights)",
+        "config": {"model": cfg["name"], "global_batch": global_batch, "per_gpu_batch": batch,
+                   "seq_len": None, "parallelism": f"dp{world}", "optimizer": cfg["optimizer"],
+                   "dist_backend": ctx.backend or "none", "dist_world_size": world,
+                   "launcher": os.environ.get("PZ_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
+                   "dropout": args.dropout, "l2": args.l2, "config_key": args.config,
+                   "engine": cfg.get("engine", "fused")},
+    }), flush=True)
+
+
+def _bench_autograd(args, cfg, model, ctx, batch, local) -> int:
+    """The reference epoch body (BASELINE.md method C: forward with dropout, CE, L2, backward,
+    optimizer step, update ratios on progress epochs) through the autograd engine on the GPU."""
+    if ctx.world_size != 1:
+        log("error: the autograd-engine bench runs on one GPU")
+        return 2
+    dev = torch.device("cuda", local)
+    g = torch.Generator(device="cpu").manual_seed(99)
+    n_data = args.n_data or 2 * batch
+    data = torch.randn(n_data, cfg["sizes"][0], generator=g).to(dev, torch.float64)
+    labels = torch.randint(0, cfg["sizes"][-1], (n_data,), generator=g).to(dev)
+    total = args.warmup + args.steps
+    every = max(1, total // 100)
+    lr0, decay = args.lr, 0.999
+    costs = []
+
+    def run(epoch: int) -> None:
+        picks = torch.randint(0, n_data, (batch,), device=dev)
+        x, y = data[picks], labels[picks]
+        for group in model.optimizer.param_groups:
+            group["lr"] = lr0 * decay ** epoch
+        prev = [w.detach().clone() for w in model.weights] if epoch % every == 0 else None
+        for p in model.params:
+            p.requires_grad_()
+        _, cost = model._forward(x, y, args.dropout)
+        cost = cost + args.l2 * sum((w ** 2).sum() for w in model.weights)
+        for p in model.params:
+            p.grad = None
+        cost.backward()
+        model.optimizer.step()
+        if prev is not None:
+            with torch.no_grad():
+                [((w - pw).std() / (w.std() + 1e-8)) for pw, w in zip(prev, model.weights)]
+        costs.append(cost.detach())
+
+    for e in range(args.warmup):
+        run(e)
+    torch.cuda.synchronize()
+    start = time.perf_counter()
+    for e in range(args.warmup, total):
+        run(e)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - start
+    _emit(args, cfg, 1, elapsed, [float(c) for c in costs[args.warmup:]], batch, ctx)
+    return 0
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -107,6 +198,10 @@ def main(argv=None) -> int:
     ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: config)")
     ap.add_argument("--dropout", type=float, default=0.2)
     ap.add_argument("--l2", type=float, default=1e-3)
+    # learning checks (not the headline): --lr 0.05 --weight-algo he --n-data 8192 --dropout 0 --l2 0
+    ap.add_argument("--lr", type=float, default=1e-3)
+    ap.add_argument("--weight-algo", default="xavier")
+    ap.add_argument("--n-data", type=int, default=None, help="synthetic dataset rows (default 2 x batch)")
     raw = list(sys.argv[1:] if argv is None else argv)
     args = ap.parse_args(raw)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -129,17 +224,19 @@ def main(argv=None) -> int:
     batch = args.batch or cfg["batch"]
 
     torch.manual_seed(1234)
-    model = NeuralNetworkModel("bench", cfg["sizes"], "xavier", "zeros", cfg["algos"], cfg["optimizer"],
+    model = NeuralNetworkModel("bench", cfg["sizes"], args.weight_algo, "zeros", cfg["algos"], cfg["optimizer"],
                                dtype=cfg["dtype"], device=f"cuda:{local}")
+    if cfg.get("engine") == "autograd":
+        return _bench_autograd(args, cfg, model, ctx, batch, local)
     trainer = FusedTrainer(model, ctx)
-    n_data = 2 * batch
+    n_data = args.n_data or 2 * batch
     g = torch.Generator(device="cpu").manual_seed(99 + rank)
     inputs = torch.randn(n_data, cfg["sizes"][0], generator=g)
     labels = torch.randint(0, cfg["sizes"][-1], (n_data,), generator=g)
     trainer.load_tensors(inputs, labels, seed=7 + rank)
     total = args.warmup + args.steps
     global_batch = batch * world
-    lr0, decay = 1e-3, 0.999
+    lr0, decay = args.lr, 0.999
     # the schedule lets the trainer tabulate per-epoch hyper-parameters and replay captured
     # hipGraphs of the step (single GPU); steps are launched eagerly under data parallelism
     trainer.begin(total, lr_schedule=lambda e: lr0 * decay ** e)
@@ -168,31 +265,7 @@ def main(argv=None) -> int:
     elapsed = ctx.all_reduce_scalar_max(elapsed)
 
     costs = [c for _, c, _, _ in trainer.drain()]
-    finite = all(c == c and abs(c) != float("inf") for c in costs)
-    ms = elapsed * 1e3 / args.steps
-    value = global_batch * args.steps / elapsed
-    ref = REFERENCE_SAMPLES_PER_S.get(args.config)
-    if rank == 0:
-        log(f"cost first/last = {costs[0]:.4f} / {costs[-1]:.4f}, finite={finite}")
-        print(json.dumps({
-            "metric": "training samples/sec (whole node), 4x8192 MLP bf16 at 1/2/4/8 MI355X",
-            "value": round(value, 1),
-            "unit": "samples/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / ref, 2) if ref else None,
-            "dtype": DTYPE_LABEL[cfg["dtype"]],
-            "data": "synthetic (random inputs/labels, random-init weights)",
-            "config": {"model": cfg["name"], "global_batch": global_batch, "per_gpu_batch": batch,
-                       "seq_len": None, "parallelism": f"dp{world}", "optimizer": cfg["optimizer"],
-                       "dist_backend": ctx.backend or "none", "dist_world_size": world,
-                       "launcher": os.environ.get("PZ_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
-                       "dropout": args.dropout, "l2": args.l2, "config_key": args.config},
-        }), flush=True)
+    _emit(args, cfg, world, elapsed, costs, batch, ctx)
     if dist.is_initialized():
         dist.destroy_process_group()
     return 0

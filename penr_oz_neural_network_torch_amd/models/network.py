@@ -243,7 +243,7 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         return out.tolist(), cost.item() if cost.numel() > 0 else None
 
     def _forward(self, input_tensor: Tensor, target: list, dropout_rate=0.0) -> Tuple[list[Tensor], Tensor]:
-        target_specified = target is not None and all(t is not None for t in target)
+        target_specified = target is not None and (isinstance(target, Tensor) or all(t is not None for t in target))
         gpu = self.on_gpu
         if gpu:
             from ..ops import functional as PF
@@ -263,8 +263,11 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         if not target_specified:
             cost = torch.empty(0)
         elif self.algos[-1] == "softmax":  # CE on the softmax layer's input (reference :400-403)
-            labels = target[0] if logits.ndim == 1 else [t[0] for t in target]
-            label_tensor = torch.tensor(labels, dtype=torch.int64)
+            if isinstance(target, Tensor):  # programmatic use: class ids already as a tensor
+                label_tensor = target.reshape(-1).to(torch.int64)
+            else:
+                labels = target[0] if logits.ndim == 1 else [t[0] for t in target]
+                label_tensor = torch.tensor(labels, dtype=torch.int64)
             if gpu:
                 cost = PF.cross_entropy(logits.to(self._loss_dtype), label_tensor.to(self.device))
             else:
