@@ -41,6 +41,7 @@ int dt_of(const Tensor& t) {
     case at::kFloat: return pz::DT_F32;
     case at::kDouble: return pz::DT_F64;
     case at::kFloat8_e4m3fn: return pz::DT_FP8;
+    case at::kFloat8_e5m2: return pz::DT_FP8;  // gradient operands (GemmArgs::a_fmt = 1)
     default: TORCH_CHECK(false, "pz: unsupported dtype ", t.scalar_type());
   }
   return -1;
@@ -95,7 +96,9 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   // (fp8 extras are attached by gemm_fp8_extras below)
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "pz::gemm: 2-D operands expected");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "pz::gemm: unit inner stride expected");
-  TORCH_CHECK(A.scalar_type() == B.scalar_type(), "pz::gemm: A/B dtype mismatch");
+  TORCH_CHECK(A.scalar_type() == B.scalar_type() ||
+                  (A.scalar_type() == at::kFloat8_e5m2 && B.scalar_type() == at::kFloat8_e4m3fn),
+              "pz::gemm: A/B dtype mismatch (mixed fp8: e5m2 A x e4m3 B only)");
   TORCH_CHECK(a_kc ? (A.size(0) >= M && A.size(1) >= K) : (A.size(0) >= K && A.size(1) >= M), "pz::gemm: A shape");
   TORCH_CHECK(b_kc ? (B.size(0) >= N && B.size(1) >= K) : (B.size(0) >= K && B.size(1) >= N), "pz::gemm: B shape");
   TORCH_CHECK(C.size(0) >= M && C.size(1) >= N, "pz::gemm: C shape");
@@ -176,6 +179,8 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
                      force_generic, mask);
   p.scale_a = f32_scalar_ptr(scale_a, "scale_a");
   p.scale_b = f32_scalar_ptr(scale_b, "scale_b");
+  p.a_fmt = A.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
+  TORCH_CHECK(B.scalar_type() != at::kFloat8_e5m2, "pz::gemm: e5m2 is supported for the A operand (gradients) only");
   if (out8.has_value() && out8->defined()) {
     TORCH_CHECK(out8->scalar_type() == at::kFloat8_e4m3fn && out8->dim() == 2 && out8->stride(1) == 1 &&
                     out8->size(0) >= M && out8->size(1) >= N,
@@ -558,12 +563,12 @@ void amax_abs_op(const Tensor& x, const Tensor& amax) {
   PZ_HIP_CHECK(pz::amax_abs(x.data_ptr(), dt_of(x), x.numel(), amax.data_ptr<float>(), cur_stream(x)));
 }
 
-void scale_update_op(const Tensor& amax, const Tensor& qs, double headroom, bool reset) {
+void scale_update_op(const Tensor& amax, const Tensor& qs, double headroom, bool reset, double maxval) {
   check_dev(amax, "amax");
   TORCH_CHECK(amax.scalar_type() == at::kFloat && qs.scalar_type() == at::kFloat && qs.numel() >= 2 * amax.numel(),
               "pz::scale_update: fp32 amax[n], qs[2n]");
   PZ_HIP_CHECK(pz::scale_update(amax.data_ptr<float>(), qs.data_ptr<float>(), static_cast<int>(amax.numel()),
-                                static_cast<float>(headroom), reset, cur_stream(amax)));
+                                static_cast<float>(headroom), reset, cur_stream(amax), static_cast<float>(maxval)));
 }
 
 void quant_transpose_op(const Tensor& w, const Tensor& out, const Tensor& qs, const optional<Tensor>& amax,
@@ -586,14 +591,15 @@ void quant_transpose_op(const Tensor& w, const Tensor& out, const Tensor& qs, co
 
 void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, const optional<Tensor>& amax) {
   check_dev(x, "x");
+  const bool e5m2 = out.scalar_type() == at::kFloat8_e5m2;
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && out.dim() == 2 && out.stride(1) == 1 &&
-                  out.scalar_type() == at::kFloat8_e4m3fn && out.size(0) >= x.size(0) && out.size(1) >= x.size(1) &&
-                  out.stride(0) % 4 == 0,
-              "pz::quantize_rows: x [rows, cols], out e4m3 [rows, cols]");
+                  (out.scalar_type() == at::kFloat8_e4m3fn || e5m2) && out.size(0) >= x.size(0) &&
+                  out.size(1) >= x.size(1) && out.stride(0) % 4 == 0 && x.size(1) % 4 == 0,
+              "pz::quantize_rows: x [rows, cols % 4 == 0], out e4m3 / e5m2 [rows, cols]");
   PZ_HIP_CHECK(pz::quantize_rows(x.data_ptr(), dt_of(x), x.stride(0), static_cast<int>(x.size(0)),
                                  static_cast<int>(x.size(1)), static_cast<uint8_t*>(out.data_ptr()), out.stride(0),
                                  qs.data_ptr<float>(), amax.has_value() ? amax->data_ptr<float>() : nullptr,
-                                 cur_stream(x)));
+                                 cur_stream(x), e5m2 ? 1 : 0));
 }
 
 void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tensor& stats_prev, const Tensor& stats_cur,
@@ -736,7 +742,7 @@ TORCH_LIBRARY(pz, m) {
         "int nslots, float l2, Tensor(b!) costs, int epoch, Tensor(c!) ratios, int ratio_row, "
         "Tensor(d!)? epoch_ctr=None, int every=1) -> ()");
   m.def("amax_abs(Tensor x, Tensor(a!) amax) -> ()");
-  m.def("scale_update(Tensor(a!) amax, Tensor(b!) qs, float headroom, bool reset) -> ()");
+  m.def("scale_update(Tensor(a!) amax, Tensor(b!) qs, float headroom, bool reset, float maxval=448.0) -> ()");
   m.def("quant_transpose(Tensor w, Tensor(a!) out, Tensor(b!) qs, Tensor? amax=None, Tensor(c!)? amax_clear=None) -> ()");
   m.def("quantize_rows(Tensor x, Tensor(a!) out, Tensor qs, Tensor(b!)? amax) -> ()");
   m.def("format_json_array(Tensor t, int level) -> str");

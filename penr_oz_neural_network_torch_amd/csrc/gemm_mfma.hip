@@ -356,7 +356,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 
   // VAR 8: e4m3 operands (both K-contiguous), v_mfma_scale_f32_32x32x64_f8f6f4 with unit block
   // scales: a ring slot holds 64 K-bytes per row (the bf16 slot geometry), one MFMA K-step
-  constexpr bool F8 = VAR == 8;
+  // VAR 9: A in e5m2 (bf8: gradients, wide range), B in e4m3 — the backward dX GEMM
+  // dZ8 · W8ᵀ of the fp8 policy, with the backward (EPI_BWD) epilogues
+  constexpr bool F8 = VAR == 8 || VAR == 9;
+  constexpr int F8_FMT_A = VAR == 9 ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
   static_assert(!F8 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "fp8: K-contiguous in, bf16 out");
   constexpr int TM8 = C::WTM / 32, TN8 = C::WTN / 32;
   struct Frags16 { i16x8_t a[KB][C::TM]; i16x8_t b[KB][C::TN]; };
@@ -382,8 +385,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 #pragma unroll
       for (int i = 0; i < TM8; ++i)
 #pragma unroll
-        for (int j = 0; j < TN8; ++j)  // cbsz/blgp 0 = e4m3; E8M0 block scales 127 = 1.0
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[j], f.a[i], acc[i][j], 0, 0, 0, 127, 0, 127);
+        for (int j = 0; j < TN8; ++j)  // issued as mfma(B, A): cbsz = B's format, blgp = A's;
+                                       // E8M0 block scales 127 = 1.0
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[j], f.a[i], acc[i][j], 0, F8_FMT_A, 0, 127,
+                                                                       0, 127);
     } else {
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
@@ -651,7 +656,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   const int g4 = 4 * (lane >> 4);
   if constexpr (F8) {
     const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
-    epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    if constexpr (VAR == 9) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
   } else if constexpr (std::is_same<OutT, uint16_t>::value) {
     epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
   } else {
@@ -784,6 +790,10 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
 
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  if (p.a_fmt == 1) {  // e5m2 x e4m3 (backward dX)
+    if (tiles >= 240 || p.split_k > 1) return launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>(p, s);
+    return launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 9>(p, s);
+  }
   if (tiles >= 240 || p.split_k > 1) return launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
   return launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
 }
@@ -801,7 +811,11 @@ bool fp8_eligible(const GemmArgs& p) {
   if (!al16(p.A) || !al16(p.B) || !al16(p.C)) return false;
   if (p.idx_ld % 2 != 0) return false;
   if (p.bias != nullptr && !al16(p.bias)) return false;
-  if (p.epi_mode == EPI_BWD) return false;  // fp8 is a forward-only operand format here
+  // e4m3 x e4m3: forward stages; e5m2 (A, gradients) x e4m3 (B): backward dX stages only
+  if ((p.a_fmt == 1) != (p.epi_mode == EPI_BWD) || (p.a_fmt == 1 && p.out8 != nullptr)) return false;
+  if (p.epi_mode == EPI_BWD && p.mask == nullptr &&
+      (p.aux == nullptr || p.aux_dtype != DT_BF16 || p.ldaux % 8 != 0 || (reinterpret_cast<uintptr_t>(p.aux) & 15)))
+    return false;
   if (p.mask != nullptr && (p.ldmask % 8 != 0 || (reinterpret_cast<uintptr_t>(p.mask) & 7) != 0)) return false;
   if (p.out8 != nullptr && (p.ldout8 % 8 != 0 || (reinterpret_cast<uintptr_t>(p.out8) & 7) != 0 ||
                             p.out8_qscale == nullptr))

@@ -216,13 +216,16 @@ hipError_t embedding_bwd(const void* dout, int dout_dtype, const void* idx, int 
 // ------------------------------------------------------------------ fp8 quantisation
 // qs records are {q, s}: T8 = sat(T * q), T ~= T8 * s
 hipError_t amax_abs(const void* x, int dtype, int64_t n, float* amax, hipStream_t s);
-hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool reset, hipStream_t s);
+// q = maxval / (amax * headroom): maxval 448 for e4m3 records, 57344 for e5m2 (gradients)
+hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool reset, hipStream_t s,
+                        float maxval = 448.f);
 // amax != nullptr: q = 448 / *amax is derived in-kernel (the optimizer reduced it), {q, 1/q} are
 // written to qs, and *amax_clear (the other parity's accumulator) is reset for the next update
 hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, float* qs,
                            const float* amax, float* amax_clear,
                            hipStream_t s);
+// fmt 0: e4m3 (sat 448), 1: e5m2 (sat 57344)
 hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
-                         const float* qs, float* amax, hipStream_t s);
+                         const float* qs, float* amax, hipStream_t s, int fmt = 0);
 
 }  // namespace pz

@@ -49,6 +49,7 @@ struct GemmArgs {
   // per-tensor factors *scale_a * *scale_b (nullptr = 1) on top of alpha
   const float* scale_a;
   const float* scale_b;
+  int a_fmt;  // fp8 A operand format: 0 = e4m3, 1 = e5m2 (gradients; B stays e4m3)
   // EPI_FWD extra output: e4m3 copy of C, out8[m*ldout8 + n] = sat(C * *out8_qscale), and the
   // running max |C| (atomicMax into *amax, which the caller zeroes) for delayed scaling
   uint8_t* out8;

@@ -21,6 +21,11 @@ PZ_DEV uint8_t to_e4m3(float x) {
   x = fminf(fmaxf(x, -kE4m3Max), kE4m3Max);
   return static_cast<uint8_t>(__builtin_amdgcn_cvt_pk_fp8_f32(x, 0.f, 0, false) & 0xFF);
 }
+constexpr float kE5m2Max = 57344.f;
+PZ_DEV uint8_t to_e5m2(float x) {
+  x = fminf(fmaxf(x, -kE5m2Max), kE5m2Max);
+  return static_cast<uint8_t>(__builtin_amdgcn_cvt_pk_bf8_f32(x, 0.f, 0, false) & 0xFF);
+}
 
 // one atomic per BLOCK (same-address atomics serialise: one per wave over a 4096-block grid
 // cost 190 us for 8 M elements)
@@ -56,11 +61,11 @@ __global__ void __launch_bounds__(256) amax_kernel(const T* __restrict__ x, int6
 }
 
 // amax -> {q, s}; optionally clears amax for the next accumulation window
-__global__ void scale_update_kernel(float* amax, float* qs, int n, float headroom, int reset) {
+__global__ void scale_update_kernel(float* amax, float* qs, int n, float headroom, int reset, float maxval) {
   const int i = threadIdx.x + blockIdx.x * blockDim.x;
   if (i >= n) return;
   const float a = amax[i];
-  const float q = a > 0.f ? kE4m3Max / (a * headroom) : 1.f;
+  const float q = a > 0.f ? maxval / (a * headroom) : 1.f;
   qs[2 * i] = q;
   qs[2 * i + 1] = 1.f / q;
   if (reset) amax[i] = 0.f;
@@ -113,8 +118,9 @@ __global__ void __launch_bounds__(256) quant_transpose_kernel(const float* __res
   }
 }
 
-// x [rows][cols] (bf16 or fp32, row stride ldx) -> x8 [rows][ldo] with quantisation factor qs[0]
-template <typename T>
+// x [rows][cols] (bf16 or fp32, row stride ldx) -> x8 [rows][ldo] (e4m3, or e5m2 when E5M2)
+// with quantisation factor qs[0]
+template <typename T, bool E5M2>
 __global__ void __launch_bounds__(256) quantize_rows_kernel(const T* __restrict__ x, int64_t ldx, int rows, int cols,
                                                             uint8_t* __restrict__ out, int64_t ldo,
                                                             const float* __restrict__ qs, float* amax) {
@@ -129,7 +135,7 @@ __global__ void __launch_bounds__(256) quantize_rows_kernel(const T* __restrict_
     for (int e = 0; e < 4; ++e) {
       const float v = to_f(x[static_cast<int64_t>(r) * ldx + c + e]);
       m = fmaxf(m, fabsf(v));
-      packed |= static_cast<uint32_t>(to_e4m3(v * q)) << (8 * e);
+      packed |= static_cast<uint32_t>(E5M2 ? to_e5m2(v * q) : to_e4m3(v * q)) << (8 * e);
     }
     *reinterpret_cast<uint32_t*>(out + static_cast<int64_t>(r) * ldo + c) = packed;
   }
@@ -154,9 +160,10 @@ hipError_t amax_abs(const void* x, int dtype, int64_t n, float* amax, hipStream_
   return hipGetLastError();
 }
 
-hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool reset, hipStream_t s) {
+hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool reset, hipStream_t s, float maxval) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(scale_update_kernel, dim3((n + 63) / 64), dim3(64), 0, s, amax, qs, n, headroom, reset ? 1 : 0);
+  hipLaunchKernelGGL(scale_update_kernel, dim3((n + 63) / 64), dim3(64), 0, s, amax, qs, n, headroom, reset ? 1 : 0,
+                     maxval);
   return hipGetLastError();
 }
 
@@ -169,19 +176,26 @@ hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* o
   return hipGetLastError();
 }
 
-hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
-                         const float* qs, float* amax, hipStream_t s) {
-  if (rows <= 0 || cols <= 0) return hipSuccess;
-  if (cols % 4 != 0) return hipErrorInvalidValue;
+template <bool E5M2>
+hipError_t quantize_rows_fmt(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
+                             const float* qs, float* amax, hipStream_t s) {
   const int g = grid_for(static_cast<int64_t>(rows) * (cols / 4), 256 * 8, 1024);
   if (dtype == DT_BF16)
-    hipLaunchKernelGGL(quantize_rows_kernel<uint16_t>, dim3(g), dim3(256), 0, s, static_cast<const uint16_t*>(x), ldx,
-                       rows, cols, out, ldo, qs, amax);
+    hipLaunchKernelGGL((quantize_rows_kernel<uint16_t, E5M2>), dim3(g), dim3(256), 0, s,
+                       static_cast<const uint16_t*>(x), ldx, rows, cols, out, ldo, qs, amax);
   else if (dtype == DT_F32)
-    hipLaunchKernelGGL(quantize_rows_kernel<float>, dim3(g), dim3(256), 0, s, static_cast<const float*>(x), ldx, rows,
-                       cols, out, ldo, qs, amax);
+    hipLaunchKernelGGL((quantize_rows_kernel<float, E5M2>), dim3(g), dim3(256), 0, s, static_cast<const float*>(x),
+                       ldx, rows, cols, out, ldo, qs, amax);
   else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
+                         const float* qs, float* amax, hipStream_t s, int fmt) {
+  if (rows <= 0 || cols <= 0) return hipSuccess;
+  if (cols % 4 != 0) return hipErrorInvalidValue;
+  if (fmt == 1) return quantize_rows_fmt<true>(x, dtype, ldx, rows, cols, out, ldo, qs, amax, s);
+  return quantize_rows_fmt<false>(x, dtype, ldx, rows, cols, out, ldo, qs, amax, s);
 }
 
 }  // namespace pz

@@ -220,6 +220,13 @@ class FusedTrainer:
             self.wamax = torch.zeros(len(gemms), device=self.dev)
             self.aqs = torch.ones(len(self.stages), 2, device=self.dev)     # activations (delayed)
             self.aamax = torch.zeros(len(self.stages), device=self.dev)
+            # backward dX GEMMs: e5m2 gradients (delayed scaling, q = 57344 / (2 amax of the previous
+            # step; the first step calibrates on its own amax) x e4m3 weights [in, out] (current
+            # scaling, the forward copy's scale)
+            self.gqs = torch.ones(len(self.stages), 2, device=self.dev)
+            self.gamax = torch.zeros(len(self.stages), device=self.dev)
+            self._g8_calibrated = False
+            self.w8n: dict[int, torch.Tensor] = {}
             self.xqs = torch.ones(2, device=self.dev)                       # first-layer input
             self.xamax = torch.zeros(1, device=self.dev)
             # weight amax accumulators per shadow parity: the optimizer update max-es |w_new| into
@@ -230,6 +237,9 @@ class FusedTrainer:
                 st.w8_index = k
                 self.w8[st.seg_w.offset] = torch.empty(st.seg_w.shape[1], st.seg_w.shape[0], device=self.dev,
                                                        dtype=torch.float8_e4m3fn)
+                if k > 0 and os.environ.get("PZ_FP8_BWD", "1") != "0":  # dX operand of layers 2..n
+                    self.w8n[st.seg_w.offset] = torch.empty(st.seg_w.shape, device=self.dev,
+                                                            dtype=torch.float8_e4m3fn)
             self._refresh_fp8_weights()
             self.opt.set_amax([{st.seg_w.offset: self.wamax2[p % 2, st.w8_index:st.w8_index + 1] for st in gemms}
                                for p in range(len(self.shadow_sets))])
@@ -403,10 +413,13 @@ class FusedTrainer:
                 p = parity % 2
                 ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k], self.wamax2[p, k:k + 1],
                                     self.wamax2[1 - p, k:k + 1])
-                continue
-            ops.amax_abs(w, self.wamax[k:k + 1])
-            ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
-            ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
+            else:
+                ops.amax_abs(w, self.wamax[k:k + 1])
+                ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
+                ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
+            w8n = self.w8n.get(st.seg_w.offset)
+            if w8n is not None:  # [in, out] copy for the backward dX GEMM, same scale
+                ops.quantize_rows(w, w8n, self.wqs[k], None)
 
     def _opt_async(self, items: list) -> None:
         """Queue the updates of optimizer groups ``[(key, handles, stages)]`` on the side stream
@@ -460,6 +473,19 @@ class FusedTrainer:
                 self.x8 = x8
             else:
                 prev.buffers["y8"] = x8
+        for i, st in enumerate(self.stages):  # backward: e5m2 dZ x e4m3 W for fused dX GEMMs
+            st.fp8_bwd = False
+            st.buffers.pop("g8", None)
+            prev = self.stages[i - 1] if i > 0 else None
+            # (the [in, out] e4m3 copy is single-buffered: the update of W must not run before this
+            # step's dX GEMM has read it — true with the updates queued after the dX GEMMs)
+            if (st.kind != "gemm" or not st.fp8 or prev is None or prev.kind != "gemm" or not prev.has_epi
+                    or st.seg_w.offset not in self.w8n or not self._after_dx):
+                continue
+            if st.out_width % 64 or prev.out_width % 8 or rows_b < 64:
+                continue
+            st.fp8_bwd = True
+            st.buffers["g8"] = torch.empty(st.buffers["g"].shape, device=self.dev, dtype=torch.float8_e5m2)
         self.data8 = None
         if self.x8 is not None:
             # first-layer input: the device-resident dataset is quantised to e4m3 ONCE with a static
@@ -704,6 +730,10 @@ class FusedTrainer:
             before = self.stages[si - 1] if si > 0 else None
             x_in = before.buffers["y"] if before is not None else self.x_in
             g, g_pre = self._backward_stage(st, before, x_in, g, g_pre, batch, dropout, keys, rec, handles)
+        if self.fp8 and any(getattr(st, "fp8_bwd", False) for st in self.stages):
+            # this step's gradient amax -> next step's e5m2 scales (delayed scaling)
+            torch.ops.pz.scale_update(self.gamax, self.gqs, 2.0, True, 57344.0)
+            self._g8_calibrated = True
 
         # ---------------- reduce + update
         self._phase("pz.update")
@@ -963,6 +993,17 @@ class FusedTrainer:
             colsum = self.store.view(before.seg_b, self.grads) if (before.kind == "gemm" and before.seg_b is not None) \
                 else None
             mask = before.buffers.get("mask")
+            if getattr(st, "fp8_bwd", False):  # e5m2 dZ x e4m3 W on the scaled fp8 MFMA
+                k, g8 = st.index, st.buffers["g8"]
+                ops = torch.ops.pz
+                if not self._g8_calibrated:  # first step: current scaling from this gradient
+                    ops.amax_abs(g, self.gamax[k:k + 1])
+                    ops.scale_update(self.gamax[k:k + 1], self.gqs[k], 2.0, True, 57344.0)
+                ops.quantize_rows(g, g8, self.gqs[k], self.gamax[k:k + 1])
+                PF.gemm(g8, True, self.w8n[st.seg_w.offset], True, dx,
+                        aux=None if mask is not None else before.buffers["y"], colsum=colsum, mode=PF.EPI_BWD,
+                        epi=(ei, ef), mask=mask, scale_a=self.gqs[k, 1:2], scale_b=self.wqs[st.w8_index, 1:2])
+                return dx, True
             PF.gemm(g, True, self._w(st), True, dx, aux=None if mask is not None else before.buffers["y"],
                     colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask)
             return dx, True

@@ -165,8 +165,8 @@ def test_record_mode_matches_fused_cost():
 
 def test_fp8_training_tracks_bf16():
     """fp8 policy: e4m3 forward GEMMs (current-scaled weights, delayed-scaled activations, e4m3
-    input at a static dataset scale) with bf16 backward; the loss curve follows the bf16 run of the
-    same model + batches."""
+    input at a static dataset scale), e5m2-gradient x e4m3-weight backward dX GEMMs (delayed
+    gradient scaling), bf16 dW; the loss curve follows the bf16 run of the same model + batches."""
     sizes = [256, 512, 512, 128]
     algos = ["relu", "relu", "softmax"]
     n, S, steps = 4096, 1024, 12
@@ -186,6 +186,10 @@ def test_fp8_training_tracks_bf16():
         curves[dtype] = [c for _, c, _, _ in tr.drain()]
         if dtype == "fp8":
             assert [st.fp8 for st in tr.stages] == [True, True, True]
+            # backward dX GEMMs of layers 2 and 3 on e5m2 gradients x e4m3 [in, out] weights
+            assert [st.fp8_bwd for st in tr.stages] == [False, True, True]
+            s_g = tr.gqs[1:, 1].cpu()
+            assert torch.all(s_g > 0) and torch.all(torch.isfinite(s_g)) and tr._g8_calibrated
             assert "y8" in tr.stages[0].buffers and "y8" in tr.stages[1].buffers
             s_w = tr.wqs[:, 1].cpu()
             assert torch.all(s_w > 0) and torch.all(torch.isfinite(s_w))

@@ -144,6 +144,48 @@ def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
     assert (out_bit.double() - ref).abs().max().item() < 0.02 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (8192, 8192, 1024), (300, 264, 192)])
+def test_gemm_fp8_e5m2_backward(native_lib, M, N, K):
+    """Backward dX of the fp8 policy: e5m2 gradient x e4m3 weight (v_mfma_scale_f32_32x32x64_f8f6f4
+    with mixed formats) + dequant scales + the ReLU-bitmask derivative / dropout scales + bias-grad
+    column sums, against an fp64 reference on the same e5m2 / e4m3 values; and the e5m2 quantiser."""
+    p, seed = 0.2, (5, 6)
+    g = torch.randn(M, K, device=DEV) * 1e-3                       # dZ (bf16 in the trainer)
+    gb = g.to(torch.bfloat16)
+    qs = torch.tensor([57344.0 / (2 * gb.float().abs().max().item()), 0.0], device=DEV)
+    qs[1] = 1.0 / qs[0]
+    g8 = torch.empty(M, K, device=DEV, dtype=torch.float8_e5m2)
+    amax = torch.zeros(1, device=DEV)
+    torch.ops.pz.quantize_rows(gb, g8, qs, amax)
+    assert amax.item() == gb.float().abs().max().item()
+    exp8 = (gb.float() * qs[0]).to(torch.float8_e5m2)
+    assert (g8.view(torch.uint8) != exp8.view(torch.uint8)).float().mean().item() < 1e-4
+    w8 = (torch.randn(N, K, device=DEV) * 8).to(torch.float8_e4m3fn)  # W stored [in, out] = B[n][k]
+    sb = torch.tensor([1.0 / 16], device=DEV)
+    y = torch.relu(torch.randn(M, N, device=DEV)).to(torch.bfloat16)
+    mask = torch.zeros(M, PF.relu_mask_cols(N), device=DEV, dtype=torch.uint8)
+    yb = (y.float() > 0).reshape(M, N // 8, 8) if N % 8 == 0 else None
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    colsum = torch.zeros(N, device=DEV)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=p, seed=seed)
+    if yb is not None:  # the trainer's form: ReLU bitmask written by the forward
+        bits = (yb.int() << torch.arange(8, device=DEV, dtype=torch.int32)).sum(-1).to(torch.uint8)
+        mask[:, :N // 8] = bits
+        PF.gemm(g8, True, w8, True, out, colsum=colsum, mode=PF.EPI_BWD, epi=epi, mask=mask, scale_a=qs[1:2],
+                scale_b=sb)
+    else:
+        PF.gemm(g8, True, w8, True, out, aux=y, colsum=colsum, mode=PF.EPI_BWD, epi=epi, scale_a=qs[1:2], scale_b=sb)
+    h = (g8.double() @ w8.double().t()) * (qs[1].double() / 16)
+    scale = 1.0 / (1 - p) ** 2  # relu' x both dropout scales (y > 0 implies kept by both)
+    ref = h * (y.double() > 0) * scale
+    err = (out.double() - ref).abs().max().item()
+    assert err < 0.01 * ref.abs().max().item(), err
+    assert (colsum.double() - out.double().sum(0)).abs().max().item() < 2e-3 * out.double().abs().sum(0).max().item()
+    # the fp8 product itself tracks the exact fp64 GEMM of the unquantised operands
+    exact = (gb.double() @ (w8.double().t() / 16)) * (y.double() > 0) * scale
+    assert (out.double() - exact).abs().max().item() < 0.15 * exact.abs().max().item()
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (4096 + 64, 4096, 512), (256, 1024, 8192)])
 def test_gemm_fp8_forward(native_lib, M, N, K):
     """e4m3 x e4m3 (v_mfma_scale_f32_32x32x64_f8f6f4) + dequant scales + fused stage epilogue +
