@@ -9,6 +9,7 @@
 #include "../penr_oz_neural_network_torch_amd/csrc/gemm_mfma.hip"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -59,7 +60,6 @@ struct Variant {
   {                                                                                  \
     {"buf", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 6>},                 \
         {"bk64g0buf", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 30>},      \
-        {"bk64spbuf", launch_cfg<256, 256, 2, 4, AKC, BKC, OUT, uint16_t, 31>},      \
   }
 
 struct Case {
@@ -84,7 +84,7 @@ int main(int argc, char** argv) {
       {"dX_L3", B, 4096, 1024, true, true, false},   {"fwd_L3", B, 1024, 4096, true, false, false},
       {"dW_L3", 4096, 1024, B, false, false, true},  {"dW_L1", 1024, 4096, B, false, false, true},
   };
-  const int rounds = 5, iters = 20;
+  const int rounds = getenv("LAB_ROUNDS") ? atoi(getenv("LAB_ROUNDS")) : 5, iters = 20;
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (const Case& c : cases) {
