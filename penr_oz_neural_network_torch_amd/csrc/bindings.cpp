@@ -403,7 +403,7 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
                        int64_t num_segments, int64_t total_blocks, bool adam, double lr, double beta1, double beta2,
                        double eps, double bias_c1, double bias_c2_sqrt, double grad_scale, double l2,
                        const optional<Tensor>& stats, const optional<Tensor>& hp, const optional<Tensor>& epoch,
-                       int64_t stats_every) {
+                       int64_t stats_every, int64_t max_grid) {
   check_dev(params, "params");
   TORCH_CHECK(params.scalar_type() == at::kFloat && grads.scalar_type() == at::kFloat, "pz::optimizer_step: fp32 master");
   pz::OptArgs a{};
@@ -427,6 +427,7 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
   a.l2_lambda = static_cast<float>(l2);
   a.stats = ptr_or_null<double>(stats);
   a.stats_every = static_cast<int>(stats_every);
+  a.max_grid = static_cast<int>(max_grid);
   if (stats_every > 1) TORCH_CHECK(epoch.has_value() && epoch->defined(), "pz::optimizer_step: stats_every > 1 needs the epoch counter");
   if (epoch.has_value() && epoch->defined()) a.epoch_ptr = epoch_counter(epoch);
   if (hp.has_value() && hp->defined()) {
@@ -725,7 +726,7 @@ TORCH_LIBRARY(pz, m) {
   m.def("optimizer_step(Tensor(a!) params, Tensor(e!) grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
         "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
         "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats, Tensor? hp=None, "
-        "Tensor? epoch=None, int stats_every=1) -> ()");
+        "Tensor? epoch=None, int stats_every=1, int max_grid=0) -> ()");
   m.def("segment_stats(Tensor params, Tensor segments, Tensor block_seg, int num_segments, int total_blocks, "
         "Tensor(a!) stats) -> ()");
   m.def("tensor_moments(Tensor x, int row_len, int rule, float thr, Tensor(a!) out) -> ()");

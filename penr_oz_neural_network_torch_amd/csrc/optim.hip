@@ -281,7 +281,8 @@ hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
     const char* e = getenv("PZ_OPT_GRID");
     return e ? atoi(e) : 0;
   }();
-  const int grid = max_grid > 0 && max_grid < a.total_blocks ? max_grid : a.total_blocks;
+  const int cap = a.max_grid > 0 ? a.max_grid : max_grid;
+  const int grid = cap > 0 && cap < a.total_blocks ? cap : a.total_blocks;
   if (a.adam) hipLaunchKernelGGL(optimizer_kernel<true>, dim3(grid), dim3(kThreads), 0, s, a);
   else hipLaunchKernelGGL(optimizer_kernel<false>, dim3(grid), dim3(kThreads), 0, s, a);
   return hipGetLastError();

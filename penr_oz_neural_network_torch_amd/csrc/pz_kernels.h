@@ -117,6 +117,7 @@ struct OptArgs {
   // update-ratio sums (sum dw, sum dw^2, sum w): 1 = this launch, 0 = not (only sum w^2, which the
   // next step's L2 cost term needs), k > 1 = when the device epoch (*epoch_ptr) % k == 0
   int stats_every;
+  int max_grid;                // > 0: at most this many workgroups (they loop over the work blocks)
 };
 
 constexpr int kOptElemsPerBlock = 4096;

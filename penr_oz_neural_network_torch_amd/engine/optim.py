@@ -164,11 +164,13 @@ class FusedOptimizer:
         self._launch(grads, self.segments_p[parity], self.block_seg, self.num_segments, self.total_blocks, l2,
                      grad_scale)
 
-    def step_group(self, key, grads: torch.Tensor, l2: float, grad_scale: float, parity: int = 0) -> None:
-        """Update one group (define_groups) with the hyper-parameters of the last begin_step()."""
+    def step_group(self, key, grads: torch.Tensor, l2: float, grad_scale: float, parity: int = 0,
+                   max_grid: int = 0) -> None:
+        """Update one group (define_groups) with the hyper-parameters of the last begin_step().
+        ``max_grid`` > 0 caps the workgroups (a background 'trickle' beside the GEMMs)."""
         g = self.groups.get((key, parity))
         if g is not None:
-            self._launch(grads, *g, l2, grad_scale)
+            self._launch(grads, *g, l2, grad_scale, max_grid)
 
     def begin_step(self, lr: float) -> None:
         if self.adam:
@@ -184,7 +186,8 @@ class FusedOptimizer:
             bc1 = bc2s = 1.0
         self._hp = (lr, b1, b2, eps, bc1, bc2s)
 
-    def _launch(self, grads, segments, block_seg, nseg, nblocks, l2: float, grad_scale: float) -> None:
+    def _launch(self, grads, segments, block_seg, nseg, nblocks, l2: float, grad_scale: float,
+                max_grid: int = 0) -> None:
         lr, b1, b2, eps, bc1, bc2s = self._hp
         hp, ctr = self.graph_tables or (None, None)
         every = self.stats_every
@@ -192,7 +195,7 @@ class FusedOptimizer:
             every = 1
         torch.ops.pz.optimizer_step(self.store.flat, grads, self.exp_avg, self.exp_avg_sq, segments, block_seg, nseg,
                                     nblocks, self.adam, lr, b1, b2, eps, bc1, bc2s, grad_scale, l2,
-                                    self.stats[self.cur], hp, ctr, every)
+                                    self.stats[self.cur], hp, ctr, every, max_grid)
 
     def finalize(self, loss: torch.Tensor | None, world: int, l2: float, costs: torch.Tensor, epoch: int,
                  ratios: torch.Tensor, ratio_row: int, epoch_ctr: torch.Tensor | None = None, every: int = 1) -> None:

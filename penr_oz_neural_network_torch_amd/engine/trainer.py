@@ -264,6 +264,15 @@ class FusedTrainer:
         # deep16x8192 (SGD) within noise. PZ_OPT_MERGE=0 queues one update per layer.
         self._merge_side = os.environ.get("PZ_OPT_MERGE", "1") == "1"
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
+        # PZ_OPT_TRICKLE=G (> 0): the LARGEST side-updated weight is updated right behind its dW
+        # GEMM by a G-workgroup launch that streams beside the remaining backward GEMMs (a few CUs'
+        # worth of HBM traffic) instead of joining the merged updates after the last dX GEMM
+        # (bf16 / fp32 policies: the update writes the other shadow parity)
+        self._trickle = int(os.environ.get("PZ_OPT_TRICKLE", "0"))
+        self._trickle_key = None
+        if self._trickle > 0 and len(gemm_w) > 1 and not self.fp8:
+            sizes = {st.seg_w.offset: st.seg_w.numel for st in self.stages if st.kind == "gemm"}
+            self._trickle_key = max(gemm_w[1:], key=lambda k: sizes[k])
         self._side_pending: list = []
         self._opt_done = None
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
@@ -421,7 +430,7 @@ class FusedTrainer:
             if w8n is not None:  # [in, out] copy for the backward dX GEMM, same scale
                 ops.quantize_rows(w, w8n, self.wqs[k], None)
 
-    def _opt_async(self, items: list) -> None:
+    def _opt_async(self, items: list, max_grid: int = 0) -> None:
         """Queue the updates of optimizer groups ``[(key, handles, stages)]`` on the side stream
         behind their gradients: ONE event recorded on the compute stream for all of them (each
         record / cross-stream wait costs the compute stream a few microseconds of idle)."""
@@ -433,7 +442,7 @@ class FusedTrainer:
             for key, handles, stages in items:
                 for h in handles:
                     self.ctx.wait_one(h)
-                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
+                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity, max_grid)
                 if self.fp8:
                     for st in stages:
                         self._refresh_fp8_weights(st, 1 - self.parity)
@@ -972,10 +981,12 @@ class FusedTrainer:
         if self._ov is not None and not own:  # updated by the final launch
             self._late_stages.append(st)
             self._late_handles.extend(mine)
-        if self._ov is not None and own and early:
-            self._opt_async([(st.seg_w.offset, mine, [st])])
+        trickle = (self._ov is not None and own and st.seg_w.offset == self._trickle_key
+                   and st.seg_w.offset in self.shadow_sets[self.parity])
+        if self._ov is not None and own and (early or trickle):
+            self._opt_async([(st.seg_w.offset, mine, [st])], self._trickle if trickle else 0)
         out = self._backward_dx(st, before, g, batch, p, keys, rec)
-        if self._ov is not None and own and not early:
+        if self._ov is not None and own and not early and not trickle:
             self._side_pending.append((st.seg_w.offset, mine, [st]))
             if not self._merge_side or st.seg_w.offset == self._flush_key:
                 self._opt_async(self._side_pending)
