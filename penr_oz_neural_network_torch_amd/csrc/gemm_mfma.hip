@@ -153,7 +153,11 @@ PZ_DEV uint32_t lds_addr(const PZ_LDS char* p) {
 }
 
 // K-contiguous operand rows [row0, row0+R) x k [k0, k0+BK) -> slot [R][BK]; NW waves share it
-template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0>
+// FULL (buffer path, dispatcher-guaranteed full row tiles): no row clamp, so the piece's row
+// offset is wave-uniform and rides in soffset — one (BK 32) or two (BK 64: the swizzle flips
+// with the piece's parity) per-lane offsets stay live instead of one per piece (the 16 of a
+// BK 64 K-contiguous pair of operands spilled to scratch inside the loop)
+template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0, bool FULL = false>
 PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
                      PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
   constexpr int CPR = BK / 8;             // 16-B chunks per row
@@ -165,6 +169,12 @@ PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int r
     const int rbase = (wave * INSTR + i) * RPI;
     const int r = rbase + lane / CPR;
     const int chunk = (lane % CPR) ^ swz_kc<BK>(r);
+    if constexpr (BUF && FULL) {
+      const uint32_t voff = (static_cast<uint32_t>(lane / CPR) * static_cast<uint32_t>(ld) + chunk * 8) * 2u;
+      const uint32_t soff = (static_cast<uint32_t>(row0 + rbase) * static_cast<uint32_t>(ld) + static_cast<uint32_t>(k0)) * 2u;
+      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(soff), lds_addr(tile + rbase * BK * 2));
+      continue;
+    }
     int gr = row0 + r;
     gr = gr < rows_valid ? gr : rows_valid - 1;
     if constexpr (BUF) {
@@ -447,6 +457,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   constexpr bool BUF_A = VAR == 6 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
   constexpr bool BUF_B = VAR == 6 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
   constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
+  // VAR 30/31: full row tiles of the K-contiguous operands (use_bk64 checks M % BM, N % BN)
+  constexpr bool FULL_KC = VAR == 30 || VAR == 31;
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
   const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;
@@ -459,13 +471,13 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   auto stage_a_t = [&](int kt, auto team, int tw) {
     constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
-    if constexpr (A_KC) stage_kc<BM, TEAM, BK, BUF_A, POL>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
+    if constexpr (A_KC) stage_kc<BM, TEAM, BK, BUF_A, POL, FULL_KC>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
     else stage_mn<BM, TEAM, BK, BUF_A, POL>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
   };
   auto stage_b_t = [&](int kt, auto team, int tw) {
     constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B, POL>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
+    if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B, POL, FULL_KC>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
     else stage_mn<BN, TEAM, BK, BUF_B, POL>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
   };
   auto stage_a = [&](int kt) { stage_a_t(kt, std::integral_constant<int, NWD>{}, wave); };
@@ -746,12 +758,17 @@ bool prefer_128(const GemmArgs& p) {
 // operand: fwd [8192,4096]x[4096,4096] +6%, dW +4%, fwd K=1024 +4% (tools/gemm_lab, same box).
 // Both operands K-contiguous (dX) stay on the 32-deep ring: the BK64 form spills there (-11%).
 bool use_bk64(const GemmArgs& p, bool buf) {
-  static const bool off = [] {  // PZ_GEMM_BK64=0: 32-deep ring everywhere (A/B experiments)
+  // PZ_GEMM_BK64=0: 32-deep ring everywhere; =2: not for K-contiguous x K-contiguous (A/B)
+  static const int mode = [] {
     const char* e = getenv("PZ_GEMM_BK64");
-    return e != nullptr && atoi(e) == 0;
+    return e != nullptr ? atoi(e) : 1;
   }();
+  const bool off = mode == 0 || (mode == 2 && p.a_kc && p.b_kc);
   const int split = p.split_k > 1 ? p.split_k : 1;
-  return !off && buf && !(p.a_kc && p.b_kc) && p.K % 64 == 0 && (p.K / 64) % split == 0;
+  // VAR 30 stages K-contiguous operands without a row clamp: full 256-row tiles only (which
+  // also frees the K-contiguous x K-contiguous dX GEMMs from a scratch spill: +5..6%, lab)
+  const bool full = (!p.a_kc || p.M % 256 == 0) && (!p.b_kc || p.N % 256 == 0);
+  return !off && buf && full && p.K % 64 == 0 && (p.K / 64) % split == 0;
 }
 
 template <typename OutT, typename AuxT>
