@@ -742,11 +742,11 @@ bool buffer_ok(const GemmArgs& p) {
 // shape has at least two such tiles per CU. In isolation fwd [8192,1024] K=4096 runs 950 vs 855
 // TFLOP/s (tools/gemm_lab), but the mlp4 step is 0.9% SLOWER with it (same-box A/B x3), so off.
 bool prefer_128(const GemmArgs& p) {
-  static const bool on = [] {
+  static const int on = [] {  // 1: every eligible shape, 2: bf16-output (forward / dX) shapes only
     const char* e = getenv("PZ_GEMM_P128");
-    return e != nullptr && atoi(e) == 1;
+    return e != nullptr ? atoi(e) : 0;
   }();
-  if (!on) return false;
+  if (on == 0 || (on == 2 && p.out_dtype != DT_BF16)) return false;
   constexpr int kFill = 240;
   const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   const int t128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
