@@ -7,10 +7,11 @@ reference test-suite passes unchanged. GPU models pick a *precision policy*:
 ============  ==================  =====================  ===========================
 dtype         master params        GEMM operands          accumulation
 ============  ==================  =====================  ===========================
-float64       fp64                 fp64                   fp64
+float64       fp64                 fp64 (f64 MFMA)        fp64
 float32       fp32                 fp32 (f32 MFMA)        fp32
 bfloat16      fp32                 bf16 shadows           fp32 (bf16 MFMA)
-fp8           fp32                 e4m3 fwd / bf16 bwd    fp32 (fp8 MFMA)
+fp8           fp32                 e4m3 fwd, e5m2 x e4m3  fp32 (fp8 MFMA)
+                                   dX, bf16 dW
 ============  ==================  =====================  ===========================
 
 Master parameters are what ``params`` exposes and what the JSON checkpoint stores.
