@@ -371,13 +371,18 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   constexpr bool F8 = VAR == 8 || VAR == 9;
   constexpr int F8_FMT_A = VAR == 9 ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
   static_assert(!F8 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "fp8: K-contiguous in, bf16 out");
+  // VAR 41 (lab A/B): bf16 on v_mfma_f32_32x32x16_bf16 (32x32 accumulator tiles, the fp8 layout)
+  constexpr bool M32 = VAR == 41;
+  static_assert(!M32 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "M32: K-contiguous in, bf16 out");
+  constexpr bool ACC32 = F8 || M32;  // 32x32 accumulator tiles
   constexpr int TM8 = C::WTM / 32, TN8 = C::WTN / 32;
   struct Frags16 { i16x8_t a[KB][C::TM]; i16x8_t b[KB][C::TN]; };
   struct Frags8 { i32x8_t a[TM8]; i32x8_t b[TN8]; };
-  using Frags = std::conditional_t<F8, Frags8, Frags16>;
-  using AccT = std::conditional_t<F8, f32x16_t[TM8][TN8], f32x4_t[C::TM][C::TN]>;
+  struct Frags32 { i16x8_t a[2][TM8]; i16x8_t b[2][TN8]; };
+  using Frags = std::conditional_t<F8, Frags8, std::conditional_t<M32, Frags32, Frags16>>;
+  using AccT = std::conditional_t<ACC32, f32x16_t[TM8][TN8], f32x4_t[C::TM][C::TN]>;
   AccT acc;
-  if constexpr (F8) {
+  if constexpr (ACC32) {
 #pragma unroll
     for (int i = 0; i < TM8; ++i)
 #pragma unroll
@@ -391,7 +396,16 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 
   auto mfma_step = [&](const Frags& f) {
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (F8) {
+    if constexpr (M32) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < TM8; ++i)
+#pragma unroll
+          for (int j = 0; j < TN8; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, f.b[ks][j]),
+                                                                __builtin_bit_cast(bf16x8_t, f.a[ks][i]), acc[i][j], 0, 0, 0);
+    } else if constexpr (F8) {
 #pragma unroll
       for (int i = 0; i < TM8; ++i)
 #pragma unroll
@@ -414,7 +428,15 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   auto read_frags = [&](int slot, Frags& f) {
     const PZ_LDS char* ta = smem + slot * C::SLOT_BYTES;
     const PZ_LDS char* tb = ta + C::A_BYTES;
-    if constexpr (F8) {  // lane l: row l&31, K bytes [32*(l>>5), +32) = 16-B chunks 2h, 2h+1
+    if constexpr (M32) {  // lane l: row l&31, k [8*(l>>5) + 16*ks, +8) = 16-B chunk (l>>5) + 2ks
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+        for (int j = 0; j < TN8; ++j) f.b[ks][j] = frag_kc(tb, wn * C::WTN + j * 32 + (lane & 31), (lane >> 5) + 2 * ks);
+#pragma unroll
+        for (int i = 0; i < TM8; ++i) f.a[ks][i] = frag_kc(ta, wm * C::WTM + i * 32 + (lane & 31), (lane >> 5) + 2 * ks);
+      }
+    } else if constexpr (F8) {  // lane l: row l&31, K bytes [32*(l>>5), +32) = 16-B chunks 2h, 2h+1
       const int h2 = 2 * (lane >> 5);
 #pragma unroll
       for (int j = 0; j < TN8; ++j) {
@@ -454,8 +476,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
   // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
   // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
-  constexpr bool BUF_A = VAR == 6 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
-  constexpr bool BUF_B = VAR == 6 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_A = VAR == 6 || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_B = VAR == 6 || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
   constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
   // VAR 30/31: full row tiles of the K-contiguous operands (use_bk64 checks M % BM, N % BN)
   constexpr bool FULL_KC = VAR == 30 || VAR == 31;
@@ -614,11 +636,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // (guide "In-launch split-K reduction": plain slab stores, vmcnt(0), barrier, ONE agent-scope
   // release + relaxed ticket; the last arriver acquires, sums the other slabs, runs the epilogue)
   if (split > 1) {
-    constexpr int CH = F8 ? TM8 * TN8 * 4 : C::TM * C::TN;  // f32x4 chunks per lane
+    constexpr int CH = ACC32 ? TM8 * TN8 * 4 : C::TM * C::TN;  // f32x4 chunks per lane
     const int tid = threadIdx.x;
     auto get_chunk = [&](auto cc) -> f32x4_t {
       constexpr int c = decltype(cc)::value;
-      if constexpr (F8) {
+      if constexpr (ACC32) {
         constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
         return f32x4_t{acc[i][j][q], acc[i][j][q + 1], acc[i][j][q + 2], acc[i][j][q + 3]};
       } else {
@@ -627,7 +649,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     };
     auto add_chunk = [&](auto cc, f32x4_t v) {
       constexpr int c = decltype(cc)::value;
-      if constexpr (F8) {
+      if constexpr (ACC32) {
         constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
         acc[i][j][q] += v[0]; acc[i][j][q + 1] += v[1]; acc[i][j][q + 2] += v[2]; acc[i][j][q + 3] += v[3];
       } else {
@@ -666,9 +688,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   OutT* __restrict__ Cp = static_cast<OutT*>(p.C);
   const AuxT* __restrict__ aux = static_cast<const AuxT*>(p.aux);
   const int g4 = 4 * (lane >> 4);
-  if constexpr (F8) {
+  if constexpr (ACC32) {
     const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
-    if constexpr (VAR == 9) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    if constexpr (VAR == 9 || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
     else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
   } else if constexpr (std::is_same<OutT, uint16_t>::value) {
     epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);

@@ -70,7 +70,11 @@ struct Case {
 
 static std::vector<Variant> variants_for(const Case& c) {
   if (c.akc && !c.bkc && !c.f32out) return PZ_VARIANTS(true, false, uint16_t);
-  if (c.akc && c.bkc && !c.f32out) return PZ_VARIANTS(true, true, uint16_t);
+  if (c.akc && c.bkc && !c.f32out) {
+    std::vector<Variant> v = PZ_VARIANTS(true, true, uint16_t);
+    v.push_back({"m32x32", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 41>});
+    return v;
+  }
   if (!c.akc && !c.bkc && c.f32out) return PZ_VARIANTS(false, false, float);
   printf("no variants for layout\n");
   exit(1);
