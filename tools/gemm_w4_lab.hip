@@ -1,0 +1,391 @@
+// Feasibility probe: a 4-wave 256x256x64 bf16 GEMM main loop (one wave per SIMD, 128x128 wave
+// tiles, accumulators in AGPRs, operands staged global -> VGPR -> ds_write_b128 two K steps ahead)
+// against the library's 8-wave ping-pong (VAR 30). K-contiguous x K-contiguous (dX layout),
+// plain bf16 store epilogue. Same harness conventions as tools/gemm_lab.hip.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I penr_oz_neural_network_torch_amd/csrc \
+//         tools/gemm_w4_lab.hip -o tools/gemm_w4_lab && tools/gemm_w4_lab
+#define PZ_GEMM_LAB 1
+#include "../penr_oz_neural_network_torch_amd/csrc/gemm_mfma.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+using namespace pz;
+
+#define CK(x)                                                                                  \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) {                                                                    \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);            \
+      exit(1);                                                                                 \
+    }                                                                                          \
+  } while (0)
+
+namespace w4 {
+constexpr int BM = 256, BN = 256, BK = 64, NT = 256;
+constexpr int A_BYTES = BM * BK * 2, SLOT = 2 * A_BYTES;  // A + B, 64 KiB
+constexpr int PIECES = A_BYTES / 1024 / 4;                 // 1-KiB pieces per wave per operand (8)
+
+PZ_DEV int swz(int row) { return (row >> 1) & 7; }  // BK 64: 128-B rows, 8 chunks
+
+template <int SCHED>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) kern(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+  const int tiles_m = p.M / BM, tiles_n = p.N / BN;
+  int tm, tn, tile_id, slice;
+  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.A), 0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.B), 0, -1, 0x00020000);
+  // piece i of this wave: rows (wave*PIECES + i)*8 + lane/8, natural chunk lane%8 (global side),
+  // swizzled chunk on the LDS side
+  const int prow = lane >> 3, pch = lane & 7;
+  const uint32_t va = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.lda) + pch * 8) * 2u;
+  const uint32_t vb = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.ldb) + pch * 8) * 2u;
+  // LDS byte offset of piece i: row r = (wave*PIECES+i)*8 + prow -> r*128 + ((pch ^ swz(r)) << 4);
+  // swz(r) = ((wave*PIECES+i)*4 + prow/2) & 7 depends on i only through its parity
+  uint32_t lo[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int r = (wave * PIECES + par) * 8 + prow;
+    lo[par] = static_cast<uint32_t>(r * 128 + ((pch ^ swz(r)) << 4));
+  }
+  i32x4_t qa[PIECES], qb[PIECES];
+  auto gload = [&](int kt) {
+    const uint32_t k2 = static_cast<uint32_t>(kt * BK) * 2u;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const uint32_t rowb = static_cast<uint32_t>(m0 + (wave * PIECES + i) * 8);
+      qa[i] = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                              ra, va, rowb * static_cast<uint32_t>(p.lda) * 2u + k2, 0));
+    }
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i) {
+      const uint32_t rowb = static_cast<uint32_t>(n0 + (wave * PIECES + i) * 8);
+      qb[i] = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rb, vb, rowb * static_cast<uint32_t>(p.ldb) * 2u + k2, 0));
+    }
+  };
+  auto lwrite = [&](int kt) {
+    PZ_LDS char* base = smem + (kt & 1) * SLOT;
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i)
+      *reinterpret_cast<PZ_LDS i32x4_t*>(base + lo[i & 1] + (i & ~1) * 1024) = qa[i];
+#pragma unroll
+    for (int i = 0; i < PIECES; ++i)
+      *reinterpret_cast<PZ_LDS i32x4_t*>(base + A_BYTES + lo[i & 1] + (i & ~1) * 1024) = qb[i];
+  };
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  const int nk = p.K / BK;
+  if constexpr (SCHED >= 2) {
+    // software-pipelined: phase 0 of step t issues the MFMAs of fragments F0 (t, k 0-31) while
+    // reading F1 (t, k 32-63) and writing stage t+1 to the other slot; barrier; phase 1 issues
+    // the MFMAs of F1 while reading F0 of step t+1 and loading stage t+2 into the staging
+    // registers. Out-of-range stages are clamped (harmless extra traffic, no branches).
+    auto rd = [&](int slot, int ks, i16x8_t (&fa)[8], i16x8_t (&fb)[8]) {
+      const PZ_LDS char* ta = smem + slot * SLOT;
+      const PZ_LDS char* tb = ta + A_BYTES;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fb[j] = frag_kc<64>(tb, wn * 128 + j * 16 + (lane & 15), (lane >> 4) + 4 * ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = frag_kc<64>(ta, wm * 128 + i * 16 + (lane & 15), (lane >> 4) + 4 * ks);
+    };
+    auto mm = [&](const i16x8_t (&fa)[8], const i16x8_t (&fb)[8]) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fb[j]),
+                                                              __builtin_bit_cast(bf16x8_t, fa[i]), acc[i][j], 0, 0, 0);
+    };
+    i16x8_t a0[8], b0[8], a1[8], b1[8];
+    // hand-placed streams: 16 groups of {4 MFMAs, 1 fragment read, 1 staging op}, each group
+    // fenced by sched_barrier so the compiler keeps the interleave
+    auto frag = [&](int slot, int ks, int f) -> i16x8_t {
+      const PZ_LDS char* ta = smem + slot * SLOT;
+      if (f < 8) return frag_kc<64>(ta + A_BYTES, wn * 128 + f * 16 + (lane & 15), (lane >> 4) + 4 * ks);
+      return frag_kc<64>(ta, wm * 128 + (f - 8) * 16 + (lane & 15), (lane >> 4) + 4 * ks);
+    };
+    auto mfma4 = [&](const i16x8_t (&fa)[8], const i16x8_t (&fb)[8], int g) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int idx = g * 4 + q, i = idx >> 3, j = idx & 7;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fb[j]),
+                                                            __builtin_bit_cast(bf16x8_t, fa[i]), acc[i][j], 0, 0, 0);
+      }
+    };
+    auto wpiece = [&](int kt, int f) {
+      PZ_LDS char* base = smem + (kt & 1) * SLOT + (f < 8 ? 0 : A_BYTES);
+      const int i = f & 7;
+      *reinterpret_cast<PZ_LDS i32x4_t*>(base + lo[i & 1] + (i & ~1) * 1024) = f < 8 ? qa[i] : qb[i];
+    };
+    auto gpiece = [&](int kt, int f) {
+      const uint32_t k2 = static_cast<uint32_t>(kt * BK) * 2u;
+      const int i = f & 7;
+      if (f < 8) {
+        const uint32_t rowb = static_cast<uint32_t>(m0 + (wave * PIECES + i) * 8);
+        qa[i] = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                ra, va, rowb * static_cast<uint32_t>(p.lda) * 2u + k2, 0));
+      } else {
+        const uint32_t rowb = static_cast<uint32_t>(n0 + (wave * PIECES + i) * 8);
+        qb[i] = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                rb, vb, rowb * static_cast<uint32_t>(p.ldb) * 2u + k2, 0));
+      }
+    };
+    gload(0);
+    lwrite(0);
+    gload(min(1, nk - 1));
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+#pragma unroll
+    for (int f = 0; f < 16; ++f) (f < 8 ? b0[f] : a0[f - 8]) = frag(0, 0, f);
+    auto mfma2 = [&](const i16x8_t (&fa)[8], const i16x8_t (&fb)[8], int h) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int idx = h * 2 + q, i = idx >> 3, j = idx & 7;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fb[j]),
+                                                            __builtin_bit_cast(bf16x8_t, fa[i]), acc[i][j], 0, 0, 0);
+      }
+    };
+    if constexpr (SCHED == 5) {  // stage t+2 loaded right behind the write of stage t+1 (a full step of latency)
+      for (int t = 0; t < nk; ++t) {
+        const int s = t & 1;
+        const int kn = min(t + 2, nk - 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          mfma4(a0, b0, g);
+          (g < 8 ? b1[g] : a1[g - 8]) = frag(s, 1, g);
+          wpiece(t + 1, g);
+          gpiece(kn, g);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+          mfma4(a1, b1, g);
+          (g < 8 ? b0[g] : a0[g - 8]) = frag(s ^ 1, 0, g);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else if constexpr (SCHED == 4) {  // finer: {2 MFMAs, 1 op} x 32 per phase, reads and staging alternating
+      for (int t = 0; t < nk; ++t) {
+        const int s = t & 1;
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int h = 0; h < 32; ++h) {
+          mfma2(a0, b0, h);
+          if (h & 1) wpiece(t + 1, h >> 1);
+          else (h < 16 ? b1[h >> 1] : a1[(h >> 1) - 8]) = frag(s, 1, h >> 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        const int kn = min(t + 2, nk - 1);
+#pragma unroll
+        for (int h = 0; h < 32; ++h) {
+          mfma2(a1, b1, h);
+          if (h & 1) gpiece(kn, h >> 1);
+          else (h < 16 ? b0[h >> 1] : a0[(h >> 1) - 8]) = frag(s ^ 1, 0, h >> 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    } else
+    for (int t = 0; t < nk; ++t) {
+      const int s = t & 1;
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        mfma4(a0, b0, g);
+        (g < 8 ? b1[g] : a1[g - 8]) = frag(s, 1, g);
+        if constexpr (SCHED == 3) {  // staging front-loaded: two pieces per group, first 8 groups
+          if (g < 8) { wpiece(t + 1, 2 * g); wpiece(t + 1, 2 * g + 1); }
+        } else {
+          wpiece(t + 1, g);  // slot s^1 (at the last step: a harmless copy of the clamped stage)
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      const int kn = min(t + 2, nk - 1);
+#pragma unroll
+      for (int g = 0; g < 16; ++g) {
+        mfma4(a1, b1, g);
+        (g < 8 ? b0[g] : a0[g - 8]) = frag(s ^ 1, 0, g);
+        if constexpr (SCHED == 3) {
+          if (g < 8) { gpiece(kn, 2 * g); gpiece(kn, 2 * g + 1); }
+        } else {
+          gpiece(kn, g);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  } else {
+  gload(0);
+  lwrite(0);
+  if (nk > 1) gload(1);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  for (int t = 0; t < nk; ++t) {
+    const PZ_LDS char* ta = smem + (t & 1) * SLOT;
+    const PZ_LDS char* tb = ta + A_BYTES;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      i16x8_t fa[8], fb[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) fb[j] = frag_kc<64>(tb, wn * 128 + j * 16 + (lane & 15), (lane >> 4) + 4 * ks);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) fa[i] = frag_kc<64>(ta, wm * 128 + i * 16 + (lane & 15), (lane >> 4) + 4 * ks);
+      if (ks == 1 && t + 1 < nk) lwrite(t + 1);  // slot (t+1)&1 was last read in step t-1
+      if (ks == 1 && t + 2 < nk) gload(t + 2);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, fb[j]),
+                                                              __builtin_bit_cast(bf16x8_t, fa[i]), acc[i][j], 0, 0, 0);
+      if constexpr (SCHED == 1) {
+        // interleave: 16 ds_read_b128 (next half's fragments are read up front, so only the
+        // staging writes/loads remain to spread) among the 64 MFMAs
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  }
+  }
+  uint16_t* C = static_cast<uint16_t*>(p.C);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + wm * 128 + i * 16 + (lane & 15), n = n0 + wn * 128 + j * 16 + 4 * (lane >> 4);
+      float v[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha, acc[i][j][3] * p.alpha};
+      store4<uint16_t>(C + static_cast<int64_t>(m) * p.ldc + n, v);
+    }
+}
+
+template <int SCHED>
+hipError_t launch(const GemmArgs& p, hipStream_t s) {
+  static bool set = false;
+  if (!set) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern<SCHED>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                           2 * SLOT));
+    set = true;
+  }
+  hipLaunchKernelGGL(kern<SCHED>, dim3((p.M / BM) * (p.N / BN)), dim3(NT), 2 * SLOT, s, p);
+  return hipGetLastError();
+}
+}  // namespace w4
+
+__global__ void fill_bf16(uint16_t* p, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t h = mix32(mix32(static_cast<uint32_t>(i) ^ seed) + static_cast<uint32_t>(i >> 32));
+    p[i] = f2bf(static_cast<float>(h >> 8) * (2.f / 16777216.f) - 1.f);
+  }
+}
+
+__global__ void ref_rows(const uint16_t* A, const uint16_t* B, float* R, int N, int K, int64_t lda, int64_t ldb,
+                         int stride) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t m = static_cast<int64_t>(blockIdx.y) * stride;
+  if (n >= N) return;
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k) acc += bf2f(A[m * lda + k]) * bf2f(B[static_cast<int64_t>(n) * ldb + k]);
+  R[static_cast<int64_t>(blockIdx.y) * N + n] = acc;
+}
+
+typedef hipError_t (*LaunchFn)(const GemmArgs&, hipStream_t);
+
+int main(int argc, char** argv) {
+  struct Case { const char* name; int M, N, K; };
+  std::vector<Case> cases = {{"dX_L2", 8192, 4096, 4096}, {"dX_L3", 8192, 4096, 1024}};
+  struct V { const char* name; LaunchFn fn; };
+  std::vector<V> vs = {{"lib_var30", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
+                       {"w4_pipe", w4::launch<2>}, {"w4_early", w4::launch<5>}};
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  for (const Case& c : cases) {
+    const int64_t na = int64_t(c.M) * c.K, nb = int64_t(c.N) * c.K, nc = int64_t(c.M) * c.N;
+    uint16_t *A, *B, *C;
+    float* R;
+    CK(hipMalloc(&A, na * 2));
+    CK(hipMalloc(&B, nb * 2));
+    CK(hipMalloc(&C, nc * 2));
+    const int stride = 61, nref = (c.M + stride - 1) / stride;
+    CK(hipMalloc(&R, int64_t(nref) * c.N * 4));
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, A, na, 12345u);
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, B, nb, 777u);
+    hipLaunchKernelGGL(ref_rows, dim3((c.N + 255) / 256, nref), dim3(256), 0, st, A, B, R, c.N, c.K, int64_t(c.K),
+                       int64_t(c.K), stride);
+    std::vector<float> ref(size_t(nref) * c.N);
+    CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
+    CK(hipStreamSynchronize(st));
+    GemmArgs p{};
+    p.A = A; p.B = B; p.C = C;
+    p.M = c.M; p.N = c.N; p.K = c.K;
+    p.lda = c.K; p.ldb = c.K; p.ldc = c.N;
+    p.a_kc = 1; p.b_kc = 1;
+    p.in_dtype = DT_BF16; p.out_dtype = DT_BF16;
+    p.alpha = 1.f; p.epi_mode = EPI_STORE; p.idx_ld = c.N; p.split_k = 1;
+    const double flop = 2.0 * c.M * c.N * c.K;
+    std::vector<std::vector<double>> tf(vs.size());
+    for (size_t v = 0; v < vs.size(); ++v) {
+      CK(hipMemsetAsync(C, 0, nc * 2, st));
+      CK(vs[v].fn(p, st));
+      CK(hipStreamSynchronize(st));
+      std::vector<uint16_t> out(nc);
+      CK(hipMemcpy(out.data(), C, nc * 2, hipMemcpyDeviceToHost));
+      double worst = 0.0;
+      for (int r = 0; r < nref; ++r)
+        for (int n = 0; n < c.N; ++n) {
+          uint32_t u = uint32_t(out[size_t(r) * stride * c.N + n]) << 16;
+          float got;
+          memcpy(&got, &u, 4);
+          const double want = ref[size_t(r) * c.N + n];
+          worst = std::max(worst, fabs(got - want) / (fabs(want) * 0.01 + 0.05));
+        }
+      printf("%s %-10s check %s (worst err/tol %.3f)\n", c.name, vs[v].name, worst <= 1.0 ? "OK" : "FAIL", worst);
+    }
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int r = 0; r < 5; ++r)
+      for (size_t v = 0; v < vs.size(); ++v) {
+        for (int w = 0; w < 3; ++w) CK(vs[v].fn(p, st));
+        CK(hipEventRecord(e0, st));
+        for (int i = 0; i < 20; ++i) CK(vs[v].fn(p, st));
+        CK(hipEventRecord(e1, st));
+        CK(hipEventSynchronize(e1));
+        float ms;
+        CK(hipEventElapsedTime(&ms, e0, e1));
+        tf[v].push_back(flop * 20 / (ms * 1e-3) / 1e12);
+      }
+    for (size_t v = 0; v < vs.size(); ++v) {
+      auto t = tf[v];
+      std::sort(t.begin(), t.end());
+      printf("%s %-10s TF/s best %.1f median %.1f\n", c.name, vs[v].name, t.back(), t[t.size() / 2]);
+    }
+    fflush(stdout);
+    CK(hipFree(A)); CK(hipFree(B)); CK(hipFree(C)); CK(hipFree(R));
+  }
+  return 0;
+}
