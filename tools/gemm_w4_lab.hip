@@ -293,7 +293,128 @@ hipError_t launch(const GemmArgs& p, hipStream_t s) {
   hipLaunchKernelGGL(kern<SCHED>, dim3((p.M / BM) * (p.N / BN)), dim3(NT), 2 * SLOT, s, p);
   return hipGetLastError();
 }
+// 32x32x16 form of the hand-placed pipe: half the MFMA instructions per FLOP (32-cycle MFMAs
+// leave 24 free issue cycles each), groups of {2 MFMAs, 1 fragment read, 1 staging op}
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) kern32(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+  const int tiles_m = p.M / BM, tiles_n = p.N / BN;
+  int tm, tn, tile_id, slice;
+  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.A), 0, -1, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p.B), 0, -1, 0x00020000);
+  const int prow = lane >> 3, pch = lane & 7;
+  const uint32_t va = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.lda) + pch * 8) * 2u;
+  const uint32_t vb = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.ldb) + pch * 8) * 2u;
+  uint32_t lo[2];
+#pragma unroll
+  for (int par = 0; par < 2; ++par) {
+    const int r = (wave * PIECES + par) * 8 + prow;
+    lo[par] = static_cast<uint32_t>(r * 128 + ((pch ^ swz(r)) << 4));
+  }
+  i32x4_t qa[PIECES], qb[PIECES];
+  auto wpiece = [&](int kt, int f) {
+    PZ_LDS char* base = smem + (kt & 1) * SLOT + (f < 8 ? 0 : A_BYTES);
+    const int i = f & 7;
+    *reinterpret_cast<PZ_LDS i32x4_t*>(base + lo[i & 1] + (i & ~1) * 1024) = f < 8 ? qa[i] : qb[i];
+  };
+  auto gpiece = [&](int kt, int f) {
+    const uint32_t k2 = static_cast<uint32_t>(kt * BK) * 2u;
+    const int i = f & 7;
+    if (f < 8) {
+      const uint32_t rowb = static_cast<uint32_t>(m0 + (wave * PIECES + i) * 8);
+      qa[i] = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                              ra, va, rowb * static_cast<uint32_t>(p.lda) * 2u + k2, 0));
+    } else {
+      const uint32_t rowb = static_cast<uint32_t>(n0 + (wave * PIECES + i) * 8);
+      qb[i] = __builtin_bit_cast(i32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                              rb, vb, rowb * static_cast<uint32_t>(p.ldb) * 2u + k2, 0));
+    }
+  };
+  // fragment f of half ks: sub-step u = f >> 3 (k16 within the 32-deep half), tile q = f & 7
+  // (q < 4: B tile q, else A tile q-4); lane: row l&31, k chunk (l>>5) + 2u + 4ks
+  auto frag = [&](int slot, int ks, int f) -> i16x8_t {
+    const PZ_LDS char* ta = smem + slot * SLOT;
+    const int u = f >> 3, q = f & 7, ch = (lane >> 5) + 2 * u + 4 * ks;
+    if (q < 4) return frag_kc<64>(ta + A_BYTES, wn * 128 + q * 32 + (lane & 31), ch);
+    return frag_kc<64>(ta, wm * 128 + (q - 4) * 32 + (lane & 31), ch);
+  };
+  f32x16_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16_t{};
+  // F[f]: 16 fragments per half
+  auto mfma2 = [&](const i16x8_t (&F)[16], int h) {  // h in [0,16): sub-step h>>3, pair (h&7)
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int u = h >> 3, idx = (h & 7) * 2 + q, i = idx >> 2, j = idx & 3;
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, F[8 * u + j]),
+                                                          __builtin_bit_cast(bf16x8_t, F[8 * u + 4 + i]), acc[i][j], 0, 0, 0);
+    }
+  };
+  const int nk = p.K / BK;
+  i16x8_t F0[16], F1[16];
+#pragma unroll
+  for (int f = 0; f < 16; ++f) gpiece(0, f);
+#pragma unroll
+  for (int f = 0; f < 16; ++f) wpiece(0, f);
+#pragma unroll
+  for (int f = 0; f < 16; ++f) gpiece(min(1, nk - 1), f);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int f = 0; f < 16; ++f) F0[f] = frag(0, 0, f);
+  for (int t = 0; t < nk; ++t) {
+    const int s = t & 1;
+    const int kn = min(t + 2, nk - 1);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      mfma2(F0, h);
+      F1[h] = frag(s, 1, h);
+      wpiece(t + 1, h);
+      gpiece(kn, h);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int h = 0; h < 16; ++h) {
+      mfma2(F1, h);
+      F0[h] = frag(s ^ 1, 0, h);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  uint16_t* C = static_cast<uint16_t*>(p.C);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {  // register quad g: columns 8g + 4(l>>5) + 0..3 of row l&31
+        const int m = m0 + wm * 128 + i * 32 + (lane & 31), n = n0 + wn * 128 + j * 32 + 8 * g + 4 * (lane >> 5);
+        float v[4] = {acc[i][j][4 * g] * p.alpha, acc[i][j][4 * g + 1] * p.alpha, acc[i][j][4 * g + 2] * p.alpha,
+                      acc[i][j][4 * g + 3] * p.alpha};
+        store4<uint16_t>(C + static_cast<int64_t>(m) * p.ldc + n, v);
+      }
+}
+
+hipError_t launch32(const GemmArgs& p, hipStream_t s) {
+  static bool set = false;
+  if (!set) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kern32), hipFuncAttributeMaxDynamicSharedMemorySize, 2 * SLOT));
+    set = true;
+  }
+  hipLaunchKernelGGL(kern32, dim3((p.M / BM) * (p.N / BN)), dim3(NT), 2 * SLOT, s, p);
+  return hipGetLastError();
+}
 }  // namespace w4
+
 
 __global__ void fill_bf16(uint16_t* p, int64_t n, uint32_t seed) {
   for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
@@ -320,7 +441,7 @@ int main(int argc, char** argv) {
   std::vector<Case> cases = {{"dX_L2", 8192, 4096, 4096}, {"dX_L3", 8192, 4096, 1024}};
   struct V { const char* name; LaunchFn fn; };
   std::vector<V> vs = {{"lib_var30", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
-                       {"w4_pipe", w4::launch<2>}, {"w4_early", w4::launch<5>}};
+                       {"w4_early", w4::launch<5>}, {"w4_32x32", w4::launch32}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (const Case& c : cases) {
