@@ -75,7 +75,14 @@ static std::vector<Variant> variants_for(const Case& c) {
     v.push_back({"m32x32", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 41>});
     return v;
   }
-  if (!c.akc && !c.bkc && c.f32out) return PZ_VARIANTS(false, false, float);
+  if (!c.akc && !c.bkc && c.f32out) {
+    std::vector<Variant> v = PZ_VARIANTS(false, false, float);
+    if (c.N <= 1024 || c.M <= 1024) {  // skinny dW: the library's split-K 4 plan (VAR 30)
+      v.push_back({"bk64_s4", launch_cfg<256, 256, 2, 4, false, false, float, uint16_t, 30>, 4});
+      v.push_back({"bk64_s2", launch_cfg<256, 256, 2, 4, false, false, float, uint16_t, 30>, 2});
+    }
+    return v;
+  }
   printf("no variants for layout\n");
   exit(1);
 }
@@ -87,6 +94,8 @@ int main(int argc, char** argv) {
       {"dW_L2", 4096, 4096, B, false, false, true},  {"fwd_L1", B, 4096, 1024, true, false, false},
       {"dX_L3", B, 4096, 1024, true, true, false},   {"fwd_L3", B, 1024, 4096, true, false, false},
       {"dW_L3", 4096, 1024, B, false, false, true},  {"dW_L1", 1024, 4096, B, false, false, true},
+      // same per-workgroup work as dW_L3 split 4 (256 tiles x K 2048), no reduction
+      {"dW_sq2k", 4096, 4096, 2048, false, false, true},
   };
   const int rounds = getenv("LAB_ROUNDS") ? atoi(getenv("LAB_ROUNDS")) : 5, iters = 20;
   hipStream_t st;
