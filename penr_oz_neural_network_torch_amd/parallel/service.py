@@ -21,6 +21,14 @@ process group, so idle workers block on ``recv`` without a collective timeout. O
 runs at a time (the group's lock); the process-wide default context stays world size 1, so CPU
 models and inference in the server never issue collectives.
 
+Failure handling: a watchdog thread polls the worker processes. A worker that dies
+marks the group lost; if a training is in flight, the default process group is aborted so rank 0's
+pending collectives fail instead of waiting out the collective timeout. A training whose workers
+do not report back (lost worker, rank 0 failed while the others wait in a collective) tears the
+group down (workers killed); the next ``train`` brings a fresh group up (new workers, new
+rendezvous) before it runs. A failure every rank reports cleanly (e.g. a bad request) keeps the
+group. ``status()`` exposes ``lost`` and ``restarts``.
+
 Configuration: ``PZ_SERVICE_GPUS`` = unset / ``1`` (reference behaviour: no group), ``auto`` (every
 visible GPU) or N. ``PZ_DIST_BACKEND`` overrides the backend (``gloo`` for CPU rehearsals).
 """
@@ -32,6 +40,7 @@ import secrets
 import subprocess
 import sys
 import threading
+import time
 from multiprocessing.connection import Listener
 
 log = logging.getLogger("pz.service")
@@ -63,9 +72,14 @@ class TrainGroup:
         self._error: str | None = None
         self.ctx = None
         self.trainings = 0   # group trainings completed on every rank
+        self.restarts = 0    # fresh groups brought up after a failure
         self.conns: list = []
         self.procs: list[subprocess.Popen] = []
+        self._lost: str | None = None      # why the current group is unusable (worker exit, no reply)
+        self._in_flight = False
+        self._stopping = False
         self._start()
+        threading.Thread(target=self._watch, name="pz-train-watchdog", daemon=True).start()
 
     # ---------------------------------------------------------------------------------------
     def _start(self) -> None:
@@ -123,11 +137,72 @@ class TrainGroup:
     # ---------------------------------------------------------------------------------------
     @property
     def healthy(self) -> bool:
-        return self._ready.is_set() and self._error is None and all(p.poll() is None for p in self.procs)
+        return (self._ready.is_set() and self._error is None and self._lost is None
+                and all(p.poll() is None for p in self.procs))
 
     def status(self) -> dict:
         return {"world_size": self.world, "backend": self.backend, "ready": self._ready.is_set(),
-                "healthy": self.healthy, "error": self._error, "trainings": self.trainings}
+                "healthy": self.healthy, "error": self._error, "trainings": self.trainings,
+                "lost": self._lost, "restarts": self.restarts}
+
+    def _watch(self) -> None:
+        """Worker-exit watchdog: mark the group lost; abort in-flight collectives on rank 0."""
+        while not self._stopping:
+            gen = self.procs  # the list object is replaced on restart: ignore exits of a torn-down group
+            for r, p in enumerate(list(gen), 1):
+                if p.poll() is not None and self._lost is None and not self._stopping and gen is self.procs:
+                    self._lost = f"worker rank {r} exited with code {p.returncode}"
+                    log.error("data-parallel group lost: %s", self._lost)
+                    if self._in_flight:
+                        self._abort_collectives()
+            time.sleep(0.2)
+
+    def _abort_collectives(self) -> None:
+        try:
+            import torch.distributed as dist
+            from torch.distributed.distributed_c10d import _abort_process_group
+            if dist.is_initialized():
+                _abort_process_group()
+        except Exception:  # gloo: the dead peer's sockets already fail the pending collectives
+            log.debug("process group abort unavailable", exc_info=True)
+
+    def _teardown(self) -> None:
+        """Stop (or kill) the workers and drop the process group (failure path and shutdown)."""
+        lost = self._lost is not None
+        for c in self.conns:
+            try:
+                if not lost:
+                    c.send({"op": "stop"})
+                c.close()
+            except OSError:
+                pass
+        for p in self.procs:
+            try:
+                if lost:
+                    p.kill()
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:  # pragma: no cover
+                p.kill()
+        try:
+            import torch.distributed as dist
+            if self._ready.is_set() and self._error is None and dist.is_initialized():
+                dist.destroy_process_group()
+        except Exception:  # pragma: no cover - an aborted group may refuse a clean destroy
+            log.debug("destroy_process_group after failure", exc_info=True)
+        self._listener.close()
+
+    def restart(self) -> None:
+        """Replace a lost group: kill what is left of it, spawn fresh workers, rendezvous again."""
+        log.warning("restarting the data-parallel train group (%s)", self._lost or self._error)
+        self._lost = self._lost or "restart"
+        self._teardown()
+        self._ready.clear()
+        self._error = None
+        self.conns = []
+        self.procs = []
+        self._lost = None
+        self.restarts += 1
+        self._start()
 
     def wait_ready(self, timeout: float | None = None) -> bool:
         return self._ready.wait(timeout) and self._error is None
@@ -135,10 +210,12 @@ class TrainGroup:
     def train(self, model, data, hp: dict) -> None:
         """Run ``model.train(data, **hp)`` on every rank (called from the service's train thread)."""
         with self._lock:
+            if self._lost is not None or (self._ready.is_set() and not self.healthy):
+                self.restart()
             if not self.wait_ready(self.timeout_s):
                 raise RuntimeError(f"data-parallel train group unavailable: {self._error or 'rendezvous timeout'}")
             if not self.healthy:
-                raise RuntimeError("a data-parallel worker process has exited")
+                raise RuntimeError(f"data-parallel train group lost: {self._lost or 'a worker process has exited'}")
             cmd = {"op": "load", "model_id": model.model_id, "data": data, "hp": hp}
             for c in self.conns:
                 c.send(cmd)
@@ -150,13 +227,27 @@ class TrainGroup:
                 raise RuntimeError("data-parallel workers could not load the model: " + "; ".join(failed))
             model._context = self.ctx
             err = None
+            self._in_flight = True
             try:
                 model.train(data, **hp)
             except Exception as e:
                 err = e
             finally:
                 model._context = None
-            results = [c.recv() for c in self.conns]
+                self._in_flight = False
+            # workers report "done" / "failed: ..."; no reply (dead worker, or workers stuck in a
+            # collective rank 0 left) means the group is unusable: tear it down now
+            results = []
+            for c in self.conns:
+                wait = self.timeout_s if err is None else 15.0
+                try:
+                    results.append(c.recv() if c.poll(wait) else None)
+                except (EOFError, OSError):
+                    results.append(None)
+            if any(m is None for m in results) or self._lost is not None:
+                self._lost = self._lost or "a worker did not report the end of the training"
+                log.error("data-parallel training lost its group: %s", self._lost)
+                self._teardown()
             bad = [f"rank {r + 1}: {m}" for r, m in enumerate(results) if m != "done"]
             if err is not None:
                 raise err
@@ -165,23 +256,8 @@ class TrainGroup:
             self.trainings += 1
 
     def shutdown(self) -> None:
-        for c in self.conns:
-            try:
-                c.send({"op": "stop"})
-            except OSError:
-                pass
-        for p in self.procs:
-            try:
-                p.wait(timeout=30)
-            except subprocess.TimeoutExpired:  # pragma: no cover
-                p.kill()
-        try:
-            import torch.distributed as dist
-            if self._ready.is_set() and self._error is None and dist.is_initialized():
-                dist.destroy_process_group()
-        except Exception:  # pragma: no cover
-            pass
-        self._listener.close()
+        self._stopping = True
+        self._teardown()
 
 
 def start_from_env() -> "TrainGroup | None":

@@ -59,3 +59,56 @@ def test_train_route_runs_on_two_ranks(models_tmpdir, monkeypatch):
         assert r.status_code == 202
         assert _wait(client, "dp", ("Trained",))["status"] == "Trained"
         assert client.get("/health").json()["train_group"]["trainings"] == 2
+
+
+def _health_group(client):
+    return client.get("/health").json()["train_group"]
+
+
+def test_group_recovers_from_lost_workers(models_tmpdir, monkeypatch):
+    """a worker that dies (idle, or in the middle of a training) is detected by the
+    watchdog; an in-flight training fails promptly instead of waiting out the collective timeout,
+    and the next ``PUT /train/`` brings a fresh group up (new worker, new rendezvous) and trains."""
+    from penr_oz_neural_network_torch_amd.parallel import service
+    monkeypatch.setenv("PZ_SERVICE_GPUS", "2")
+    monkeypatch.setenv("PZ_DIST_BACKEND", "gloo")
+    with TestClient(main.app) as client:
+        _group_ready(client)
+        r = client.post("/model/", json={"model_id": "ft", "layer_sizes": [4, 8, 2], "optimizer": "adam",
+                                         "activation_algos": ["tanh", "softmax"]})
+        assert r.status_code == 200
+        data = [{"activation_vector": [i % 3, 1, 0, -(i % 2)], "target_vector": [i % 2]} for i in range(64)]
+        short = {"model_id": "ft", "training_data": data, "epochs": 3, "batch_size": 8}
+        group = service.get_group()
+
+        # 1) idle worker killed: the watchdog marks the group lost, the next training restarts it
+        group.procs[0].kill()
+        t0 = time.time()
+        while _health_group(client)["lost"] is None:
+            assert time.time() - t0 < 10, "watchdog did not notice the dead worker"
+            time.sleep(0.05)
+        assert not _health_group(client)["healthy"]
+        assert client.put("/train/", json=short).status_code == 202
+        assert _wait(client, "ft", ("Trained", "Failed"))["status"] == "Trained"
+        g = _health_group(client)
+        assert g["healthy"] and g["restarts"] == 1 and g["trainings"] == 1
+
+        # 2) worker killed in the middle of a training: prompt failure, then a fresh group
+        long = dict(short, epochs=200000)
+        assert client.put("/train/", json=long).status_code == 202
+        _wait(client, "ft", ("Training",))
+        time.sleep(0.5)
+        victim = group.procs[0]
+        victim.kill()
+        t0 = time.time()
+        assert _wait(client, "ft", ("Failed", "Trained"), timeout=60)["status"] == "Failed"
+        assert time.time() - t0 < 60
+        assert client.put("/train/", json=short).status_code == 202
+        t0 = time.time()  # (the status reads "Failed" until the new training starts)
+        while _health_group(client)["trainings"] < 2:
+            assert time.time() - t0 < 120, _health_group(client)
+            time.sleep(0.05)
+        assert _wait(client, "ft", ("Trained",))["status"] == "Trained"
+        g = _health_group(client)
+        assert g["healthy"] and g["restarts"] == 2 and g["trainings"] == 2
+        assert group.procs[0] is not victim and group.procs[0].poll() is None
