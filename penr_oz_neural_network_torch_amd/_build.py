@@ -101,12 +101,22 @@ def _compile(src: str, key: str, manifest: dict, force: bool) -> str:
     return obj
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
-    os.makedirs(BUILD, exist_ok=True)
+def _sources_and_keys():
     sources = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     hdr = _headers_digest()
     keys = {s: _object_key(s, hdr) for s in sources}
-    lib_key = hashlib.sha256("".join(keys[s] for s in sources).encode()).hexdigest()
+    return sources, keys, hashlib.sha256("".join(keys[s] for s in sources).encode()).hexdigest()
+
+
+def is_fresh() -> bool:
+    """True when the in-tree library was linked from exactly the current sources, headers and
+    compile commands (content hashes, not mtimes)."""
+    return os.path.exists(OUT) and _load_manifest().get("library") == _sources_and_keys()[2]
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = True) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    sources, keys, lib_key = _sources_and_keys()
     manifest = _load_manifest()
     if not force and os.path.exists(OUT) and manifest.get("library") == lib_key:
         if verbose:

@@ -13,7 +13,6 @@ Policy:
 """
 from __future__ import annotations
 
-import glob
 import os
 import threading
 
@@ -68,9 +67,7 @@ def format_json_array(t: torch.Tensor, level: int) -> str:
 
 
 def built_sources_stale() -> bool:
-    """True when any csrc file is newer than the built library (dev helper)."""
-    lib = library_path()
-    if not os.path.exists(lib):
-        return True
-    newest = max(os.path.getmtime(p) for p in glob.glob(os.path.join(_PKG_DIR, "csrc", "*")))
-    return newest > os.path.getmtime(lib)
+    """True when the built library does not match the current csrc/ content (the build's
+    content-hash manifest, ``_build.is_fresh``; dev helper)."""
+    from .. import _build
+    return not _build.is_fresh()

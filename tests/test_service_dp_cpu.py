@@ -32,6 +32,16 @@ def _group_ready(client, timeout=120.0):
     raise AssertionError("train group did not come up")
 
 
+def _wait_trainings(client, n, timeout=60.0):
+    """The model reads "Trained" as soon as rank 0's train() returns; the group counts the training
+    once every worker has reported back — poll for that."""
+    t0 = time.time()
+    while client.get("/health").json()["train_group"]["trainings"] < n:
+        assert time.time() - t0 < timeout, client.get("/health").json()["train_group"]
+        time.sleep(0.02)
+    return client.get("/health").json()["train_group"]
+
+
 def test_train_route_runs_on_two_ranks(models_tmpdir, monkeypatch):
     monkeypatch.setenv("PZ_SERVICE_GPUS", "2")
     monkeypatch.setenv("PZ_DIST_BACKEND", "gloo")
@@ -48,7 +58,7 @@ def test_train_route_runs_on_two_ranks(models_tmpdir, monkeypatch):
         prog = _wait(client, "dp", ("Trained", "Failed"))
         assert prog["status"] == "Trained"
         assert len(prog["progress"]) == 8 and all(p["world_size"] == 2 for p in prog["progress"])
-        assert client.get("/health").json()["train_group"]["trainings"] == 1
+        assert _wait_trainings(client, 1)["trainings"] == 1
         # a sample smaller than the group fails on every rank (no hang) and the group survives it
         r = client.put("/train/", json={"model_id": "dp", "training_data": data, "epochs": 2, "batch_size": 1})
         assert r.status_code == 202
@@ -58,7 +68,7 @@ def test_train_route_runs_on_two_ranks(models_tmpdir, monkeypatch):
         r = client.put("/train/", json={"model_id": "dp", "training_data": data, "epochs": 2, "batch_size": 8})
         assert r.status_code == 202
         assert _wait(client, "dp", ("Trained",))["status"] == "Trained"
-        assert client.get("/health").json()["train_group"]["trainings"] == 2
+        assert _wait_trainings(client, 2)["trainings"] == 2
 
 
 def _health_group(client):
@@ -90,7 +100,7 @@ def test_group_recovers_from_lost_workers(models_tmpdir, monkeypatch):
         assert not _health_group(client)["healthy"]
         assert client.put("/train/", json=short).status_code == 202
         assert _wait(client, "ft", ("Trained", "Failed"))["status"] == "Trained"
-        g = _health_group(client)
+        g = _wait_trainings(client, 1)
         assert g["healthy"] and g["restarts"] == 1 and g["trainings"] == 1
 
         # 2) worker killed in the middle of a training: prompt failure, then a fresh group

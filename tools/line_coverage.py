@@ -2,9 +2,12 @@
 
 Runs pytest in-process under a ``sys.settrace`` line tracer restricted to the package, main.py
 and neural_net_model.py, and counts a file's executable lines as the line numbers carried by its
-code objects (``co_lines``), i.e. the statements coverage.py measures. Files listed under
-``omit`` in .coveragerc are skipped like coverage.py skips them. Prints a per-file table and
-the total, which is what ``fail_under`` in .coveragerc is checked against.
+code objects (``co_lines``), i.e. the statements coverage.py measures. Python subprocesses (the
+multi-rank gloo tests' ranks, the REST service's worker ranks) are traced too: a
+``usercustomize`` hook (tools/_covhook) on their PYTHONPATH records their lines and the hits are
+merged. Files listed under ``omit`` in .coveragerc are skipped like coverage.py skips them.
+Prints a per-file table and the total, which is what ``fail_under`` in .coveragerc is checked
+against.
 
     python tools/line_coverage.py [pytest args...]      (default: tests -q -m "not gpu")
 """
@@ -12,8 +15,11 @@ from __future__ import annotations
 
 import configparser
 import fnmatch
+import glob
+import json
 import os
 import sys
+import tempfile
 import threading
 import types
 
@@ -67,6 +73,11 @@ def main(argv: list[str]) -> int:
             return tracer
         return None
 
+    sub_dir = tempfile.mkdtemp(prefix="pz_linecov_")
+    hook = os.path.join(ROOT, "tools", "_covhook")
+    os.environ["PZ_LINECOV_DIR"] = sub_dir
+    os.environ["PZ_LINECOV_FILES"] = json.dumps(sorted(files))
+    os.environ["PYTHONPATH"] = hook + (os.pathsep + os.environ["PYTHONPATH"] if os.environ.get("PYTHONPATH") else "")
     sys.settrace(global_tracer)
     threading.settrace(global_tracer)
     try:
@@ -74,6 +85,14 @@ def main(argv: list[str]) -> int:
     finally:
         sys.settrace(None)
         threading.settrace(None)
+    n_sub = 0
+    for path in glob.glob(os.path.join(sub_dir, "*.json")):
+        with open(path) as fh:
+            for f, lines in json.load(fh).items():
+                if f in hit:
+                    hit[f].update(lines)
+        n_sub += 1
+    print(f"(merged line hits of {n_sub} traced subprocesses)")
     total_exec = total_hit = 0
     rows = []
     for f in sorted(files):
@@ -87,6 +106,11 @@ def main(argv: list[str]) -> int:
         print(f"{name:64} {n:6d} {h:6d} {100.0 * h / max(n, 1):5.1f}%")
     pct = 100.0 * total_hit / max(total_exec, 1)
     print(f"{'TOTAL':64} {total_exec:6d} {total_hit:6d} {pct:5.1f}%")
+    if os.environ.get("PZ_LINECOV_MISSING"):  # show_missing: uncovered statement lines per file
+        for f in sorted(files):
+            miss = sorted(_executable(f) - hit[f])
+            if miss:
+                print(os.path.relpath(f, ROOT), ",".join(map(str, miss)))
     return int(rc)
 
 
