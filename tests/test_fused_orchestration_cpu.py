@@ -92,3 +92,27 @@ def test_fused_orchestration_schedule_progress_and_stats(models_tmpdir, monkeypa
     # the checkpoint written at the end carries the same progress
     again = NeuralNetworkModel.deserialize("orch")
     assert [p["epoch"] for p in again.progress] == [1, 4, 7, 10] and again.status == "Trained"
+
+
+def test_long_trainings_checkpoint_in_the_background(models_tmpdir, monkeypatch):
+    """CHECKPOINT_INTERVAL_S elapsed: the fused loop drains, records and writes a background
+    checkpoint mid-training (reference ``neural_net_model.py:488-492``)."""
+    fakes = []
+    monkeypatch.setattr(NeuralNetworkModel, "on_gpu", property(lambda self: getattr(self, "_fake_gpu", False)))
+    monkeypatch.setattr(NeuralNetworkModel, "_fused_trainer", lambda self: fakes.append(FakeTrainer(self)) or fakes[-1])
+    monkeypatch.setattr(network_mod, "CHECKPOINT_INTERVAL_S", 0.0)
+    saves = []
+    real = NeuralNetworkModel.serialize_background
+    monkeypatch.setattr(NeuralNetworkModel, "serialize_background", lambda self: saves.append(1) or real(self))
+    m = NeuralNetworkModel("long", [4, 8, 3], activation_algos=["relu", "softmax"])
+    m._fake_gpu = True
+    m.train([([float(i % 5), 1.0, -1.0, 0.0], [i % 3]) for i in range(80)], epochs=3, batch_size=8)
+    assert [s["record"] for s in fakes[0].steps] == [True, True, True]
+    assert len(saves) == 3 and m.status == "Trained"
+
+
+def test_fused_engine_declines_cpu_models_and_gpu_requests_fall_back(models_tmpdir):
+    m = NeuralNetworkModel("cpu", [4, 8, 2], activation_algos=["relu", "softmax"])
+    assert m._fused_trainer() is None  # CPU models train under autograd (reference semantics)
+    g = NeuralNetworkModel("want_gpu", [4, 8, 2], activation_algos=["relu", "softmax"], device="cuda")
+    assert g.device.type == ("cuda" if torch.cuda.is_available() else "cpu")

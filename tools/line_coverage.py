@@ -49,7 +49,24 @@ def _executable(path: str) -> set[int]:
             if isinstance(c, types.CodeType):
                 walk(c)
     walk(compile(src, path, "exec"))
-    # docstring-only / `pass` bodies carry lines too; drop the module docstring line like coverage.py
+    # coverage.py's default exclusion: a line marked `# pragma: no cover` — and, when it opens a
+    # block (`if ...:`, `def ...:`, `except ...:`), every line of that block — is not a statement
+    text = src.splitlines()
+    i = 0
+    while i < len(text):
+        line = text[i]
+        if "pragma: no cover" in line:
+            lines.discard(i + 1)
+            code = line.split("#", 1)[0].rstrip()
+            if code.endswith(":"):
+                indent = len(line) - len(line.lstrip())
+                j = i + 1
+                while j < len(text) and (not text[j].strip() or len(text[j]) - len(text[j].lstrip()) > indent):
+                    lines.discard(j + 1)
+                    j += 1
+                i = j
+                continue
+        i += 1
     return lines
 
 
