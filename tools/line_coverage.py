@@ -128,6 +128,12 @@ def main(argv: list[str]) -> int:
             miss = sorted(_executable(f) - hit[f])
             if miss:
                 print(os.path.relpath(f, ROOT), ",".join(map(str, miss)))
+    cfg = configparser.ConfigParser()
+    cfg.read(os.path.join(ROOT, ".coveragerc"))
+    gate = cfg.getfloat("report", "fail_under", fallback=0.0)
+    if rc == 0 and pct < gate:
+        print(f"FAIL: coverage {pct:.1f}% is below fail_under = {gate}")
+        return 2
     return int(rc)
 
 
