@@ -822,8 +822,10 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     if (bk64) return launch_layout<256, 256, 2, 4, OutT, AuxT, 30>(p, s);
     return buf ? launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s) : launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
   }
-  if (!prefer_128(p) && tiles(256, 128) >= kFill)
+  if (!prefer_128(p) && tiles(256, 128) >= kFill) {
+    if (bk64) return launch_layout<256, 128, 4, 2, OutT, AuxT, 30>(p, s);
     return buf ? launch_layout<256, 128, 4, 2, OutT, AuxT, 6>(p, s) : launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
+  }
   return buf ? launch_layout<128, 128, 2, 2, OutT, AuxT, 6>(p, s) : launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
 }
 
@@ -903,6 +905,16 @@ int gemm_split(const GemmArgs& p) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   constexpr int kFill = 240;
   if (tiles >= kFill || prefer_128(p)) return 1;
+  // PZ_GEMM_W128=1: bf16 outputs (forward / dX) on 256x128 tiles (64-deep ring) instead of a
+  // split. Isolated fwd [8192,1024] K=4096 runs 1008 vs 881 TF/s (tools/gemm_lab,
+  // profiles/r2_lab_skinny_fwd.txt) but the steps are SLOWER with it (mlp4 1.260-1.272 vs
+  // 1.243 ms, mlp8192 bf16 0.918 vs 0.878 ms, same box): off
+  static const bool w128 = [] {
+    const char* e = getenv("PZ_GEMM_W128");
+    return e != nullptr && atoi(e) == 1;
+  }();
+  const int t256x128 = ((p.M + 255) / 256) * ((p.N + 127) / 128);
+  if (w128 && p.out_dtype == DT_BF16 && t256x128 >= kFill) return 1;
   const int nk = p.K / (p.in_dtype == DT_FP8 ? 64 : kBK);
   for (int sp : {2, 4, 8})
     if (tiles * sp >= kFill && nk % sp == 0 && nk / sp >= 16) return sp;

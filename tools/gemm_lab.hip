@@ -69,7 +69,15 @@ struct Case {
 };
 
 static std::vector<Variant> variants_for(const Case& c) {
-  if (c.akc && !c.bkc && !c.f32out) return PZ_VARIANTS(true, false, uint16_t);
+  if (c.akc && !c.bkc && !c.f32out) {
+    std::vector<Variant> v = PZ_VARIANTS(true, false, uint16_t);
+    if (c.N <= 1024) {  // skinny forward (fwd_L3): split-K 2 (library) vs 256x128 tiles
+      v.push_back({"bk64_s2", launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>, 2});
+      v.push_back({"t256x128", launch_cfg<256, 128, 4, 2, true, false, uint16_t, uint16_t, 6>});
+      v.push_back({"t256x128bk64", launch_cfg<256, 128, 4, 2, true, false, uint16_t, uint16_t, 30>});
+    }
+    return v;
+  }
   if (c.akc && c.bkc && !c.f32out) {
     std::vector<Variant> v = PZ_VARIANTS(true, true, uint16_t);
     v.push_back({"m32x32", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 41>});
