@@ -368,8 +368,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // scales: a ring slot holds 64 K-bytes per row (the bf16 slot geometry), one MFMA K-step
   // VAR 9: A in e5m2 (bf8: gradients, wide range), B in e4m3 — the backward dX GEMM
   // dZ8 · W8ᵀ of the fp8 policy, with the backward (EPI_BWD) epilogues
-  constexpr bool F8 = VAR == 8 || VAR == 9;
-  constexpr int F8_FMT_A = VAR == 9 ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
+  // VAR 10 / 11: VAR 8 / 9 with buffer-addressed staging DMA
+  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11;
+  constexpr int F8_FMT_A = (VAR == 9 || VAR == 11) ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
   static_assert(!F8 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "fp8: K-contiguous in, bf16 out");
   // VAR 41 (lab A/B): bf16 on v_mfma_f32_32x32x16_bf16 (32x32 accumulator tiles, the fp8 layout)
   constexpr bool M32 = VAR == 41;
@@ -476,8 +477,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
   // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
   // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
-  constexpr bool BUF_A = VAR == 6 || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
-  constexpr bool BUF_B = VAR == 6 || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_A = VAR == 6 || VAR == 10 || VAR == 11 || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_B = VAR == 6 || VAR == 10 || VAR == 11 || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
   constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
   // VAR 30/31: full row tiles of the K-contiguous operands (use_bk64 checks M % BM, N % BN)
   constexpr bool FULL_KC = VAR == 30 || VAR == 31;
@@ -690,7 +691,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   const int g4 = 4 * (lane >> 4);
   if constexpr (ACC32) {
     const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
-    if constexpr (VAR == 9 || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    if constexpr (VAR == 9 || VAR == 11 || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
     else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
   } else if constexpr (std::is_same<OutT, uint16_t>::value) {
     epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
@@ -831,12 +832,24 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
 
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  // PZ_GEMM_F8BUF=1: buffer-addressed staging DMA (VAR 10 / 11), A/B
+  static const bool f8buf = [] {
+    const char* e = getenv("PZ_GEMM_F8BUF");
+    return e != nullptr && atoi(e) == 1;
+  }();
+  const bool buf = f8buf && buffer_ok(p);
   if (p.a_fmt == 1) {  // e5m2 x e4m3 (backward dX)
-    if (tiles >= 240 || p.split_k > 1) return launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>(p, s);
-    return launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 9>(p, s);
+    if (tiles >= 240 || p.split_k > 1)
+      return buf ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 11>(p, s)
+                 : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>(p, s);
+    return buf ? launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 11>(p, s)
+               : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 9>(p, s);
   }
-  if (tiles >= 240 || p.split_k > 1) return launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
-  return launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
+  if (tiles >= 240 || p.split_k > 1)
+    return buf ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 10>(p, s)
+               : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
+  return buf ? launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 10>(p, s)
+             : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
 }
 
 #endif  // PZ_GEMM_LAB
