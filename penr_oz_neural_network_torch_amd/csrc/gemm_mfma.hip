@@ -36,8 +36,15 @@ namespace {
 
 constexpr int kBK = 32;  // K depth of one ring slot (BK64 variants: two of these per slot)
 
-// Per-variant ring geometry: VAR 20/21 stage 64-deep K steps into two 64 KiB slots (one MFMA
-// interval = 64 MFMAs per wave, half the barriers per FLOP of the 32-deep ring)
+// Main-loop variants (template VAR). The library instantiates 0 (flat DMA, ragged > 4 GiB
+// operands), 6 (buffer DMA, 32-deep ring), 30 (buffer DMA, 64-deep 2-slot ring, the default),
+// 8 / 9 (fp8 e4m3 / e5m2 x e4m3) and 10 / 11 (their buffer-DMA forms, PZ_GEMM_F8BUF=1). The
+// rest are tools/gemm_lab probes whose measurements are in profiles/: 1 / 2 / 3 (no MFMA / no
+// DMA / no fragment reads), 4 (no deferred wait), 5 / 23 (3- / 5-slot rings), 20 / 21 / 31
+// (64-deep ring with flat DMA / split staging), 24 (L2 prefetch), 25 (buffer DMA for M/N-
+// contiguous operands only), 27-29 (cache policies), 41 (32x32x16 MFMA).
+// Per-variant ring geometry: VAR 20/21/30/31 stage 64-deep K steps into two 64 KiB slots (one
+// MFMA interval = 64 MFMAs per wave, half the barriers per FLOP of the 32-deep ring)
 template <int VAR> constexpr int var_bk() { return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31) ? 64 : 32; }
 template <int VAR> constexpr int var_ns() { return VAR == 5 ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4); }
 
