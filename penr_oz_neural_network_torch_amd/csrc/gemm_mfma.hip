@@ -38,14 +38,17 @@ constexpr int kBK = 32;  // K depth of one ring slot (BK64 variants: two of thes
 
 // Main-loop variants (template VAR). The library instantiates 0 (flat DMA, ragged > 4 GiB
 // operands), 6 (buffer DMA, 32-deep ring), 30 (buffer DMA, 64-deep 2-slot ring, the default),
-// 8 / 9 (fp8 e4m3 / e5m2 x e4m3) and 10 / 11 (their buffer-DMA forms, PZ_GEMM_F8BUF=1). The
+// 8 / 9 (fp8 e4m3 / e5m2 x e4m3), 10 / 11 (their buffer-DMA forms, PZ_GEMM_F8BUF=1) and 12 / 13
+// (fp8 on the 64-deep buffer-DMA ring: 128 K-bytes per slot, two MFMA K-steps). The
 // rest are tools/gemm_lab probes whose measurements are in profiles/: 1 / 2 / 3 (no MFMA / no
 // DMA / no fragment reads), 4 (no deferred wait), 5 / 23 (3- / 5-slot rings), 20 / 21 / 31
 // (64-deep ring with flat DMA / split staging), 24 (L2 prefetch), 25 (buffer DMA for M/N-
 // contiguous operands only), 27-29 (cache policies), 41 (32x32x16 MFMA).
 // Per-variant ring geometry: VAR 20/21/30/31 stage 64-deep K steps into two 64 KiB slots (one
 // MFMA interval = 64 MFMAs per wave, half the barriers per FLOP of the 32-deep ring)
-template <int VAR> constexpr int var_bk() { return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31) ? 64 : 32; }
+template <int VAR> constexpr int var_bk() {
+  return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31 || VAR == 12 || VAR == 13) ? 64 : 32;
+}
 template <int VAR> constexpr int var_ns() { return VAR == 5 ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4); }
 
 // K-contiguous slot [rows][BK]. BK 32: 64-B rows = 4 chunks; chunk XOR for conflict-free
@@ -376,8 +379,9 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // VAR 9: A in e5m2 (bf8: gradients, wide range), B in e4m3 — the backward dX GEMM
   // dZ8 · W8ᵀ of the fp8 policy, with the backward (EPI_BWD) epilogues
   // VAR 10 / 11: VAR 8 / 9 with buffer-addressed staging DMA
-  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11;
-  constexpr int F8_FMT_A = (VAR == 9 || VAR == 11) ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
+  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11 || VAR == 12 || VAR == 13;
+  constexpr bool F8_BWD = VAR == 9 || VAR == 11 || VAR == 13;
+  constexpr int F8_FMT_A = F8_BWD ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
   static_assert(!F8 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "fp8: K-contiguous in, bf16 out");
   // VAR 41 (lab A/B): bf16 on v_mfma_f32_32x32x16_bf16 (32x32 accumulator tiles, the fp8 layout)
   constexpr bool M32 = VAR == 41;
@@ -385,7 +389,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   constexpr bool ACC32 = F8 || M32;  // 32x32 accumulator tiles
   constexpr int TM8 = C::WTM / 32, TN8 = C::WTN / 32;
   struct Frags16 { i16x8_t a[KB][C::TM]; i16x8_t b[KB][C::TN]; };
-  struct Frags8 { i32x8_t a[TM8]; i32x8_t b[TN8]; };
+  struct Frags8 { i32x8_t a[KB][TM8]; i32x8_t b[KB][TN8]; };  // KB MFMA K-steps of 64 bytes
   struct Frags32 { i16x8_t a[2][TM8]; i16x8_t b[2][TN8]; };
   using Frags = std::conditional_t<F8, Frags8, std::conditional_t<M32, Frags32, Frags16>>;
   using AccT = std::conditional_t<ACC32, f32x16_t[TM8][TN8], f32x4_t[C::TM][C::TN]>;
@@ -415,12 +419,14 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
                                                                 __builtin_bit_cast(bf16x8_t, f.a[ks][i]), acc[i][j], 0, 0, 0);
     } else if constexpr (F8) {
 #pragma unroll
-      for (int i = 0; i < TM8; ++i)
+      for (int kb = 0; kb < KB; ++kb)
 #pragma unroll
-        for (int j = 0; j < TN8; ++j)  // issued as mfma(B, A): cbsz = B's format, blgp = A's;
-                                       // E8M0 block scales 127 = 1.0
-          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[j], f.a[i], acc[i][j], 0, F8_FMT_A, 0, 127,
-                                                                       0, 127);
+        for (int i = 0; i < TM8; ++i)
+#pragma unroll
+          for (int j = 0; j < TN8; ++j)  // issued as mfma(B, A): cbsz = B's format, blgp = A's;
+                                         // E8M0 block scales 127 = 1.0
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[kb][j], f.a[kb][i], acc[i][j], 0, F8_FMT_A,
+                                                                         0, 127, 0, 127);
     } else {
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
@@ -444,17 +450,21 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 #pragma unroll
         for (int i = 0; i < TM8; ++i) f.a[ks][i] = frag_kc(ta, wm * C::WTM + i * 32 + (lane & 31), (lane >> 5) + 2 * ks);
       }
-    } else if constexpr (F8) {  // lane l: row l&31, K bytes [32*(l>>5), +32) = 16-B chunks 2h, 2h+1
+    } else if constexpr (F8) {  // lane l: row l&31, K bytes [32*(l>>5), +32) of K-step kb = 16-B chunks
+                                // 4kb + 2h, 4kb + 2h + 1
       const int h2 = 2 * (lane >> 5);
 #pragma unroll
-      for (int j = 0; j < TN8; ++j) {
-        const int row = wn * C::WTN + j * 32 + (lane & 31);
-        f.b[j] = cat_frag(frag_kc(tb, row, h2), frag_kc(tb, row, h2 + 1));
-      }
+      for (int kb = 0; kb < KB; ++kb) {
 #pragma unroll
-      for (int i = 0; i < TM8; ++i) {
-        const int row = wm * C::WTM + i * 32 + (lane & 31);
-        f.a[i] = cat_frag(frag_kc(ta, row, h2), frag_kc(ta, row, h2 + 1));
+        for (int j = 0; j < TN8; ++j) {
+          const int row = wn * C::WTN + j * 32 + (lane & 31);
+          f.b[kb][j] = cat_frag(frag_kc<BK>(tb, row, 4 * kb + h2), frag_kc<BK>(tb, row, 4 * kb + h2 + 1));
+        }
+#pragma unroll
+        for (int i = 0; i < TM8; ++i) {
+          const int row = wm * C::WTM + i * 32 + (lane & 31);
+          f.a[kb][i] = cat_frag(frag_kc<BK>(ta, row, 4 * kb + h2), frag_kc<BK>(ta, row, 4 * kb + h2 + 1));
+        }
       }
     } else {
 #pragma unroll
@@ -478,17 +488,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     __builtin_amdgcn_sched_barrier(0);
   };
 
-  const int nk = p.K / (F8 ? 2 * kBK : BK) / split;  // K steps of this slice
+  const int nk = p.K / (F8 ? 2 * BK : BK) / split;  // K steps of this slice (fp8: 2 bytes per 16-bit unit)
   const int kt0 = slice * nk;
   // LDS-DMA addressing per operand: buffer (MUBUF, 32-bit per-lane offsets from one descriptor)
   // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
   // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
   // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
-  constexpr bool BUF_A = VAR == 6 || VAR == 10 || VAR == 11 || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
-  constexpr bool BUF_B = VAR == 6 || VAR == 10 || VAR == 11 || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_A = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_B = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
   constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
   // VAR 30/31: full row tiles of the K-contiguous operands (use_bk64 checks M % BM, N % BN)
-  constexpr bool FULL_KC = VAR == 30 || VAR == 31;
+  constexpr bool FULL_KC = VAR == 30 || VAR == 31 || VAR == 12 || VAR == 13;
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
   const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;
@@ -556,7 +566,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     using T4 = std::integral_constant<int, 4>;
     auto stage_g0 = [&](int kt) {
       stage_a_t(kt, T4{}, tw);
-      if constexpr (VAR == 20 || VAR == 30) stage_b_t(kt, T4{}, tw);
+      if constexpr (!(VAR == 21 || VAR == 31)) stage_b_t(kt, T4{}, tw);  // 21 / 31: group 1 stages B
     };
     stage(0, 0);
     wait_vm<0>();
@@ -698,7 +708,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   const int g4 = 4 * (lane >> 4);
   if constexpr (ACC32) {
     const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
-    if constexpr (VAR == 9 || VAR == 11 || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    if constexpr (F8_BWD || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
     else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
   } else if constexpr (std::is_same<OutT, uint16_t>::value) {
     epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
@@ -845,6 +855,19 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
     return e != nullptr && atoi(e) == 1;
   }();
   const bool buf = f8buf && buffer_ok(p);
+  // PZ_GEMM_F8BK64=1: the 64-deep ring (VAR 12 / 13: 256x256 tiles, full rows of both
+  // K-contiguous operands, K a multiple of 128 bytes per slice). Within noise of the 32-deep ring
+  // (f8 GEMMs -1..+3%, mlp8192 step 0.822-0.832 vs 0.819-0.827 ms, profiles/r2_ab_fp8_bk64.txt): off
+  static const bool bk64_on = [] {
+    const char* e = getenv("PZ_GEMM_F8BK64");
+    return e != nullptr && atoi(e) == 1;
+  }();
+  const int split = p.split_k > 1 ? p.split_k : 1;
+  const bool bk64 = bk64_on && buffer_ok(p) && p.M % 256 == 0 && p.N % 256 == 0 && p.K % 128 == 0 &&
+                    (p.K / 128) % split == 0 && (tiles >= 240 || p.split_k > 1);
+  if (bk64)
+    return p.a_fmt == 1 ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 13>(p, s)
+                        : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 12>(p, s);
   if (p.a_fmt == 1) {  // e5m2 x e4m3 (backward dX)
     if (tiles >= 240 || p.split_k > 1)
       return buf ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 11>(p, s)

@@ -186,7 +186,7 @@ def test_gemm_fp8_e5m2_backward(native_lib, M, N, K):
     assert (out.double() - exact).abs().max().item() < 0.15 * exact.abs().max().item()
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (4096 + 64, 4096, 512), (256, 1024, 8192)])
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (4096 + 64, 4096, 512), (256, 1024, 8192), (4096, 4096, 512)])
 def test_gemm_fp8_forward(native_lib, M, N, K):
     """e4m3 x e4m3 (v_mfma_scale_f32_32x32x64_f8f6f4) + dequant scales + fused stage epilogue +
     e4m3 copy of the output + amax, against an fp32 reference on the same e4m3 values."""
