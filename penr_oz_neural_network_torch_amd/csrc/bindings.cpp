@@ -208,6 +208,79 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
   PZ_HIP_CHECK(pz::gemm(p, cur_stream(A)));
 }
 
+// dW GEMM with the optimizer update fused into its epilogue (EPI_OPT): `grad` is the weight's
+// gradient view (shape / leading dimension only — it is NOT written); params / exp_avg /
+// exp_avg_sq / shadow are views of the same [in, out] shape; stats = this weight's 4 doubles
+void gemm_update_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& grad, int64_t M, int64_t N,
+                    int64_t K, double alpha, const Tensor& params, const optional<Tensor>& exp_avg,
+                    const optional<Tensor>& exp_avg_sq, const optional<Tensor>& shadow, const optional<Tensor>& stats,
+                    const optional<Tensor>& amax, bool adam, double lr, double beta1, double beta2, double eps,
+                    double bias_c1, double bias_c2_sqrt, double grad_scale, double l2, const optional<Tensor>& hp,
+                    const optional<Tensor>& epoch, int64_t stats_every) {
+  check_dev(A, "A");
+  auto p = gemm_args(A, a_kc, B, b_kc, grad, c10::nullopt, c10::nullopt, c10::nullopt, pz::EPI_OPT, {}, {}, alpha, false,
+                     M, N, K, 0, false, c10::nullopt);
+  TORCH_CHECK(grad.scalar_type() == at::kFloat, "pz::gemm_update: the gradient view must be fp32");
+  auto same = [&](const Tensor& t, at::ScalarType dt, const char* what) {
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == dt && t.dim() == 2 && t.size(0) >= M && t.size(1) >= N &&
+                    t.stride(1) == 1 && t.stride(0) == grad.stride(0),
+                "pz::gemm_update: ", what, " must match the gradient view's layout");
+  };
+  same(params, at::kFloat, "params");
+  pz::GemmOpt& o = p.opt;
+  o.params = params.data_ptr<float>();
+  o.adam = adam;
+  if (adam) {
+    TORCH_CHECK(exp_avg.has_value() && exp_avg_sq.has_value(), "pz::gemm_update: Adam needs moment buffers");
+    same(*exp_avg, at::kFloat, "exp_avg");
+    same(*exp_avg_sq, at::kFloat, "exp_avg_sq");
+    o.exp_avg = exp_avg->data_ptr<float>();
+    o.exp_avg_sq = exp_avg_sq->data_ptr<float>();
+  }
+  if (shadow.has_value() && shadow->defined()) {
+    same(*shadow, shadow->scalar_type(), "shadow");
+    TORCH_CHECK(shadow->scalar_type() == at::kBFloat16 || shadow->scalar_type() == at::kFloat,
+                "pz::gemm_update: bf16 or fp32 shadow");
+    o.shadow = shadow->data_ptr();
+    o.shadow_dtype = dt_of(*shadow);
+  }
+  if (stats.has_value() && stats->defined()) {
+    TORCH_CHECK(stats->scalar_type() == at::kDouble && stats->numel() >= 4 && stats->is_contiguous(),
+                "pz::gemm_update: stats must be 4 contiguous doubles");
+    o.stats = stats->data_ptr<double>();
+  }
+  if (amax.has_value() && amax->defined()) {
+    TORCH_CHECK(amax->scalar_type() == at::kFloat, "pz::gemm_update: amax must be fp32");
+    o.amax = amax->data_ptr<float>();
+  }
+  o.lr = static_cast<float>(lr);
+  o.beta1 = static_cast<float>(beta1);
+  o.beta2 = static_cast<float>(beta2);
+  o.eps = static_cast<float>(eps);
+  o.bias_c1 = static_cast<float>(bias_c1);
+  o.bias_c2_sqrt = static_cast<float>(bias_c2_sqrt);
+  o.grad_scale = static_cast<float>(grad_scale);
+  o.l2x2 = static_cast<float>(2.0 * l2);
+  o.stats_every = static_cast<int>(stats_every);
+  if (epoch.has_value() && epoch->defined()) o.epoch_ptr = epoch_counter(epoch);
+  if (stats_every > 1) TORCH_CHECK(o.epoch_ptr != nullptr, "pz::gemm_update: stats_every > 1 needs the epoch counter");
+  if (hp.has_value() && hp->defined()) {
+    TORCH_CHECK(hp->scalar_type() == at::kFloat && hp->is_contiguous() && hp->is_cuda(), "pz::gemm_update: hp table");
+    TORCH_CHECK(o.epoch_ptr != nullptr, "pz::gemm_update: an hp table needs the epoch counter");
+    o.hp = hp->data_ptr<float>();
+  }
+  TORCH_CHECK(pz::gemm_path(p) == 1, "pz::gemm_update: needs an MFMA-eligible bf16 shape (16-B aligned state)");
+  at::Tensor ws;
+  const int64_t ws_floats = pz::gemm_split_ws_floats(p);
+  if (ws_floats > 0) {
+    ws = at::empty({ws_floats}, A.options().dtype(at::kFloat));
+    p.split_k = pz::gemm_split(p);
+    p.ws = ws.data_ptr<float>();
+    p.counters = split_counters(static_cast<int>(((M + 255) / 256) * ((N + 255) / 256)), A.device());
+  }
+  PZ_HIP_CHECK(pz::gemm(p, cur_stream(A)));
+}
+
 int64_t gemm_path_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, int64_t M, int64_t N,
                      int64_t K) {
   auto p = gemm_args(A, a_kc, B, b_kc, C, c10::nullopt, c10::nullopt, c10::nullopt, 0, {}, {}, 1.0, false, M, N, K, 0,
@@ -708,6 +781,10 @@ TORCH_LIBRARY(pz, m) {
         "int epi_mode, int[] epi_i, float[] epi_f, float alpha, bool accumulate, int M, int N, int K, int idx_ld, "
         "bool force_generic, Tensor(c!)? mask=None, Tensor? scale_a=None, Tensor? scale_b=None, "
         "Tensor(d!)? out8=None, Tensor? out8_qscale=None, Tensor(e!)? amax=None) -> ()");
+  m.def("gemm_update(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor grad, int M, int N, int K, float alpha, "
+        "Tensor(a!) params, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor(d!)? shadow, Tensor(e!)? stats, "
+        "Tensor(f!)? amax, bool adam, float lr, float beta1, float beta2, float eps, float bias_c1, "
+        "float bias_c2_sqrt, float grad_scale, float l2, Tensor? hp=None, Tensor? epoch=None, int stats_every=1) -> ()");
   m.def("gemm_path(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor C, int M, int N, int K) -> int");
   m.def("stage_fwd(Tensor x, Tensor(a!) y, int[] epi_i, float[] epi_f) -> ()");
   m.def("stage_bwd(Tensor g, Tensor y, Tensor(a!) dx, int[] epi_i, float[] epi_f) -> ()");
@@ -755,6 +832,7 @@ TORCH_LIBRARY(pz, m) {
 TORCH_LIBRARY_IMPL(pz, CUDA, m) {
   m.impl("gemm", TORCH_FN(gemm_op));
   m.impl("gemm_path", TORCH_FN(gemm_path_op));
+  m.impl("gemm_update", TORCH_FN(gemm_update_op));
   m.impl("stage_fwd", TORCH_FN(stage_fwd_op));
   m.impl("stage_bwd", TORCH_FN(stage_bwd_op));
   m.impl("xent_head", TORCH_FN(xent_head_op));

@@ -143,6 +143,7 @@ int gemm_path(const GemmArgs& p) { return mfma_eligible(p) ? 1 : (wide_eligible(
 
 hipError_t gemm(const GemmArgs& p, hipStream_t s) {
   if (mfma_eligible(p)) return gemm_mfma(p, s);
+  if (p.epi_mode == EPI_OPT) return hipErrorInvalidValue;  // the fused update: bf16 MFMA path only
   if (wide_eligible(p)) return gemm_wide(p, s);
   // bitmask / e4m3 epilogues and e4m3 operands exist on the MFMA path only
   if (p.mask != nullptr || p.out8 != nullptr || p.in_dtype == DT_FP8) return hipErrorInvalidValue;

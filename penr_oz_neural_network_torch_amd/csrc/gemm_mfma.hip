@@ -353,6 +353,107 @@ PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int split, int& tm, i
 
 #include "gemm_epilogue.h"
 
+// EPI_OPT: the tile's accumulators are a block of the weight gradient g = alpha*AB; instead of
+// storing it (and a separate optimizer pass reading it back), apply the optimizer update of the
+// weight right here (GemmOpt). Each lane owns 4 consecutive columns of one row per fragment
+// (acc[i][j]: m = lane & 15, n = 4*(lane >> 4)), so p / m / v move as 16-B vectors like the fp32
+// C store they replace. The per-tile statistics (update-ratio sums, sum(w^2), amax) are reduced
+// in LDS and leave as one atomic per accumulator.
+template <class C, class Acc>
+PZ_DEV void epilogue_opt(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0, int n0, int wm, int wn, int lane) {
+  const GemmOpt& o = p.opt;
+  float lr = o.lr, bc1 = o.bias_c1, bc2s = o.bias_c2_sqrt;
+  int epoch = -1;
+  if (o.epoch_ptr != nullptr) epoch = *o.epoch_ptr;
+  if (o.hp != nullptr) {  // graph-replayed step: this epoch's hyper-parameters
+    const float* h = o.hp + 4 * static_cast<int64_t>(epoch);
+    lr = h[0];
+    bc1 = h[1];
+    bc2s = h[2];
+  }
+  const bool full = o.stats_every == 1 || (o.stats_every > 1 && (epoch < 0 || epoch % o.stats_every == 0));
+  const float step_size = lr / bc1;
+  const bool adam = o.adam != 0;
+  const int g4 = 4 * (lane >> 4);
+  double st[4] = {0.0, 0.0, 0.0, 0.0};
+  float am = 0.f;
+  static_for<C::TN>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const int n = n0 + wn * C::WTN + j * 16 + g4;
+    static_for<C::TM>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const int m = m0 + wm * C::WTM + i * 16 + (lane & 15);
+      if (n < p.N && m < p.M) {
+        const int64_t gi = static_cast<int64_t>(m) * p.ldc + n;
+        const f32x4_t p0 = *reinterpret_cast<const f32x4_t*>(o.params + gi);
+        f32x4_t mm = {0.f, 0.f, 0.f, 0.f}, vv = mm, p1;
+        if (adam) {
+          mm = *reinterpret_cast<const f32x4_t*>(o.exp_avg + gi);
+          vv = *reinterpret_cast<const f32x4_t*>(o.exp_avg_sq + gi);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float graw = acc[i][j][r] * p.alpha;
+          float mr = mm[r], vr = vv[r];
+          p1[r] = adam ? opt_update<true>(p0[r], graw, o.grad_scale, o.l2x2, lr, step_size, o.beta1, o.beta2, bc2s,
+                                          o.eps, mr, vr)
+                       : opt_update<false>(p0[r], graw, o.grad_scale, o.l2x2, lr, step_size, 0.f, 0.f, 1.f, 0.f, mr,
+                                           vr);
+          mm[r] = mr;
+          vv[r] = vr;
+        }
+        if (adam) {
+          *reinterpret_cast<f32x4_t*>(o.exp_avg + gi) = mm;
+          *reinterpret_cast<f32x4_t*>(o.exp_avg_sq + gi) = vv;
+        }
+        *reinterpret_cast<f32x4_t*>(o.params + gi) = p1;
+        if (o.shadow != nullptr) {
+          if (o.shadow_dtype == DT_BF16)
+            *reinterpret_cast<u32x2_t*>(static_cast<uint16_t*>(o.shadow) + gi) =
+                u32x2_t{pack_bf2(p1[0], p1[1]), pack_bf2(p1[2], p1[3])};
+          else
+            *reinterpret_cast<f32x4_t*>(static_cast<float*>(o.shadow) + gi) = p1;
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          st[3] += static_cast<double>(p1[r]) * p1[r];
+          if (full) {
+            const double d = static_cast<double>(p1[r] - p0[r]);
+            st[0] += d;
+            st[1] += d * d;
+            st[2] += p1[r];
+          }
+          am = fmaxf(am, fabsf(p1[r]));
+        }
+      }
+    });
+  });
+  const bool want_st = o.stats != nullptr, want_am = o.amax != nullptr;
+  if (!want_st && !want_am) return;
+  constexpr int NW = C::NT / 64;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) st[k] = wave_sum_d(st[k]);
+  am = wave_max(am);
+  __syncthreads();  // every wave is past its last ring read: the LDS is free
+  PZ_LDS double* part = (PZ_LDS double*)(smem);  // [NW][5]
+  const int w = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) part[w * 5 + k] = st[k];
+    part[w * 5 + 4] = am;
+  }
+  __syncthreads();
+  const int k = threadIdx.x;
+  if (k < 5) {
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) s = k == 4 ? fmax(s, part[q * 5 + 4]) : s + part[q * 5 + k];
+    if (k < 4 && want_st && (full || k == 3)) atomicAdd(o.stats + k, s);
+    if (k == 4 && want_am)  // non-negative floats order like their bits
+      atomicMax(reinterpret_cast<unsigned int*>(o.amax), __float_as_uint(static_cast<float>(s)));
+  }
+}
+
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
   constexpr int BK = var_bk<VAR>();
@@ -712,6 +813,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
   } else if constexpr (std::is_same<OutT, uint16_t>::value) {
     epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
+  } else if (p.epi_mode == EPI_OPT) {
+    epilogue_opt<C>(p, acc, smem, m0, n0, wm, wn, lane);
   } else {
   static_for<C::TN>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
@@ -919,7 +1022,16 @@ bool mfma_eligible(const GemmArgs& p) {
   if (!p.a_kc && p.M % 8 != 0) return false;
   if (p.idx_ld % 2 != 0) return false;  // 4-element epilogue groups start at even element indices
   // fused stage epilogues: bf16 output only; accumulate: fp32 output only
-  if (p.out_dtype == DT_F32 && p.epi_mode != EPI_STORE) return false;
+  if (p.out_dtype == DT_F32 && p.epi_mode != EPI_STORE && p.epi_mode != EPI_OPT) return false;
+  if (p.epi_mode == EPI_OPT) {  // fused optimizer update: plain gradient tiles, 16-B state vectors
+    if (p.out_dtype != DT_F32 || p.bias != nullptr || p.colsum != nullptr || p.accumulate || p.mask != nullptr ||
+        p.out8 != nullptr || p.ldc % 4 != 0 || p.opt.params == nullptr || !al16(p.opt.params))
+      return false;
+    if (p.opt.adam && (!al16(p.opt.exp_avg) || !al16(p.opt.exp_avg_sq))) return false;
+    if (p.opt.shadow != nullptr &&
+        (reinterpret_cast<uintptr_t>(p.opt.shadow) & (p.opt.shadow_dtype == DT_BF16 ? 7 : 15)) != 0)
+      return false;
+  }
   if (p.out_dtype == DT_BF16 && p.accumulate) return false;
   if (p.bias != nullptr && !al16(p.bias)) return false;
   if (p.out8 != nullptr && (p.out_dtype != DT_BF16 || p.epi_mode == EPI_BWD || p.ldout8 % 8 != 0 ||

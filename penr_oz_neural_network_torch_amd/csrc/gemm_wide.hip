@@ -245,7 +245,7 @@ hipError_t launch_wide_in(const GemmArgs& p, hipStream_t s) {
 // reference's 9x9 tic-tac-toe layers) stay on the generic VALU tile, which wastes fewer lanes
 bool wide_eligible(const GemmArgs& p) {
   if (p.force_generic || (p.in_dtype != DT_F32 && p.in_dtype != DT_F64)) return false;
-  if (p.mask != nullptr || p.out8 != nullptr || p.split_k > 1) return false;
+  if (p.mask != nullptr || p.out8 != nullptr || p.split_k > 1 || p.epi_mode == EPI_OPT) return false;
   return static_cast<int64_t>(p.M) * p.N >= 64 * 64 && p.K >= 16;
 }
 

@@ -62,15 +62,7 @@ PZ_DEV void block_reduce_add(double v[4], double* dst, bool full = true) {
 // one parameter's update: returns the new value; m / v are Adam's moments (in and out)
 template <bool ADAM>
 PZ_DEV float update_one(const OptArgs& a, float p0, float graw, float l2x2, float step_size, float& m, float& v) {
-  const float g = graw * a.grad_scale + l2x2 * p0;
-  if constexpr (ADAM) {
-    m = m + (1.f - a.beta1) * (g - m);
-    v = v * a.beta2 + (1.f - a.beta2) * g * g;
-    const float denom = sqrtf(v) / a.bias_c2_sqrt + a.eps;
-    return p0 - step_size * (m / denom);
-  } else {
-    return p0 - a.lr * g;
-  }
+  return opt_update<ADAM>(p0, graw, a.grad_scale, l2x2, a.lr, step_size, a.beta1, a.beta2, a.bias_c2_sqrt, a.eps, m, v);
 }
 
 // max |w_new| of the block -> one atomic per block (non-negative floats order like their bits)

@@ -214,4 +214,24 @@ PZ_DEV double wave_sum_d(double v) {
   return v;
 }
 
+// ------------------------------------------------------------------------------------------
+// one parameter's optimizer update, shared by optimizer_step (optim.hip) and the dW-GEMM-fused
+// update (EPI_OPT, gemm_mfma.hip) so both round identically. Adam = torch.optim.Adam's single-
+// tensor step (lerp_, mul_/addcmul_, sqrt/div/add_, addcdiv_); SGD = the reference's
+// `p -= lr * grad` (neural_net_model.py:496-507). g = graw * grad_scale + 2*l2*p0 (L2 term).
+// ------------------------------------------------------------------------------------------
+template <bool ADAM>
+PZ_DEV float opt_update(float p0, float graw, float grad_scale, float l2x2, float lr, float step_size, float beta1,
+                        float beta2, float bias_c2_sqrt, float eps, float& m, float& v) {
+  const float g = graw * grad_scale + l2x2 * p0;
+  if constexpr (ADAM) {
+    m = m + (1.f - beta1) * (g - m);
+    v = v * beta2 + (1.f - beta2) * g * g;
+    const float denom = sqrtf(v) / bias_c2_sqrt + eps;
+    return p0 - step_size * (m / denom);
+  } else {
+    return p0 - lr * g;
+  }
+}
+
 }  // namespace pz

@@ -15,6 +15,31 @@ enum EpiMode : int {
   EPI_STORE = 0,  // C = alpha*AB (+bias)                      [+ optional colsum of C]
   EPI_FWD = 1,    // C = epi_fwd(alpha*AB + bias)               (fused dropout/act/dropout)
   EPI_BWD = 2,    // C = epi_bwd(alpha*AB, aux)                 [+ optional colsum of C]
+  EPI_OPT = 3,    // C is NOT stored: g = alpha*AB is the gradient of the fp32 weight p[M][N] and the
+                  // optimizer update of p (GemmOpt) runs in the epilogue (fp32 output, MFMA path)
+};
+
+// EPI_OPT: the weight-gradient GEMM applies the update of the weight whose gradient it produces
+// (single process: nothing has to be reduced first) — the fp32 gradient is never written to
+// memory nor read back by a separate optimizer pass (8 B/param of HBM traffic and one launch per
+// weight saved), and the update leaves the step's tail. Numerics are those of optimizer_step
+// (torch.optim.Adam single-tensor / the reference's SGD). Element (m, n) of every array below is
+// at m * ldc + n (the weight's own [in, out] layout, the dW GEMM's C).
+struct GemmOpt {
+  float* params;          // fp32 master weight
+  float* exp_avg;         // Adam moments (nullptr: SGD)
+  float* exp_avg_sq;
+  void* shadow;           // low-precision GEMM copy written after the update (nullptr: none)
+  int shadow_dtype;       // DT_BF16 or DT_F32
+  int adam;
+  double* stats;          // this weight's 4 accumulators: sum(dw), sum(dw^2), sum(w), sum(w^2)
+  float* amax;            // optional: max |w_new| (fp8 weight scaling)
+  const float* hp;        // graph-replayed steps: {lr, bias_c1, bias_c2_sqrt, -} of epoch *epoch_ptr
+  const int* epoch_ptr;
+  int stats_every;        // as OptArgs::stats_every
+  float lr, beta1, beta2, eps, bias_c1, bias_c2_sqrt;
+  float grad_scale;       // 1 / world
+  float l2x2;             // 2 * l2 (the L2 term's gradient, weights only)
 };
 
 // C[M][N] = op(A) · op(B); row-major C with leading dim ldc.
@@ -62,6 +87,7 @@ struct GemmArgs {
   int split_k;
   float* ws;       // [tiles * split_k][BM * BN] fp32
   int* counters;   // [tiles], zero; reset by the last arriver
+  GemmOpt opt;     // EPI_OPT only
 };
 
 // split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().

@@ -172,6 +172,29 @@ class FusedOptimizer:
         if g is not None:
             self._launch(grads, *g, l2, grad_scale, max_grid)
 
+    def gemm_update(self, a: torch.Tensor, a_kc: bool, b: torch.Tensor, b_kc: bool, seg, l2: float,
+                    grad_scale: float, parity: int = 0) -> None:
+        """The weight-gradient GEMM ``op(a) @ op(b)`` of segment ``seg`` with this weight's update
+        fused into its epilogue (``pz::gemm_update``, EPI_OPT): the gradient is never stored. Same
+        hyper-parameters, statistics and shadow / amax targets as :meth:`step_group` would use."""
+        lr, b1, b2, eps, bc1, bc2s = self._hp
+        hp, ctr = self.graph_tables or (None, None)
+        every = self.stats_every
+        if every > 1 and ctr is None:
+            every = 1
+        slot = self.slot_of.get(id(seg))
+        stats = self.stats[self.cur][4 * slot:4 * slot + 4] if slot is not None else None
+        view = self.store.view
+        w = view(seg)  # also the layout of the (never stored) gradient
+        M, N = w.shape
+        K = a.shape[1] if a_kc else a.shape[0]
+        torch.ops.pz.gemm_update(a, a_kc, b, b_kc, w, M, N, K, 1.0, w,
+                                 view(seg, self.exp_avg) if self.adam else None,
+                                 view(seg, self.exp_avg_sq) if self.adam else None,
+                                 self.shadow_sets[parity].get(seg.offset), stats,
+                                 self.amax_sets[parity].get(seg.offset), self.adam, lr, b1, b2, eps, bc1, bc2s,
+                                 grad_scale, l2, hp, ctr, every)
+
     def begin_step(self, lr: float) -> None:
         if self.adam:
             group = self.torch_opt.param_groups[0]

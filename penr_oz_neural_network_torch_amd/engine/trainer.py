@@ -254,10 +254,24 @@ class FusedTrainer:
         # one launch per GEMM weight except the first layer's, which comes last anyway and
         # shares the final launch with the small accumulated parameters (biases, BN, embedding)
         gemm_w = [st.seg_w.offset for st in self.stages if st.kind == "gemm"]
-        self._early_keys = set(gemm_w[1:])
+        # PZ_OPT_FUSE (one process, bf16 policy): every dense weight is updated INSIDE its own dW
+        # GEMM's epilogue (pz::gemm_update, EPI_OPT) — the fp32 gradient never makes the HBM round
+        # trip and no weight update is left for the side stream or the step's tail; the last launch
+        # only updates the biases / batchnorm / embedding parameters. Under data parallelism the
+        # gradient must be all-reduced first, so the launches stay separate. The fused update's
+        # traffic runs AFTER each CU's main loop instead of beside other GEMMs, so it pays only
+        # where it removes most bytes: SGD (10 vs 18 B/param; deep16x8192 40.2 vs 40.6 ms), not
+        # Adam (26 vs 34 B/param; mlp4 1.39 vs 1.25 ms, mlp8192 0.96 vs 0.87, mlp4x8192 11.2 vs
+        # 10.8 — profiles/r2_ab_opt_fuse.txt). auto (default) = SGD only; 1 = always; 0 = never.
+        mode = os.environ.get("PZ_OPT_FUSE", "auto")
+        want = mode == "1" or (mode == "auto" and model.optimizer is None)
+        self.fuse_opt = (want and self.overlap and not self.ctx.enabled and self.compute == torch.bfloat16
+                         and not self.fp8)
+        self._fuse_ok: dict = {}
+        self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
         self._after_dx = os.environ.get("PZ_OPT_AFTER_DX", "1") == "1"  # measured 0.6% faster on one GPU
         self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "2")))  # first-layer dW under DP
-        self.opt.define_groups(gemm_w[1:])
+        self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
         # PZ_OPT_MERGE=1: the side-stream updates of all layers but the first are queued together
         # behind the last of their gradients (one event instead of one per layer). Default on:
         # same-box A/B x3 mlp4 1.311-1.320 vs 1.321-1.326 ms, fp8 mlp8192 0.867 vs 0.869 ms;
@@ -960,6 +974,9 @@ class FusedTrainer:
                 rec[("grad", before.layers[-1])] = dx[:batch * st.pos_in]
             return dx, False
         # GEMM stage: dW = x_inᵀ · dZ
+        if self.fuse_opt and self._ov is not None:
+            self._dw_update(st, x_in, g)
+            return self._backward_dx(st, before, g, batch, p, keys, rec)
         w_grad = self._w_grad(st.seg_w)
         # Data parallel: the first layer's gradient is the last bucket of the backward and nothing
         # is left to hide its all-reduce behind, so its dW GEMM runs in row chunks and chunk c's
@@ -992,6 +1009,22 @@ class FusedTrainer:
                 self._opt_async(self._side_pending)
                 self._side_pending = []
         return out
+
+    def _dw_update(self, st: Stage, x_in, g) -> None:
+        """dW GEMM + the weight's optimizer update in one launch (fuse_opt). The update writes the
+        OTHER shadow parity, so this layer's dX GEMM (next) still reads the weights of this step.
+        Shapes the MFMA path does not take fall back to dW GEMM + a one-segment update launch."""
+        _, l2, scale = self._ov
+        parity = 1 - self.parity
+        key = (st.seg_w.offset, x_in.shape[0], g.shape[0])
+        ok = self._fuse_ok.get(key)
+        if ok is None:
+            ok = self._fuse_ok[key] = PF.gemm_path(x_in, False, g, False, self.store.view(st.seg_w)) == "mfma"
+        if ok:
+            self.opt.gemm_update(x_in, False, g, False, st.seg_w, l2, scale, parity)
+        else:
+            PF.gemm(x_in, False, g, False, self._w_grad(st.seg_w))
+            self.opt.step_group(st.seg_w.offset, self.grads, l2, scale, parity)
 
     def _backward_dx(self, st: Stage, before: Stage | None, g, batch, p, keys, rec):
         if before is None:

@@ -221,6 +221,59 @@ def test_fp8_training_tracks_bf16():
 
 
 @pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
+def test_fused_dw_update_matches_separate_launches(monkeypatch, optimizer):
+    """PZ_OPT_FUSE: the weight updates applied in the dW GEMMs' epilogues reproduce the unfused
+    schedule (dW GEMM -> fp32 gradient -> side-stream optimizer launches): costs, update ratios,
+    parameters and Adam moments. Shapes cover the one-pass and the split-K dW GEMM."""
+    sizes = [1024, 2048, 1024, 256]
+    algos = ["relu", "relu", "softmax"]
+    n, S, steps = 8192, 4096, 4
+    g = torch.Generator().manual_seed(5)
+    inputs = torch.randn(n, sizes[0], generator=g)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    idx = torch.randint(0, n, (steps, S), generator=g)
+    runs = {}
+    for run in ("0", "0b", "1"):  # 0b: a second unfused run = the noise floor between two runs
+        fuse = run[0]
+        monkeypatch.setenv("PZ_OPT_FUSE", fuse)
+        gpu, _ = _pair(sizes, algos, optimizer, "bfloat16")
+        tr = FusedTrainer(gpu)
+        assert tr.fuse_opt == (fuse == "1")
+        tr.load_tensors(inputs, labels, seed=3)
+        tr.begin(steps)
+        for e in range(steps):
+            tr.step(e, 0.005, S, 0.1, 1e-3, want_ratios=e % 2 == 0, record=False, indices=idx[e])
+        out = tr.drain()
+        if fuse == "1":
+            assert tr._fuse_ok and all(tr._fuse_ok.values())  # every dW GEMM took the fused path
+        state = gpu.optimizer.state_dict() if gpu.optimizer is not None else None
+        runs[run] = ([c for _, c, _, _ in out], [r for _, _, r, _ in out], gpu._param_store.flat.clone(), state,
+                     tr.opt.exp_avg.clone() if tr.opt.adam else None)
+    (c0, r0, p0, s0, m0), (c1, r1, p1, s1, m1) = runs["0"], runs["1"]
+    for a, b in zip(c0, c1):
+        assert abs(a - b) < 1e-4 * max(1.0, abs(a)), (c0, c1)
+    for a, b in zip(r0, r1):
+        assert (a is None) == (b is None)
+        if a is not None:
+            assert all(abs(x - y) < 1e-3 * abs(x) + 1e-7 for x, y in zip(a, b)), (a, b)
+    # both schedules sum split-K slices and bias column sums in arrival order, so two runs of the
+    # SAME schedule already differ at fp32 rounding level, which bf16 activation rounding and Adam's
+    # ~lr * sign(m) first steps amplify: fused vs separate must stay within that noise floor
+    pn = runs["0b"][2]
+    d, dn = (p0 - p1).abs(), (p0 - pn).abs()
+    mean, mean_n = d.mean().item(), dn.mean().item()
+    frac, frac_n = (d > 1e-3).double().mean().item(), (dn > 1e-3).double().mean().item()
+    assert mean <= 3 * mean_n + 1e-7 and frac <= 3 * frac_n + 1e-4, (mean, mean_n, frac, frac_n)
+    if optimizer == "adam":
+        assert mean < 1e-4, mean
+        assert (m0 - m1).abs().mean().item() <= 3 * (m0 - runs["0b"][4]).abs().mean().item() + 1e-8
+        for k in s0["state"]:
+            assert float(s0["state"][k]["step"]) == float(s1["state"][k]["step"]) == steps
+    else:
+        assert d.max().item() < 1e-3 and mean < 1e-6, (d.max(), mean)
+
+
+@pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
 def test_graph_replay_matches_eager_steps(optimizer):
     """hipGraph-replayed steps (epoch-dependent dropout keys, sampler seeds and optimizer
     hyper-parameters read from the device epoch counter / tables) reproduce eager launches."""

@@ -306,6 +306,47 @@ def test_adam_matches_torch(native_lib):
         torch.testing.assert_close(store.view(seg), ref_params[seg.param_index].detach(), rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("shape", [(512, 4096, 512), (1024, 2048, 4096)])  # one pass / split-K (8 slices)
+@pytest.mark.parametrize("adam", [True, False])
+def test_gemm_update_matches_separate_update(native_lib, shape, adam):
+    """dW GEMM with the optimizer update in its epilogue (EPI_OPT) vs the fp64 gradient GEMM followed
+    by the same update formula in torch fp32 (torch.optim.Adam's single-tensor step / the reference's
+    SGD), plus the statistics the update reduces (update-ratio sums, sum w^2, amax)."""
+    M, N, K = shape
+    g = torch.Generator(device="cpu").manual_seed(M + N + K + adam)
+    a = (torch.randn(K, M, generator=g) * 0.1).to(DEV, torch.bfloat16)  # x_in [rows, in]
+    b = (torch.randn(K, N, generator=g) * 0.1).to(DEV, torch.bfloat16)  # dZ [rows, out]
+    p0 = torch.randn(M, N, generator=g).to(DEV)
+    m0 = (torch.randn(M, N, generator=g) * 0.01).to(DEV)
+    v0 = (torch.rand(M, N, generator=g) * 1e-3 + 1e-4).to(DEV)
+    p, m, v = p0.clone(), m0.clone(), v0.clone()
+    shadow = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    stats = torch.zeros(4, device=DEV, dtype=torch.float64)
+    amax = torch.zeros(1, device=DEV)
+    lr, b1, b2, eps, l2, t, scale = 0.01, 0.9, 0.99, 1e-7, 1e-3, 3, 0.5
+    bc1, bc2s = 1 - b1 ** t, math.sqrt(1 - b2 ** t)
+    assert PF.gemm_path(a, False, b, False, p) == "mfma"
+    torch.ops.pz.gemm_update(a, False, b, False, p, M, N, K, 1.0, p, m if adam else None, v if adam else None,
+                             shadow, stats, amax, adam, lr, b1, b2, eps, bc1, bc2s, scale, l2, None, None, 1)
+    grad = (a.double().t() @ b.double()).float()
+    gg = grad * scale + 2 * l2 * p0
+    if adam:
+        m_ref = m0 + (1 - b1) * (gg - m0)
+        v_ref = v0 * b2 + (1 - b2) * gg * gg
+        p_ref = p0 - (lr / bc1) * (m_ref / (v_ref.sqrt() / bc2s + eps))
+        torch.testing.assert_close(m, m_ref, rtol=1e-4, atol=1e-6)
+        torch.testing.assert_close(v, v_ref, rtol=1e-4, atol=1e-9)
+    else:
+        p_ref = p0 - lr * gg
+        assert torch.equal(m, m0) and torch.equal(v, v0)  # SGD has no moments
+    torch.testing.assert_close(p, p_ref, rtol=1e-5, atol=1e-5)
+    assert torch.equal(shadow, p.to(torch.bfloat16))
+    d = (p - p0).double()
+    ref_st = torch.stack([d.sum(), (d * d).sum(), p.double().sum(), (p.double() ** 2).sum()])
+    torch.testing.assert_close(stats, ref_st, rtol=1e-9, atol=1e-9)
+    assert amax.item() == p.abs().max().item()
+
+
 def test_histogram_and_moments(native_lib):
     x = torch.randn(10000, 7, device=DEV, dtype=torch.float64) * 3 + 1
     s = PF.tensor_summary(x, "tanh", 100)
