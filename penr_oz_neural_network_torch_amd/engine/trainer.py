@@ -10,7 +10,7 @@ HIP kernels with nothing on the host between epochs:
     per stage:  GEMM(+bias+dropout+act+dropout epilogue) | batchnorm(+epilogue) | flatten(+dropout)
     head:       xent_head / mse_head  (loss + dZ of the last stage + its bias-grad colsum)
     per stage, reversed:
-                dW GEMM  (XᵀdZ straight into the flat grad buffer: fp32; bf16 under data parallel)
+                dW GEMM  (XᵀdZ straight into the gradient buffer, bf16; PZ_GRAD_DTYPE=fp32: fp32)
                 -> async RCCL all-reduce of that bucket (data parallel)
                 dX GEMM  (dZ Wᵀ with the previous stage's epilogue derivative + bias colsum fused)
                 | batchnorm_bwd | embedding_bwd
@@ -197,9 +197,14 @@ class FusedTrainer:
         # deltas of 1.3e-5 / 1.8e-5 — a few bf16 ulps of the update, far below minibatch noise —
         # while the fp32 L2 bucket of the headline model (67 MB) would no longer hide behind the
         # remaining backward (dX L2 + dW L1, ~0.3 ms) at a ~300 GB/s ring over xGMI.
+        # One process: the dense weight gradients are stored in bf16 as well (PZ_GRAD_DTYPE, default
+        # bf16; fp32 keeps them exact): half the dW store and optimizer read traffic, the same
+        # rounding the DP buckets already apply. Same-box A/B x3: mlp4 1.204-1.210 vs 1.212-1.221 ms,
+        # fp8 mlp8192 0.801-0.809 vs 0.810-0.814 (profiles/r2_ab_opt_sched.txt).
         self.grads16: dict[int, torch.Tensor] = {}
         policy = os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower()
-        if self.ctx.enabled and self.compute == torch.bfloat16 and policy in ("bf16", "bfloat16"):
+        local16 = os.environ.get("PZ_GRAD_DTYPE", "bf16").lower() in ("bf16", "bfloat16")
+        if self.compute == torch.bfloat16 and (local16 if not self.ctx.enabled else policy in ("bf16", "bfloat16")):
             buf16 = torch.zeros(max(1, self.store.accum_offset), device=self.dev, dtype=torch.bfloat16)
             for st in self.stages:
                 if st.kind == "gemm":
@@ -248,7 +253,7 @@ class FusedTrainer:
         # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
         self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
         # PZ_OPT_PRIO=-1: the side stream at high priority (its workgroups are dispatched ahead of
-        # a GEMM's pending ones)
+        # a GEMM's pending ones); within noise of priority 0 (profiles/r2_ab_opt_sched.txt)
         prio = int(os.environ.get("PZ_OPT_PRIO", "0"))
         self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
         # one launch per GEMM weight except the first layer's, which comes last anyway and

@@ -87,7 +87,7 @@ TOL = {  # (comm, world): (cost rel, adam mean |dp|, adam frac |dp| > 1e-3, sgd 
     (2, "adam", "fp32", False), (2, "adam", "bf16", False), (2, "stochastic", "fp32", False),
     (2, "stochastic", "bf16", False), (2, "adam", "fp32", True),
     (8, "adam", "bf16", False), (8, "stochastic", "fp32", False), (8, "stochastic", "bf16", False)])
-def test_multi_rank_step_equals_single_rank(tmp_path, world, optimizer, comm, bn):
+def test_multi_rank_step_equals_single_rank(tmp_path, monkeypatch, world, optimizer, comm, bn):
     """A W-rank data-parallel fused step == one rank on the concatenated batch (W ranks share the
     box's GPU over gloo; the code path is the RCCL one). Batchnorm statistics are synchronised:
     every rank ends with the single rank's running mean / variance."""
@@ -99,6 +99,7 @@ def test_multi_rank_step_equals_single_rank(tmp_path, world, optimizer, comm, bn
 
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
     model = _build(optimizer, comm, bn)
+    monkeypatch.setenv("PZ_GRAD_DTYPE", comm)  # the single process stores its gradients like the buckets
     tr = FusedTrainer(model)
     x, y, idx = _data(world)
     tr.load_tensors(x, y, seed=3)
@@ -154,13 +155,14 @@ def _forced_main(rank, comm, out_path):
 
 
 @pytest.mark.parametrize("comm", ["fp32", "bf16"])
-def test_forced_rccl_world1_matches_no_comm(tmp_path, comm):
+def test_forced_rccl_world1_matches_no_comm(tmp_path, monkeypatch, comm):
     out = str(tmp_path / "forced.pt")
     mp.start_processes(_forced_main, args=(comm, out), nprocs=1, start_method="spawn")
     got = torch.load(out, weights_only=True)
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
     model = _build("adam", "bf16")
+    monkeypatch.setenv("PZ_GRAD_DTYPE", comm)
     tr = FusedTrainer(model, DataParallelContext())
     x, y, idx = _data()
     tr.load_tensors(x, y, seed=3)

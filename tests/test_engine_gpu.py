@@ -236,6 +236,7 @@ def test_fused_dw_update_matches_separate_launches(monkeypatch, optimizer):
     for run in ("0", "0b", "1"):  # 0b: a second unfused run = the noise floor between two runs
         fuse = run[0]
         monkeypatch.setenv("PZ_OPT_FUSE", fuse)
+        monkeypatch.setenv("PZ_GRAD_DTYPE", "fp32")  # the unfused schedule's gradients exact, as the fused ones
         gpu, _ = _pair(sizes, algos, optimizer, "bfloat16")
         tr = FusedTrainer(gpu)
         assert tr.fuse_opt == (fuse == "1")
