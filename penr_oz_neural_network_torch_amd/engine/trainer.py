@@ -293,6 +293,9 @@ class FusedTrainer:
             sizes = {st.seg_w.offset: st.seg_w.numel for st in self.stages if st.kind == "gemm"}
             self._trickle_key = max(gemm_w[1:], key=lambda k: sizes[k])
         self._side_pending: list = []
+        self._pf_args = None       # (epoch, parity, batch) of the sample _prefetch gathers next
+        self._pf_ready = None      # ((epoch, parity, batch, data id), event) of a gathered sample
+        self.prefetched_steps = 0  # steps that consumed a prefetched sample
         self._opt_done = None
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
         self._ov = None
@@ -390,10 +393,14 @@ class FusedTrainer:
         self._invalidate_graphs()  # captured steps point at the old buffers
         dev, cd = self.dev, self.compute
         pos = self.block
-        self.x_in = torch.empty(rows_b, self.data.shape[1], device=dev, dtype=torch.float32 if
-                                self.stages[0].kind == "embed" else cd)
-        self.lab = torch.empty(rows_b, device=dev, dtype=torch.int64) if self.head == "softmax" else None
-        self.picked = torch.empty(rows_b, device=dev, dtype=torch.int64)
+        # sampled inputs / labels / picks, one set per weight-shadow parity: the NEXT step's sample
+        # can be gathered into the other set while this step still reads its own (_prefetch)
+        self._sample_sets = [(torch.empty(rows_b, self.data.shape[1], device=dev, dtype=torch.float32 if
+                                          self.stages[0].kind == "embed" else cd),
+                              torch.empty(rows_b, device=dev, dtype=torch.int64) if self.head == "softmax" else None,
+                              torch.empty(rows_b, device=dev, dtype=torch.int64)) for _ in range(2)]
+        self.x_in, self.lab, self.picked = self._sample_sets[0]
+        self._pf_ready = None
         self.tgt = torch.empty(rows_b, self.targets.shape[1], device=dev, dtype=cd) if self.targets is not None \
             else None
         for st in self.stages:
@@ -458,6 +465,8 @@ class FusedTrainer:
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             self.opt_stream.wait_event(ready)
+            if self._pf_args is not None:
+                self._prefetch()
             for key, handles, stages in items:
                 for h in handles:
                     self.ctx.wait_one(h)
@@ -465,6 +474,19 @@ class FusedTrainer:
                 if self.fp8:
                     for st in stages:
                         self._refresh_fp8_weights(st, 1 - self.parity)
+
+    def _prefetch(self) -> None:
+        """Gather the next step's minibatch into the other sample set (current stream: the side
+        stream, after the event that orders it behind everything the previous step read)."""
+        epoch, sel, batch = self._pf_args
+        self._pf_args = None
+        x, lab, picked = self._sample_sets[sel]
+        seed = self._gather_seed(epoch)
+        torch.ops.pz.gather_rows(self.data, None, seed[0], seed[1], x, batch, self.labels, lab, picked, None, None,
+                                 None)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(self.dev))
+        self._pf_ready = ((epoch, sel, batch, id(self.data)), ev)
 
     def _plan_fp8(self, rows_b: int) -> None:
         """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
@@ -719,8 +741,24 @@ class FusedTrainer:
             idx = indices.to(device=self.dev, dtype=torch.int64).contiguous()
             if idx.numel() < batch:
                 raise ValueError(f"need {batch} indices, got {idx.numel()}")
-        ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
-                        self.epoch_ctr if capture else None, self.data8, self.x8 if self.data8 is not None else None)
+        self.x_in, self.lab, self.picked = self._sample_sets[self.parity]
+        pf, self._pf_ready = self._pf_ready, None
+        if pf is not None and idx is None and not capture and pf[0] == (epoch, self.parity, batch, id(self.data)):
+            main.wait_event(pf[1])  # gathered by the previous step's side stream (_prefetch)
+            self.prefetched_steps += 1
+        else:
+            ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
+                            self.epoch_ctr if capture else None, self.data8,
+                            self.x8 if self.data8 is not None else None)
+        # PZ_PREFETCH=1: the next step's sample rides on this step's side stream, beside the dW GEMM
+        # of the first layer, instead of opening the next step between HBM-bound updates. Off: the
+        # gather starves beside a one-tile-per-CU GEMM (82 us instead of 10) and slows it (dW_L1 90
+        # -> 105 us): mlp4 1.221-1.223 vs 1.210-1.212 ms (profiles/r2_ab_prefetch.txt)
+        self._pf_args = None
+        if (overlap and not capture and indices is None and self.data8 is None and self.tgt is None
+                and os.environ.get("PZ_PREFETCH", "0") == "1" and not self._launch_bound(batch)
+                and epoch + 1 < self.costs.numel()):
+            self._pf_args = (epoch + 1, 1 - self.parity, batch)
         if self.tgt is not None:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
