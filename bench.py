@@ -266,8 +266,8 @@ def main(argv=None) -> int:
 
     costs = [c for _, c, _, _ in trainer.drain()]
     _emit(args, cfg, world, elapsed, costs, batch, ctx)
-    if dist.is_initialized():
-        dist.destroy_process_group()
+    from penr_oz_neural_network_torch_amd.parallel import shutdown
+    shutdown()  # the native RCCL communicator, then the process group
     return 0
 
 

@@ -1,0 +1,196 @@
+// N8 — the data-parallel communicator: RCCL driven directly from this extension (SURVEY §2.5,
+// §5.8). One communicator per process/GPU (one rank per GPU), its collectives on a comm stream
+// owned here (normal priority by default: a high-priority stream measured 1.7x slower steps),
+// fenced to the compute stream with HIP events:
+//
+//   rccl_all_reduce(h, t)  current stream --event--> comm stream: ncclAllReduce(t, SUM, in place)
+//                          --event[ticket]-->  (returns the ticket)
+//   rccl_wait(h, ticket)   the CURRENT stream waits for that bucket (no host blocking) — the
+//                          optimizer side stream waits for exactly the buckets it updates
+//
+// so a layer's gradient bucket crosses xGMI while the following layers' backward GEMMs run, and
+// nothing but stream waits orders the update behind it (the ordering ProcessGroupNCCL's
+// Work::wait() only implies). The RCCL entry points are resolved from the librccl that
+// torch already mapped (same SONAME), so one RCCL runtime serves both.
+#include <ATen/ATen.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <c10/hip/HIPStream.h>
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+#include <torch/library.h>
+
+#include <array>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <vector>
+
+namespace {
+
+struct Api {
+  ncclResult_t (*get_unique_id)(ncclUniqueId*);
+  ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int);
+  ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*destroy)(ncclComm_t);
+  ncclResult_t (*async_error)(ncclComm_t, ncclResult_t*);
+  const char* (*error_string)(ncclResult_t);
+};
+
+template <typename F>
+void resolve(void* lib, const char* name, F& fn) {
+  fn = reinterpret_cast<F>(dlsym(lib, name));
+  TORCH_CHECK(fn != nullptr, "pz rccl: ", name, " not found in librccl");
+}
+
+const Api& api() {
+  static const Api a = [] {
+    void* lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);  // torch's copy, already mapped
+    if (lib == nullptr) lib = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (lib == nullptr) lib = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    TORCH_CHECK(lib != nullptr, "pz rccl: cannot load librccl: ", dlerror());
+    Api x{};
+    resolve(lib, "ncclGetUniqueId", x.get_unique_id);
+    resolve(lib, "ncclCommInitRank", x.init_rank);
+    resolve(lib, "ncclAllReduce", x.all_reduce);
+    resolve(lib, "ncclCommDestroy", x.destroy);
+    resolve(lib, "ncclCommGetAsyncError", x.async_error);
+    resolve(lib, "ncclGetErrorString", x.error_string);
+    return x;
+  }();
+  return a;
+}
+
+#define PZ_NCCL_CHECK(expr)                                                                 \
+  do {                                                                                      \
+    const ncclResult_t r_ = (expr);                                                         \
+    TORCH_CHECK(r_ == ncclSuccess, "pz rccl: ", #expr, " failed: ", api().error_string(r_)); \
+  } while (0)
+#define PZ_HIP_OK(expr)                                                                      \
+  do {                                                                                       \
+    const hipError_t e_ = (expr);                                                            \
+    TORCH_CHECK(e_ == hipSuccess, "pz rccl: ", #expr, " failed: ", hipGetErrorString(e_));   \
+  } while (0)
+
+// a bucket's completion event is reused after kRing later buckets: the trainer waits for every
+// bucket within the step that issued it (at most a few per layer)
+constexpr int kRing = 256;
+
+struct Comm {
+  ncclComm_t comm = nullptr;
+  int device = 0;
+  int nranks = 1;
+  c10::hip::HIPStream stream;
+  hipEvent_t ready = nullptr;
+  std::array<hipEvent_t, kRing> done{};
+  int64_t next = 0;
+  explicit Comm(c10::hip::HIPStream s) : stream(s) {}
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<Comm>> g_comms;
+
+Comm& get(int64_t h) {
+  std::lock_guard<std::mutex> lock(g_mu);
+  TORCH_CHECK(h >= 0 && h < static_cast<int64_t>(g_comms.size()) && g_comms[h], "pz rccl: bad communicator handle");
+  return *g_comms[h];
+}
+
+ncclDataType_t nccl_type(const at::Tensor& t) {
+  switch (t.scalar_type()) {
+    case at::kFloat: return ncclFloat32;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kDouble: return ncclFloat64;
+    case at::kHalf: return ncclFloat16;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    default: TORCH_CHECK(false, "pz rccl: unsupported dtype ", t.scalar_type());
+  }
+}
+
+at::Tensor unique_id_op() {
+  ncclUniqueId id;
+  PZ_NCCL_CHECK(api().get_unique_id(&id));
+  at::Tensor out = at::empty({static_cast<int64_t>(sizeof(id))}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(out.data_ptr(), &id, sizeof(id));
+  return out;
+}
+
+int64_t init_op(const at::Tensor& id, int64_t nranks, int64_t rank, bool high_priority) {
+  TORCH_CHECK(id.device().is_cpu() && id.scalar_type() == at::kByte && id.numel() == sizeof(ncclUniqueId),
+              "pz rccl: the unique id is ", sizeof(ncclUniqueId), " CPU bytes");
+  TORCH_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "pz rccl: rank ", rank, " of ", nranks);
+  ncclUniqueId uid;
+  std::memcpy(&uid, id.contiguous().data_ptr(), sizeof(uid));
+  int dev = 0;
+  PZ_HIP_OK(hipGetDevice(&dev));
+  auto c = std::make_unique<Comm>(c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(dev)));
+  c->device = dev;
+  c->nranks = static_cast<int>(nranks);
+  PZ_NCCL_CHECK(api().init_rank(&c->comm, static_cast<int>(nranks), uid, static_cast<int>(rank)));
+  PZ_HIP_OK(hipEventCreateWithFlags(&c->ready, hipEventDisableTiming));
+  for (auto& e : c->done) PZ_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_comms.push_back(std::move(c));
+  return static_cast<int64_t>(g_comms.size()) - 1;
+}
+
+int64_t all_reduce_op(int64_t h, const at::Tensor& t) {
+  Comm& c = get(h);
+  TORCH_CHECK(t.is_cuda() && t.device().index() == c.device, "pz rccl: tensor must live on the communicator's GPU");
+  TORCH_CHECK(t.is_contiguous(), "pz rccl: contiguous buckets only");
+  const int64_t ticket = c.next++;
+  if (t.numel() == 0) {
+    PZ_HIP_OK(hipEventRecord(c.done[ticket % kRing], c10::hip::getCurrentHIPStream(c.device).stream()));
+    return ticket;
+  }
+  const hipStream_t cur = c10::hip::getCurrentHIPStream(c.device).stream();
+  PZ_HIP_OK(hipEventRecord(c.ready, cur));
+  PZ_HIP_OK(hipStreamWaitEvent(c.stream.stream(), c.ready, 0));
+  PZ_NCCL_CHECK(api().all_reduce(t.data_ptr(), t.data_ptr(), static_cast<size_t>(t.numel()), nccl_type(t), ncclSum,
+                                 c.comm, c.stream.stream()));
+  // the caching allocator must not hand the bucket's memory out again before the comm stream is done
+  c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), c.stream);
+  PZ_HIP_OK(hipEventRecord(c.done[ticket % kRing], c.stream.stream()));
+  return ticket;
+}
+
+void wait_op(int64_t h, int64_t ticket) {
+  Comm& c = get(h);
+  TORCH_CHECK(ticket >= 0 && ticket < c.next && c.next - ticket <= kRing, "pz rccl: stale or unknown bucket ticket");
+  ncclResult_t async = ncclSuccess;
+  PZ_NCCL_CHECK(api().async_error(c.comm, &async));
+  TORCH_CHECK(async == ncclSuccess || async == ncclInProgress, "pz rccl: communicator failed: ",
+              api().error_string(async));
+  PZ_HIP_OK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream(c.device).stream(), c.done[ticket % kRing], 0));
+}
+
+void destroy_op(int64_t h) {
+  std::unique_ptr<Comm> c;
+  {
+    std::lock_guard<std::mutex> lock(g_mu);
+    TORCH_CHECK(h >= 0 && h < static_cast<int64_t>(g_comms.size()) && g_comms[h], "pz rccl: bad communicator handle");
+    c = std::move(g_comms[h]);
+  }
+  PZ_HIP_OK(hipStreamSynchronize(c->stream.stream()));
+  PZ_NCCL_CHECK(api().destroy(c->comm));
+  hipEventDestroy(c->ready);
+  for (auto& e : c->done) hipEventDestroy(e);
+}
+
+}  // namespace
+
+TORCH_LIBRARY_FRAGMENT(pz, m) {
+  m.def("rccl_unique_id() -> Tensor");
+  m.def("rccl_init(Tensor uid, int nranks, int rank, bool high_priority) -> int");
+  m.def("rccl_all_reduce(int comm, Tensor(a!) t) -> int");
+  m.def("rccl_wait(int comm, int ticket) -> ()");
+  m.def("rccl_destroy(int comm) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(pz, CompositeExplicitAutograd, m) {
+  m.impl("rccl_unique_id", TORCH_FN(unique_id_op));
+  m.impl("rccl_init", TORCH_FN(init_op));
+  m.impl("rccl_all_reduce", TORCH_FN(all_reduce_op));
+  m.impl("rccl_wait", TORCH_FN(wait_op));
+  m.impl("rccl_destroy", TORCH_FN(destroy_op));
+}

@@ -1,13 +1,17 @@
 """Data parallelism over RCCL / xGMI (absent in the reference).
 
-One process per GPU, ``torch.distributed`` with the ``nccl`` backend (= RCCL on ROCm). Every rank
-holds a full parameter replica in one flat buffer (:mod:`..engine.params`); the global minibatch
-is sharded over ranks; gradients are summed with bucketed all-reduces that are *issued during
-backward*: the fused trainer calls :meth:`DataParallelContext.all_reduce_async` right after each
-layer's dW GEMM is enqueued. ProcessGroupNCCL runs the collective on its own HIP stream that waits
-on the compute stream at issue time, so layer L's gradient travels over xGMI while layers L-1 ...
-0 are still computing; :meth:`wait_all` only inserts stream waits (no host blocking) before the
-fused optimizer, which folds the 1/world mean into its update.
+One process per GPU. ``torch.distributed`` (``nccl`` = RCCL on ROCm) brings the ranks up
+(rendezvous, parameter broadcast, barriers) and, by default, carries the gradient buckets through
+ProcessGroupNCCL; ``PZ_COMM=native`` moves the buckets to the extension's own RCCL communicator
+(``csrc/rccl_comm.cpp``, N8).
+Every rank holds a full parameter replica in one flat buffer (:mod:`..engine.params`); the global
+minibatch is sharded over ranks; gradients are summed with bucketed all-reduces that are *issued
+during backward*: the fused trainer calls :meth:`DataParallelContext.all_reduce_async` right after
+each layer's dW GEMM is enqueued. The collective runs on the communicator's stream, fenced to the
+compute stream by an event at issue time, so layer L's gradient travels over xGMI while layers
+L-1 ... 0 are still computing; :meth:`wait_one` only makes the CURRENT stream (the optimizer's)
+wait for that bucket's completion event (no host blocking), and the fused optimizer folds the
+1/world mean into its update.
 
 The same class runs on ``gloo`` for CPU tests (world_size > 1 without GPUs).
 
@@ -35,6 +39,7 @@ class DataParallelContext:
     # PZ_FORCE_COMM=1: run every collective even at world size 1 (a 1-rank RCCL communicator), so
     # the comm-stream / wait ordering of the data-parallel step is exercised on a single GPU
     force: bool = False
+    native: object = None  # _NativeComm: the extension's RCCL communicator (gradient buckets)
 
     @property
     def enabled(self) -> bool:
@@ -49,11 +54,15 @@ class DataParallelContext:
         (buckets that carry the loss or small accumulated parameters)."""
         if not self.enabled or t.numel() == 0:
             return None
+        low = None
         if not exact and self.comm_dtype is not None and t.dtype != self.comm_dtype:
             low = t.to(self.comm_dtype)
-            work = dist.all_reduce(low, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
-            return (work, low, t)
-        return (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True), None, None)
+        buf = t if low is None else low
+        if self.native is not None:
+            work = self.native.all_reduce(buf)
+        else:
+            work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        return (work, low, t if low is not None else None)
 
     def all_reduce_(self, t: torch.Tensor) -> None:
         """Blocking exact SUM all-reduce in place (stream-ordered under RCCL): the synchronised
@@ -95,6 +104,47 @@ class DataParallelContext:
             dist.barrier(group=self.group)
 
 
+class _Ticket:
+    """One bucket in flight on the native communicator: ``wait()`` makes the current stream wait."""
+    __slots__ = ("comm", "ticket")
+
+    def __init__(self, comm: int, ticket: int):
+        self.comm, self.ticket = comm, ticket
+
+    def wait(self) -> None:
+        torch.ops.pz.rccl_wait(self.comm, self.ticket)
+
+
+class _NativeComm:
+    """The extension's RCCL communicator (``csrc/rccl_comm.cpp``): rank 0's unique id travels over
+    the already initialised process group, then every rank joins with ncclCommInitRank on its GPU.
+    A sum of ``rank + 1`` over the new communicator checks it before any gradient goes through."""
+
+    def __init__(self, rank: int, world: int, group=None):
+        from ..ops import native
+        native.require()
+        dev = torch.device("cuda", torch.cuda.current_device())
+        uid = torch.ops.pz.rccl_unique_id() if rank == 0 else torch.zeros(128, dtype=torch.uint8)
+        uid_dev = uid.to(dev)
+        dist.broadcast(uid_dev, src=0, group=group)
+        # comm stream at NORMAL priority (PZ_COMM_PRIO=1: high): a high-priority stream slowed every
+        # compute kernel of the forced 1-rank step (2.44 vs 1.40 ms/step, profiles/r2_ab_native_comm.txt)
+        self.handle = torch.ops.pz.rccl_init(uid_dev.cpu(), world, rank, os.environ.get("PZ_COMM_PRIO", "0") == "1")
+        probe = torch.full((1,), float(rank + 1), device=dev, dtype=torch.float64)
+        self.all_reduce(probe).wait()
+        got, want = probe.item(), world * (world + 1) / 2
+        if got != want:
+            raise RuntimeError(f"pz rccl communicator self-check failed: sum {got}, expected {want}")
+
+    def all_reduce(self, t: torch.Tensor) -> _Ticket:
+        return _Ticket(self.handle, torch.ops.pz.rccl_all_reduce(self.handle, t))
+
+    def close(self) -> None:
+        if self.handle is not None:
+            torch.ops.pz.rccl_destroy(self.handle)
+            self.handle = None
+
+
 _CONTEXT: DataParallelContext | None = None
 
 
@@ -134,6 +184,12 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
     comm_dtype = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": None, None: None}.get(comm)
     if dist.is_initialized():
         _CONTEXT = DataParallelContext(dist.get_rank(), dist.get_world_size(), None, comm_dtype, force=force)
+        # PZ_COMM=native: gradient buckets on the extension's own RCCL communicator instead of
+        # ProcessGroupNCCL. Opt-in: with the same bucket schedule it measured 1.8% slower on the
+        # forced 1-rank step (1.390-1.396 vs 1.366-1.373 ms, profiles/r2_ab_native_comm.txt), and
+        # the multi-GPU node runs are the driver's, not ours to A/B
+        if dist.get_backend() == "nccl" and os.environ.get("PZ_COMM", "torch") == "native":
+            _CONTEXT.native = _NativeComm(_CONTEXT.rank, _CONTEXT.world_size)
     else:
         _CONTEXT = DataParallelContext(0, 1, None, comm_dtype)
     return _CONTEXT
@@ -156,6 +212,10 @@ def set_context(ctx: DataParallelContext | None) -> None:
 
 def shutdown() -> None:
     global _CONTEXT
+    if _CONTEXT is not None and _CONTEXT.native is not None:
+        torch.cuda.synchronize()
+        _CONTEXT.native.close()
+        _CONTEXT.native = None
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _CONTEXT = None

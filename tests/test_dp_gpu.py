@@ -129,10 +129,10 @@ def test_multi_rank_step_equals_single_rank(tmp_path, monkeypatch, world, optimi
                 torch.testing.assert_close(v, wv, rtol=1e-4, atol=1e-5)
 
 
-def _forced_main(rank, comm, out_path):
+def _forced_main(rank, comm, out_path, impl="native"):
     """World size 1 with PZ_FORCE_COMM=1: every gradient bucket goes through a real 1-rank RCCL
     all-reduce on its comm stream, waited for by the optimizer's stream."""
-    os.environ.update(PZ_FORCE_COMM="1", PZ_GRAD_COMM_DTYPE=comm, MASTER_ADDR="127.0.0.1",
+    os.environ.update(PZ_FORCE_COMM="1", PZ_GRAD_COMM_DTYPE=comm, PZ_COMM=impl, MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(_free_port()))
     if comm == "fp32":  # unchunked first-layer dW (chunks change the split-K choice = rounding)
         os.environ["PZ_DW_CHUNKS"] = "1"
@@ -141,6 +141,8 @@ def _forced_main(rank, comm, out_path):
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
     ctx = init_from_env()
     assert ctx.force and ctx.enabled and ctx.world_size == 1 and ctx.backend == "nccl", ctx
+    # gradient buckets on the extension's RCCL communicator (csrc/rccl_comm.cpp) or ProcessGroupNCCL
+    assert (ctx.native is not None) == (impl == "native"), ctx
     model = _build("adam", "bf16")
     tr = FusedTrainer(model, ctx)
     assert bool(tr.grads16) == (comm == "bf16")
@@ -154,10 +156,10 @@ def _forced_main(rank, comm, out_path):
     shutdown()
 
 
-@pytest.mark.parametrize("comm", ["fp32", "bf16"])
-def test_forced_rccl_world1_matches_no_comm(tmp_path, monkeypatch, comm):
+@pytest.mark.parametrize("comm,impl", [("fp32", "native"), ("bf16", "native"), ("fp32", "torch")])
+def test_forced_rccl_world1_matches_no_comm(tmp_path, monkeypatch, comm, impl):
     out = str(tmp_path / "forced.pt")
-    mp.start_processes(_forced_main, args=(comm, out), nprocs=1, start_method="spawn")
+    mp.start_processes(_forced_main, args=(comm, out, impl), nprocs=1, start_method="spawn")
     got = torch.load(out, weights_only=True)
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
@@ -208,3 +210,26 @@ def test_bench_launches_its_own_ranks(tmp_path):
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1"],
                        capture_output=True, text=True, timeout=300, env=dict(env, WORLD_SIZE="1"), cwd=str(tmp_path))
     assert r.returncode != 0 and "process group holds 1" in r.stderr
+
+
+def test_native_rccl_communicator_world1(native_lib):
+    """csrc/rccl_comm.cpp on one GPU: a 1-rank communicator sums in place (identity), a bucket's
+    ticket orders ANOTHER stream behind the collective, stale tickets are refused."""
+    uid = native_lib.rccl_unique_id()
+    assert uid.dtype == torch.uint8 and uid.numel() == 128
+    h = native_lib.rccl_init(uid, 1, 0, True)
+    try:
+        side = torch.cuda.Stream()
+        for dt in (torch.float32, torch.bfloat16, torch.float64):
+            x = torch.randn(1 << 20, device="cuda").to(dt)
+            ref = x.clone()
+            ticket = native_lib.rccl_all_reduce(h, x)
+            with torch.cuda.stream(side):
+                native_lib.rccl_wait(h, ticket)
+                y = x * 2
+            torch.cuda.synchronize()
+            assert torch.equal(x, ref) and torch.equal(y, ref * 2)
+        with pytest.raises(RuntimeError):
+            native_lib.rccl_wait(h, 10 ** 6)
+    finally:
+        native_lib.rccl_destroy(h)
