@@ -120,10 +120,11 @@ class _NativeComm:
     the already initialised process group, then every rank joins with ncclCommInitRank on its GPU.
     A sum of ``rank + 1`` over the new communicator checks it before any gradient goes through."""
 
-    def __init__(self, rank: int, world: int, group=None):
-        from ..ops import native
-        native.require()
-        dev = torch.device("cuda", torch.cuda.current_device())
+    def __init__(self, rank: int, world: int, group=None, device: torch.device | None = None):
+        if device is None:
+            from ..ops import native
+            native.require()
+        dev = device or torch.device("cuda", torch.cuda.current_device())
         uid = torch.ops.pz.rccl_unique_id() if rank == 0 else torch.zeros(128, dtype=torch.uint8)
         uid_dev = uid.to(dev)
         dist.broadcast(uid_dev, src=0, group=group)
@@ -213,7 +214,8 @@ def set_context(ctx: DataParallelContext | None) -> None:
 def shutdown() -> None:
     global _CONTEXT
     if _CONTEXT is not None and _CONTEXT.native is not None:
-        torch.cuda.synchronize()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
         _CONTEXT.native.close()
         _CONTEXT.native = None
     if dist.is_available() and dist.is_initialized():

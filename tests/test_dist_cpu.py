@@ -111,3 +111,73 @@ def test_gloo_data_parallel_training_equals_single_process(tmp_path, world, opti
         for (m, v), (wm, wv) in zip(stats, want):
             torch.testing.assert_close(m, wm, rtol=tol, atol=tol * 1e-2)
             torch.testing.assert_close(v, wv, rtol=tol, atol=tol * 1e-2)
+
+
+def _native_rank(rank, world, port, out_dir):
+    """The native-communicator plumbing of parallel/dist.py (unique-id broadcast from rank 0, init
+    self-check, bucket tickets, reduced-precision buckets, shutdown) over gloo, with the RCCL ops of
+    csrc/rccl_comm.cpp stood in by host all-reduces (the GPU tier runs the real ones)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    from penr_oz_neural_network_torch_amd.parallel import dist as pd
+    from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
+    log = {"init": [], "reduced": 0, "waited": [], "closed": []}
+
+    class FakeOps:
+        @staticmethod
+        def rccl_unique_id():
+            return torch.arange(128, dtype=torch.uint8)
+
+        @staticmethod
+        def rccl_init(uid, nranks, r, high_priority):
+            log["init"].append((uid.tolist(), nranks, r, high_priority))
+            return 7
+
+        @staticmethod
+        def rccl_all_reduce(h, t):
+            dist.all_reduce(t)
+            log["reduced"] += 1
+            return log["reduced"] - 1
+
+        @staticmethod
+        def rccl_wait(h, ticket):
+            log["waited"].append((h, ticket))
+
+        @staticmethod
+        def rccl_destroy(h):
+            log["closed"].append(h)
+
+    class FakeTorch:  # torch with the pz namespace swapped
+        ops = type("ops", (), {"pz": FakeOps})
+
+        def __getattr__(self, name):
+            return getattr(torch, name)
+
+    pd.torch = FakeTorch()
+    ctx = init_from_env("gloo")
+    ctx.native = pd._NativeComm(rank, world, device=torch.device("cpu"))
+    flat = torch.arange(100, dtype=torch.float32) * (rank + 1)
+    handles = [ctx.all_reduce_async(flat[50:]), ctx.all_reduce_async(flat[:50])]
+    assert all(isinstance(h[0], pd._Ticket) for h in handles)
+    ctx.wait_all(handles)
+    ctx.comm_dtype = torch.bfloat16
+    g = torch.full((8,), 0.5 * (rank + 1))
+    ctx.all_reduce_(g)  # exact: stays fp32
+    g2 = torch.full((8,), 0.25 * (rank + 1))
+    ctx.wait_one(ctx.all_reduce_async(g2))  # through a bf16 copy
+    shutdown()
+    pd.torch = torch
+    torch.save({"flat": flat, "g": g, "g2": g2, "log": log}, os.path.join(out_dir, f"n{rank}.pt"))
+
+
+def test_native_communicator_plumbing_two_ranks(tmp_path):
+    mp.start_processes(_native_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, start_method="spawn")
+    for r in range(2):
+        got = torch.load(tmp_path / f"n{r}.pt", weights_only=True)
+        assert torch.equal(got["flat"], torch.arange(100, dtype=torch.float32) * 3)
+        assert torch.equal(got["g"], torch.full((8,), 1.5)) and torch.equal(got["g2"], torch.full((8,), 0.75))
+        log = got["log"]
+        # rank 0's id reached both ranks; normal-priority comm stream; self-check + 4 buckets; closed
+        assert log["init"] == [(list(range(128)), 2, r, False)]
+        assert log["reduced"] == 5 and [t for _, t in log["waited"]] == [0, 1, 2, 3, 4]
+        assert log["closed"] == [7]
