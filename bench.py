@@ -78,14 +78,13 @@ def _launch_ranks(n: int, argv: list[str]) -> int:
     """Start ``n`` rank processes of this script and wait for them (this process never
     initialises the GPU: ``device_count`` does not, on this ROCm build)."""
     import signal
-    import socket
     import subprocess
+    import tempfile
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(n),
-               LOCAL_WORLD_SIZE=str(n), PZ_BENCH_LAUNCHER="self")
+    # file rendezvous: a port picked here could be taken by someone else before rank 0 listens
+    rdv_dir = tempfile.mkdtemp(prefix="pz_rdv_")
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1", PZ_RENDEZVOUS_FILE=os.path.join(rdv_dir, "store"),
+               WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n), PZ_BENCH_LAUNCHER="self")
     visible = torch.cuda.device_count()
     if visible < n and "PZ_DIST_BACKEND" not in os.environ:
         log(f"{visible} GPU(s) visible for {n} ranks: rehearsing over gloo with ranks sharing GPUs")
@@ -108,6 +107,8 @@ def _launch_ranks(n: int, argv: list[str]) -> int:
                 for q in alive:  # our own children only, by exact pid
                     q.send_signal(signal.SIGTERM)
         time.sleep(0.05)
+    import shutil
+    shutil.rmtree(rdv_dir, ignore_errors=True)
     return rc
 
 

@@ -180,7 +180,12 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
             # node; the REST layer then persists status "Failed" 
             os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         timeout = timedelta(seconds=float(os.environ.get("PZ_DIST_TIMEOUT_S", "600")))
-        dist.init_process_group(backend=backend, timeout=timeout)
+        rdv = os.environ.get("PZ_RENDEZVOUS_FILE")
+        if rdv:  # a shared-file store: no TCP port to pick ahead of the ranks (and lose in a race)
+            dist.init_process_group(backend=backend, init_method=f"file://{rdv}", timeout=timeout,
+                                    rank=int(os.environ.get("RANK", "0")), world_size=world)
+        else:
+            dist.init_process_group(backend=backend, timeout=timeout)
     comm = os.environ.get("PZ_GRAD_COMM_DTYPE")
     comm_dtype = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": None, None: None}.get(comm)
     if dist.is_initialized():

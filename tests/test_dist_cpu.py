@@ -14,7 +14,7 @@ def _free_port() -> int:
 
 
 def _worker(rank, world, port, out_dir):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+    os.environ.update(PZ_RENDEZVOUS_FILE=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
     ctx = init_from_env("gloo")
@@ -39,7 +39,7 @@ def _worker(rank, world, port, out_dir):
 
 
 def test_gloo_two_rank_communicator(tmp_path):
-    mp.start_processes(_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, start_method="spawn")
+    mp.start_processes(_worker, args=(2, str(tmp_path / "rdv"), str(tmp_path)), nprocs=2, start_method="spawn")
     expect = torch.arange(1000, dtype=torch.float32) * 3
     for r in range(2):
         got = torch.load(tmp_path / f"r{r}.pt", weights_only=True)
@@ -50,7 +50,7 @@ def test_gloo_two_rank_communicator(tmp_path):
 
 
 def _train_rank(rank, world, port, optimizer, out_dir, bn=False):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+    os.environ.update(PZ_RENDEZVOUS_FILE=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     torch.set_num_threads(1)
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
@@ -90,7 +90,7 @@ def test_gloo_data_parallel_training_equals_single_process(tmp_path, world, opti
     """CPU data parallelism (reference fp64 path): W ranks x 32/W samples == 1 process x 32, to
     fp64 rounding — at world 8 too, and for batchnorm models, whose statistics are synchronised
     over the ranks (every rank ends with the single process's running mean / variance)."""
-    mp.start_processes(_train_rank, args=(world, _free_port(), optimizer, str(tmp_path), bn), nprocs=world,
+    mp.start_processes(_train_rank, args=(world, str(tmp_path / "rdv"), optimizer, str(tmp_path), bn), nprocs=world,
                        start_method="spawn")
     dp = torch.load(tmp_path / "dp.pt", weights_only=True)
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
@@ -117,7 +117,7 @@ def _native_rank(rank, world, port, out_dir):
     """The native-communicator plumbing of parallel/dist.py (unique-id broadcast from rank 0, init
     self-check, bucket tickets, reduced-precision buckets, shutdown) over gloo, with the RCCL ops of
     csrc/rccl_comm.cpp stood in by host all-reduces (the GPU tier runs the real ones)."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+    os.environ.update(PZ_RENDEZVOUS_FILE=str(port), RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_RANK=str(rank))
     from penr_oz_neural_network_torch_amd.parallel import dist as pd
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
@@ -171,7 +171,7 @@ def _native_rank(rank, world, port, out_dir):
 
 
 def test_native_communicator_plumbing_two_ranks(tmp_path):
-    mp.start_processes(_native_rank, args=(2, _free_port(), str(tmp_path)), nprocs=2, start_method="spawn")
+    mp.start_processes(_native_rank, args=(2, str(tmp_path / "rdv"), str(tmp_path)), nprocs=2, start_method="spawn")
     for r in range(2):
         got = torch.load(tmp_path / f"n{r}.pt", weights_only=True)
         assert torch.equal(got["flat"], torch.arange(100, dtype=torch.float32) * 3)

@@ -51,10 +51,10 @@ def _bn_stats(model):
 
 
 def _rank_main(rank, world, port, optimizer, comm, out_path, bn=False):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
-                      PZ_GRAD_COMM_DTYPE=comm)
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), PZ_GRAD_COMM_DTYPE=comm)
     torch.set_num_threads(2)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # file rendezvous (port = the store path): no TCP port picked ahead of the spawned ranks
+    dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
     model = _build(optimizer, comm, bn)
@@ -92,7 +92,7 @@ def test_multi_rank_step_equals_single_rank(tmp_path, monkeypatch, world, optimi
     box's GPU over gloo; the code path is the RCCL one). Batchnorm statistics are synchronised:
     every rank ends with the single rank's running mean / variance."""
     out = str(tmp_path / "dp.pt")
-    mp.start_processes(_rank_main, args=(world, _free_port(), optimizer, comm, out, bn), nprocs=world,
+    mp.start_processes(_rank_main, args=(world, str(tmp_path / "rdv"), optimizer, comm, out, bn), nprocs=world,
                        start_method="spawn")
     ranks = [torch.load(out + f".{r}", weights_only=True) for r in range(world)]
     dp = ranks[0]
