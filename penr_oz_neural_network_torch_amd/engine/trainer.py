@@ -293,6 +293,14 @@ class FusedTrainer:
             sizes = {st.seg_w.offset: st.seg_w.numel for st in self.stages if st.kind == "gemm"}
             self._trickle_key = max(gemm_w[1:], key=lambda k: sizes[k])
         self._side_pending: list = []
+        # PZ_OPT_DEFER=1: the largest side-updated weight is updated only after the first-layer /
+        # bias launch, so that launch (on the critical path) gets the HBM to itself. Off: the next
+        # fwd_L1 then runs beside that update at ~175 instead of ~95 us (mlp4 1.251-1.254 vs
+        # 1.229-1.232 ms, profiles/r2_ab_opt_defer.txt)
+        self._defer = os.environ.get("PZ_OPT_DEFER", "0") == "1" and len(gemm_w) > 1
+        sizes = {st.seg_w.offset: st.seg_w.numel for st in self.stages if st.kind == "gemm"}
+        self._defer_key = max(gemm_w[1:], key=lambda k: sizes[k]) if self._defer else None
+        self._deferred: list = []
         self._pf_args = None       # (epoch, parity, batch) of the sample _prefetch gathers next
         self._pf_ready = None      # ((epoch, parity, batch, data id), event) of a gathered sample
         self.prefetched_steps = 0  # steps that consumed a prefetched sample
@@ -824,6 +832,14 @@ class FusedTrainer:
             rest_ev.record(main)
             with torch.cuda.stream(self.opt_stream):
                 self.opt_stream.wait_event(rest_ev)
+                for key, hs, stages in self._deferred:  # PZ_OPT_DEFER
+                    for h in hs:
+                        self.ctx.wait_one(h)
+                    self.opt.step_group(key, self.grads, l2, 1.0 / world, 1 - self.parity)
+                    if self.fp8:
+                        for st in stages:
+                            self._refresh_fp8_weights(st, 1 - self.parity)
+                self._deferred = []
                 self.opt.finalize(self.loss_slot, world, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
                 ev = torch.cuda.Event(enable_timing=not capture)
@@ -1047,8 +1063,9 @@ class FusedTrainer:
             self._opt_async([(st.seg_w.offset, mine, [st])], self._trickle if trickle else 0)
         out = self._backward_dx(st, before, g, batch, p, keys, rec)
         if self._ov is not None and own and not early and not trickle:
-            self._side_pending.append((st.seg_w.offset, mine, [st]))
-            if not self._merge_side or st.seg_w.offset == self._flush_key:
+            item = (st.seg_w.offset, mine, [st])
+            (self._deferred if st.seg_w.offset == self._defer_key else self._side_pending).append(item)
+            if (not self._merge_side or st.seg_w.offset == self._flush_key) and self._side_pending:
                 self._opt_async(self._side_pending)
                 self._side_pending = []
         return out
