@@ -47,6 +47,7 @@ def main():
         ("dXL3_mask", B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask"),
         # one dropout instead of two in front of the ReLU mask (the hashing's share of the epilogue)
         ("fwdL1_mask1", B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask1"),
+        ("fwdL1_mask0", B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask0"),  # ReLU + mask, no dropout
         ("fwdL2_mask1", B, 4096, 4096, True, False, torch.bfloat16, "fwd_mask1"),
         ("dXL3_mask_nocs", B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask_nocs"),
         ("dXL2_mask", B, 4096, 4096, True, True, torch.bfloat16, "bwd_mask"),
@@ -90,6 +91,9 @@ def main():
         elif mode == "fwd_mask1":
             e1 = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, p=0.36, seed=(1, 2))
             fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=e1, mask=mask)
+        elif mode == "fwd_mask0":
+            e0 = PF.epi_spec(act=PF.ACT_RELU)
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=e0, mask=mask)
         elif mode == "bwd_mask":
             fused = lambda: PF.gemm(a, akc, b, bkc, c, colsum=colsum, mode=PF.EPI_BWD, epi=epi, mask=mask)
         elif mode == "bwd_mask_nocs":
