@@ -273,7 +273,11 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       }
     }
     if (!bwd && use_mask) {  // 4 neighbouring chunks of a row -> one 4-byte store (not 4 byte stores)
-      const uint32_t b1 = __shfl_down(byte, 1, 64), b2 = __shfl_down(byte, 2, 64), b3 = __shfl_down(byte, 3, 64);
+      // the 4 chunks are one DPP quad (lane % 4 == chunk % 4): quad_perm broadcasts of lanes 1..3
+      // (full-rate VALU) instead of ds_bpermute round trips through the LDS the image reads use
+      const uint32_t b1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0x55, 0xF, 0xF, false));
+      const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xAA, 0xF, 0xF, false));
+      const uint32_t b3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xFF, 0xF, 0xF, false));
       if (in_range && (my_chunk & 3) == 0)
         *reinterpret_cast<uint32_t*>(p.mask + static_cast<int64_t>(gm) * p.ldmask + gn / 8) =
             byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
