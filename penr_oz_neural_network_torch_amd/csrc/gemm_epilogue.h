@@ -75,6 +75,25 @@ PZ_DEV void dropout_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, uint32_t key, u
   }
 }
 
+// dropout -> ReLU -> dropout (every hidden ReLU stage of the reference MLPs): the scale is
+// positive, so relu(z * m1 * s) * m2 * s = (m1 & m2) ? relu(z) * s^2 : 0 — both keep decisions are
+// combined before ONE select and multiply per element (the backward applies the same s^2)
+template <class L>
+PZ_DEV void dropout_relu_dropout_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, uint32_t pr_row) {
+  const uint32_t th = e.thresh16;
+  const float s2 = e.scale * e.scale;
+#pragma unroll
+  for (int j = 0; j < L::COLS; ++j) {
+    const uint32_t pr = pr_row + static_cast<uint32_t>(L::n_off(j) / 2);
+    const uint32_t a0 = mix32(pr ^ e.key_pre), a1 = mix32((pr + 1u) ^ e.key_pre);
+    const uint32_t c0 = mix32(pr ^ e.key_post), c1 = mix32((pr + 1u) ^ e.key_post);
+    const bool k[4] = {(a0 & 0xFFFFu) >= th && (c0 & 0xFFFFu) >= th, (a0 >> 16) >= th && (c0 >> 16) >= th,
+                       (a1 & 0xFFFFu) >= th && (c1 & 0xFFFFu) >= th, (a1 >> 16) >= th && (c1 >> 16) >= th};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[j][r] = k[r] ? fmaxf(v[j][r], 0.f) * s2 : 0.f;
+  }
+}
+
 template <int COLS>
 PZ_DEV void act_fwd_row(f32x4_t (&v)[COLS], int act) {
 #define PZ_ACT_LOOP(expr)                                                       \
@@ -204,9 +223,13 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     for (int j = 0; j < COLS; ++j) v[j] = L::get(acc, i, j) * alpha + bias4[j];
     if (!bwd) {
       if (p.epi_mode == EPI_FWD) {
-        if (e.drop_pre) dropout_row<L>(v, e, e.key_pre, pr_row);
-        if (e.act != ACT_NONE) act_fwd_row<COLS>(v, e.act);
-        if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
+        if (e.drop_pre && e.drop_post && e.act == ACT_RELU && !e.drop_all) {
+          dropout_relu_dropout_row<L>(v, e, pr_row);
+        } else {
+          if (e.drop_pre) dropout_row<L>(v, e, e.key_pre, pr_row);
+          if (e.act != ACT_NONE) act_fwd_row<COLS>(v, e.act);
+          if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
+        }
       }
     } else if (use_mask) {
       // ReLU stage: y > 0  <=>  kept by drop_post AND kept by drop_pre AND z > 0, so the whole
