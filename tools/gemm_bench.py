@@ -48,6 +48,8 @@ def main():
         # one dropout instead of two in front of the ReLU mask (the hashing's share of the epilogue)
         ("fwdL1_mask1", B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask1"),
         ("fwdL1_mask0", B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask0"),  # ReLU + mask, no dropout
+        ("fwdL1_bias", B, 4096, 1024, True, False, torch.bfloat16, "fwd_bias"),
+        ("fwdL1_relu", B, 4096, 1024, True, False, torch.bfloat16, "fwd_relu"),
         ("fwdL2_mask1", B, 4096, 4096, True, False, torch.bfloat16, "fwd_mask1"),
         ("dXL3_mask_nocs", B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask_nocs"),
         ("dXL2_mask", B, 4096, 4096, True, True, torch.bfloat16, "bwd_mask"),
