@@ -251,8 +251,9 @@ def test_fused_dw_update_matches_separate_launches(monkeypatch, optimizer):
         runs[run] = ([c for _, c, _, _ in out], [r for _, _, r, _ in out], gpu._param_store.flat.clone(), state,
                      tr.opt.exp_avg.clone() if tr.opt.adam else None)
     (c0, r0, p0, s0, m0), (c1, r1, p1, s1, m1) = runs["0"], runs["1"]
-    for a, b in zip(c0, c1):
-        assert abs(a - b) < 1e-4 * max(1.0, abs(a)), (c0, c1)
+    cn = runs["0b"][0]
+    for a, b, n in zip(c0, c1, cn):  # within the run-to-run noise of the unfused schedule itself
+        assert abs(a - b) <= 3 * abs(a - n) + 2e-4 * max(1.0, abs(a)), (c0, c1, cn)
     for a, b in zip(r0, r1):
         assert (a is None) == (b is None)
         if a is not None:

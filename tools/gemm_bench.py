@@ -50,6 +50,8 @@ def main():
         ("fwdL1_mask0", B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask0"),  # ReLU + mask, no dropout
         ("fwdL1_bias", B, 4096, 1024, True, False, torch.bfloat16, "fwd_bias"),
         ("fwdL1_relu", B, 4096, 1024, True, False, torch.bfloat16, "fwd_relu"),
+        ("fwdL1_nobias", B, 4096, 1024, True, False, torch.bfloat16, "fwd_nobias"),  # EPI_FWD, nothing enabled
+        ("storeL1_bias", B, 4096, 1024, True, False, torch.bfloat16, "store_bias"),  # EPI_STORE + bias
         ("fwdL2_mask1", B, 4096, 4096, True, False, torch.bfloat16, "fwd_mask1"),
         ("dXL3_mask_nocs", B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask_nocs"),
         ("dXL2_mask", B, 4096, 4096, True, True, torch.bfloat16, "bwd_mask"),
@@ -83,6 +85,10 @@ def main():
                                     epi=PF.epi_spec(drop_pre=3, p=0.2, seed=(1, 2)))
         elif mode == "fwd_bias":
             fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=PF.epi_spec())
+        elif mode == "fwd_nobias":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, mode=PF.EPI_FWD, epi=PF.epi_spec())
+        elif mode == "store_bias":
+            fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias)
         elif mode == "fwd_relu":
             fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=PF.epi_spec(act=PF.ACT_RELU))
         elif mode == "bwd_nodrop":
