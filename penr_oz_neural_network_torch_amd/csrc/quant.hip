@@ -9,6 +9,8 @@
 // is quantised once, quantize_rows, and the minibatch gather copies its e4m3 rows).
 //
 // Scale records are fp32 device arrays {q, s} so no host sync is ever needed.
+#include <cstdlib>
+
 #include "pz_common.h"
 #include "pz_kernels.h"
 
@@ -142,6 +144,57 @@ __global__ void __launch_bounds__(256) quantize_rows_kernel(const T* __restrict_
   if (amax != nullptr) block_amax_commit(m, amax);
 }
 
+// 8 elements per lane: one 16-B (bf16) or two 16-B (fp32) loads, four packed conversions and one
+// 8-B store, one 32-bit row division per 8 elements (the scalar kernel above spends a 64-bit
+// division and four 2-B loads per 4 elements: 18 us for the [8192, 1024] dX operand of mlp8192).
+// Same clamp + conversion per value as to_e4m3 / to_e5m2, so the bytes are identical.
+template <typename T, bool E5M2>
+__global__ void __launch_bounds__(256) quantize_rows8_kernel(const T* __restrict__ x, int64_t ldx, int rows, int cols,
+                                                             uint8_t* __restrict__ out, int64_t ldo,
+                                                             const float* __restrict__ qs, float* amax) {
+  const float q = qs[0];
+  const float lim = E5M2 ? kE5m2Max : kE4m3Max;
+  float m = 0.f;
+  const uint32_t per_row = static_cast<uint32_t>(cols / 8);
+  const uint32_t total = static_cast<uint32_t>(rows) * per_row;
+#pragma unroll 4
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < total; i += gridDim.x * 256u) {
+    const uint32_t r = i / per_row, c = (i - r * per_row) * 8u;
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      const uint4 w = *reinterpret_cast<const uint4*>(x + static_cast<int64_t>(r) * ldx + c);
+      const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { v[2 * e] = bf2f(u[e] & 0xFFFF); v[2 * e + 1] = bf2f(u[e] >> 16); }
+    } else {
+      const float4 a0 = *reinterpret_cast<const float4*>(x + static_cast<int64_t>(r) * ldx + c);
+      const float4 a1 = *reinterpret_cast<const float4*>(x + static_cast<int64_t>(r) * ldx + c + 4);
+      v[0] = a0.x; v[1] = a0.y; v[2] = a0.z; v[3] = a0.w; v[4] = a1.x; v[5] = a1.y; v[6] = a1.z; v[7] = a1.w;
+    }
+    uint32_t w2[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float cl[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        m = fmaxf(m, fabsf(v[4 * h + e]));
+        cl[e] = fminf(fmaxf(v[4 * h + e] * q, -lim), lim);
+      }
+      int pk;
+      if constexpr (E5M2) {
+        pk = __builtin_amdgcn_cvt_pk_bf8_f32(cl[0], cl[1], 0, false);
+        pk = __builtin_amdgcn_cvt_pk_bf8_f32(cl[2], cl[3], pk, true);
+      } else {
+        pk = __builtin_amdgcn_cvt_pk_fp8_f32(cl[0], cl[1], 0, false);
+        pk = __builtin_amdgcn_cvt_pk_fp8_f32(cl[2], cl[3], pk, true);
+      }
+      w2[h] = static_cast<uint32_t>(pk);
+    }
+    *reinterpret_cast<uint2*>(out + static_cast<int64_t>(r) * ldo + c) = make_uint2(w2[0], w2[1]);
+  }
+  if (amax != nullptr) block_amax_commit(m, amax);
+}
+
 int grid_for(int64_t work, int per_block = 256, int cap = 4096) {
   const int64_t g = (work + per_block - 1) / per_block;
   return static_cast<int>(g < 1 ? 1 : (g > cap ? cap : g));
@@ -179,6 +232,26 @@ hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* o
 template <bool E5M2>
 hipError_t quantize_rows_fmt(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
                              const float* qs, float* amax, hipStream_t s) {
+  const int esz = dtype == DT_BF16 ? 2 : 4;
+  const bool vec8 = (dtype == DT_BF16 || dtype == DT_F32) && cols % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0 &&
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0 &&
+                    static_cast<int64_t>(rows) * (cols / 8) < (int64_t(1) << 31) && esz > 0;
+  if (vec8) {
+    // block cap (PZ_QUANT_GRID): the per-block amax atomics hit one address and serialise, so
+    // fewer, longer-lived blocks; see profiles/r2_ab_quant_grid.txt
+    static const int cap = [] {
+      const char* e = getenv("PZ_QUANT_GRID");
+      return e != nullptr ? atoi(e) : 256;
+    }();
+    const int g8 = grid_for(static_cast<int64_t>(rows) * (cols / 8), 256 * 4, cap > 0 ? cap : 256);
+    if (dtype == DT_BF16)
+      hipLaunchKernelGGL((quantize_rows8_kernel<uint16_t, E5M2>), dim3(g8), dim3(256), 0, s,
+                         static_cast<const uint16_t*>(x), ldx, rows, cols, out, ldo, qs, amax);
+    else
+      hipLaunchKernelGGL((quantize_rows8_kernel<float, E5M2>), dim3(g8), dim3(256), 0, s, static_cast<const float*>(x),
+                         ldx, rows, cols, out, ldo, qs, amax);
+    return hipGetLastError();
+  }
   const int g = grid_for(static_cast<int64_t>(rows) * (cols / 4), 256 * 8, 1024);
   if (dtype == DT_BF16)
     hipLaunchKernelGGL((quantize_rows_kernel<uint16_t, E5M2>), dim3(g), dim3(256), 0, s,

@@ -446,3 +446,21 @@ def test_gemm_fp8_split_k(native_lib):
     PF.gemm(x8, True, w8, True, y, mode=PF.EPI_FWD, epi=PF.epi_spec(), scale_a=one, scale_b=one)
     ref = x8.double() @ w8.double().t()
     assert (y.double() - ref).abs().max().item() < 0.01 * ref.abs().max().item()
+
+
+@pytest.mark.parametrize("dtype,fmt,cols", [(torch.bfloat16, torch.float8_e4m3fn, 1024),
+                                            (torch.float32, torch.float8_e5m2, 520),
+                                            (torch.bfloat16, torch.float8_e4m3fn, 12)])  # 12: scalar path
+def test_quantize_rows_matches_torch_cast(native_lib, dtype, fmt, cols):
+    """e4m3 / e5m2 row quantiser (8-wide vector path and the scalar fallback): saturating
+    sat(x * q) bytes as torch's float8 cast of the clamped values, exact amax."""
+    x = (torch.randn(777, cols, device=DEV) * 3).to(dtype)
+    lim = 448.0 if fmt == torch.float8_e4m3fn else 57344.0
+    q = lim / (0.5 * x.float().abs().max().item())  # half the values saturate
+    qs = torch.tensor([q, 1.0 / q], device=DEV)
+    out = torch.empty(777, cols, device=DEV, dtype=fmt)
+    amax = torch.zeros(1, device=DEV)
+    native_lib.quantize_rows(x, out, qs, amax)
+    ref = (x.float() * qs[0]).clamp(-lim, lim).to(fmt)
+    assert (out.view(torch.uint8) != ref.view(torch.uint8)).float().mean().item() < 1e-4
+    assert amax.item() == x.float().abs().max().item()
