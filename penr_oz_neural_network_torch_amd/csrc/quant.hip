@@ -78,6 +78,9 @@ __global__ void scale_update_kernel(float* amax, float* qs, int n, float headroo
 // amax the optimizer reduced while writing W: every block derives q itself, block 0 publishes
 // {q, 1/q} for the GEMM and clears the other parity's accumulator (its last reader, the previous
 // transpose of this weight, finished before this launch in stream order).
+// FULL = every 64 x 64 tile in range with 16-B aligned rows (w: ldw % 4, out: ldo % 16): 16-B
+// loads (4 instead of 16 per lane) and one 16-B store of 16 consecutive k per lane
+template <bool FULL>
 __global__ void __launch_bounds__(256) quant_transpose_kernel(const float* __restrict__ w, int64_t ldw, int K, int N,
                                                               uint8_t* __restrict__ out, int64_t ldo, float* qs,
                                                               const float* amax, float* amax_clear) {
@@ -96,15 +99,40 @@ __global__ void __launch_bounds__(256) quant_transpose_kernel(const float* __res
   } else {
     q = qs[0];
   }
+  if constexpr (FULL) {
 #pragma unroll
-  for (int r = ty; r < 64; r += 4) {
-    const int k = k0 + r, n = n0 + tx;
-    tile[r][tx] = (k < K && n < N) ? w[static_cast<int64_t>(k) * ldw + n] : 0.f;
+    for (int pass = 0; pass < 4; ++pass) {
+      const int r = (threadIdx.x >> 4) + 16 * pass, c = (threadIdx.x & 15) * 4;
+      const float4 v = *reinterpret_cast<const float4*>(w + static_cast<int64_t>(k0 + r) * ldw + n0 + c);
+      tile[r][c] = v.x;
+      tile[r][c + 1] = v.y;
+      tile[r][c + 2] = v.z;
+      tile[r][c + 3] = v.w;
+    }
+  } else {
+#pragma unroll
+    for (int r = ty; r < 64; r += 4) {
+      const int k = k0 + r, n = n0 + tx;
+      tile[r][tx] = (k < K && n < N) ? w[static_cast<int64_t>(k) * ldw + n] : 0.f;
+    }
   }
   __syncthreads();
-  // each thread writes 4 consecutive k of one output row n: 64 rows x 16 quads
+  // each thread writes 16 consecutive k of one output row n: 64 rows x 4 sixteen-byte runs
   const int n_local = threadIdx.x >> 2, kq = (threadIdx.x & 3) * 16;
   const int n = n0 + n_local;
+  if constexpr (FULL) {
+    uint32_t words[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      uint32_t packed = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) packed |= static_cast<uint32_t>(to_e4m3(tile[kq + 4 * c + e][n_local] * q)) << (8 * e);
+      words[c] = packed;
+    }
+    *reinterpret_cast<uint4*>(out + static_cast<int64_t>(n) * ldo + k0 + kq) =
+        make_uint4(words[0], words[1], words[2], words[3]);
+    return;
+  }
   if (n >= N) return;
 #pragma unroll
   for (int c = 0; c < 16; c += 4) {
@@ -224,8 +252,14 @@ hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* o
                            const float* amax, float* amax_clear, hipStream_t s) {
   if (K <= 0 || N <= 0) return hipSuccess;
   if (amax != nullptr && amax_clear == nullptr) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(quant_transpose_kernel, dim3((N + 63) / 64, (K + 63) / 64), dim3(256), 0, s, w, ldw, K, N, out, ldo,
-                     qs, amax, amax_clear);
+  const bool full = K % 64 == 0 && N % 64 == 0 && ldw % 4 == 0 && ldo % 16 == 0 &&
+                    (reinterpret_cast<uintptr_t>(w) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 15) == 0;
+  if (full)
+    hipLaunchKernelGGL(quant_transpose_kernel<true>, dim3(N / 64, K / 64), dim3(256), 0, s, w, ldw, K, N, out, ldo, qs,
+                       amax, amax_clear);
+  else
+    hipLaunchKernelGGL(quant_transpose_kernel<false>, dim3((N + 63) / 64, (K + 63) / 64), dim3(256), 0, s, w, ldw, K, N,
+                       out, ldo, qs, amax, amax_clear);
   return hipGetLastError();
 }
 

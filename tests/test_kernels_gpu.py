@@ -464,3 +464,18 @@ def test_quantize_rows_matches_torch_cast(native_lib, dtype, fmt, cols):
     ref = (x.float() * qs[0]).clamp(-lim, lim).to(fmt)
     assert (out.view(torch.uint8) != ref.view(torch.uint8)).float().mean().item() < 1e-4
     assert amax.item() == x.float().abs().max().item()
+
+
+@pytest.mark.parametrize("K,N", [(192, 320), (100, 70)])  # full 64x64 tiles (16-B path) / ragged edges
+def test_quant_transpose_matches_torch_cast(native_lib, K, N):
+    """fp32 W [K, N] -> e4m3 W^T [N, K] at q = 448 / amax (taken from the optimizer's amax record)."""
+    w = torch.randn(K, N, device=DEV) * 0.05
+    out = torch.empty(N, K, device=DEV, dtype=torch.float8_e4m3fn)
+    qs = torch.zeros(2, device=DEV)
+    amax = w.abs().max().reshape(1)
+    clear = torch.full((1,), 7.0, device=DEV)
+    native_lib.quant_transpose(w, out, qs, amax, clear)
+    q = 448.0 / amax.item()
+    assert abs(qs[0].item() - q) <= 1e-6 * q and clear.item() == 0.0
+    ref = (w.t() * qs[0]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert (out.view(torch.uint8) != ref.view(torch.uint8)).float().mean().item() < 1e-4
