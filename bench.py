@@ -39,7 +39,8 @@ import torch.distributed as dist
 REFERENCE_SAMPLES_PER_S = {  # BASELINE.md, reference on CPU fp64 (no published numbers exist)
     "mlp4": 2064.0,
     "mlp4_fp32": 2064.0,
-    "mlp4_fp64": 2064.0,
+    "mlp4_fp64": 1775.0,  # BASELINE.md method C via_lists (the per-epoch torch.tensor(list) build)
+    "mlp4_fp64_autograd": 2064.0,
     "deep16x8192": 22.8,
     "mlp8192": 3095.0,
     "mlp8192_bf16": 3095.0,
@@ -59,13 +60,17 @@ CONFIGS = {
     "mlp4x8192": dict(sizes=[8192] * 5, algos=["relu"] * 3 + ["softmax"], batch=8192, dtype="bfloat16",
                       optimizer="adam", name="mlp[8192]x5 (4 layers 8192-wide, 268M params)"),
     # the headline model at the reference's own precisions: fp32 on the fused engine (f32 MFMA
-    # GEMMs), fp64 through the autograd engine (f64 MFMA GEMMs, HIP loss / stage kernels,
-    # torch.optim.Adam) — the reference epoch body (BASELINE.md method C) on the GPU
+    # GEMMs); fp64 (f64 MFMA GEMMs, fp64 Adam) the way a REST user gets it — NeuralNetworkModel.train()
+    # on Python lists (BASELINE.md method A), timed from the model's own progress timestamps; and
+    # fp64 through the autograd engine (the reference epoch body, method C, on the GPU)
     "mlp4_fp32": dict(sizes=[1024, 4096, 4096, 1024], algos=["relu", "relu", "softmax"], batch=8192,
                       dtype="float32", optimizer="adam", name="mlp[1024,4096,4096,1024] relu,relu,softmax fp32"),
     "mlp4_fp64": dict(sizes=[1024, 4096, 4096, 1024], algos=["relu", "relu", "softmax"], batch=8192,
-                      dtype="float64", optimizer="adam", engine="autograd",
-                      name="mlp[1024,4096,4096,1024] relu,relu,softmax fp64 (autograd engine)"),
+                      dtype="float64", optimizer="adam", engine="train",
+                      name="mlp[1024,4096,4096,1024] relu,relu,softmax fp64 (NeuralNetworkModel.train, lists)"),
+    "mlp4_fp64_autograd": dict(sizes=[1024, 4096, 4096, 1024], algos=["relu", "relu", "softmax"], batch=8192,
+                               dtype="float64", optimizer="adam", engine="autograd",
+                               name="mlp[1024,4096,4096,1024] relu,relu,softmax fp64 (autograd engine)"),
 }
 DTYPE_LABEL = {"bfloat16": "bf16", "fp8": "fp8", "float32": "fp32", "float64": "fp64"}
 
@@ -190,6 +195,42 @@ def _bench_autograd(args, cfg, model, ctx, batch, local) -> int:
     return 0
 
 
+def _bench_train(args, cfg, model, ctx, batch) -> int:
+    """The REST user's path: ``NeuralNetworkModel.train()`` on Python lists (the data a PUT /train/
+    body carries), here on one GPU with the fused engine. ms/step comes from the model's own
+    progress points (one per epoch; each carries the device-event time at which its step ended):
+    the span from the end of the last warm-up epoch to the end of the last epoch, divided by
+    --steps. The buffer gate (num_params samples, reference :429) is lowered to the data at hand."""
+    import tempfile
+    if ctx.world_size != 1:
+        log("error: the train() bench runs on one GPU")
+        return 2
+    g = torch.Generator(device="cpu").manual_seed(99)
+    n_data = args.n_data or batch
+    x = torch.randn(n_data, cfg["sizes"][0], generator=g, dtype=torch.float64)
+    y = torch.randint(0, cfg["sizes"][-1], (n_data,), generator=g)
+    data = [(x[i].tolist(), [int(y[i])]) for i in range(n_data)]
+    model.training_buffer_size = len(data)
+    total = args.warmup + args.steps
+    os.environ["PZ_MODELS_DIR"] = tempfile.mkdtemp(prefix="pz_bench_models_")
+    t0 = time.time()
+    model.train(data, epochs=total, learning_rate=args.lr, batch_size=batch, decay_rate=0.999,
+                dropout_rate=args.dropout, l2_lambda=args.l2)
+    log(f"train() of {total} epochs incl. checkpoints: {time.time() - t0:.1f}s, status {model.status}")
+    from datetime import datetime
+    pts = {p["epoch"]: p for p in model.progress}
+    if len(pts) != total or args.warmup < 1:
+        log(f"error: need one progress point per epoch and --warmup >= 1 (got {len(pts)} / {total})")
+        return 2
+    t_a = datetime.fromisoformat(pts[args.warmup]["dt"])
+    t_b = datetime.fromisoformat(pts[total]["dt"])
+    elapsed = (t_b - t_a).total_seconds()
+    import shutil
+    shutil.rmtree(os.environ["PZ_MODELS_DIR"], ignore_errors=True)
+    _emit(args, cfg, 1, elapsed, [pts[e]["cost"] for e in range(args.warmup + 1, total + 1)], batch, ctx)
+    return 0
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -229,6 +270,8 @@ def main(argv=None) -> int:
                                dtype=cfg["dtype"], device=f"cuda:{local}")
     if cfg.get("engine") == "autograd":
         return _bench_autograd(args, cfg, model, ctx, batch, local)
+    if cfg.get("engine") == "train":
+        return _bench_train(args, cfg, model, ctx, batch)
     trainer = FusedTrainer(model, ctx)
     n_data = args.n_data or 2 * batch
     g = torch.Generator(device="cpu").manual_seed(99 + rank)

@@ -87,6 +87,25 @@ pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
   return e;
 }
 
+
+// head accumulators (loss slots, bias-gradient column sums): fp32, or fp64 for fp64 models
+template <typename Args>
+void head_accumulators(Args& a, const optional<Tensor>& loss, const optional<Tensor>& colsum, bool f64,
+                       const char* what) {
+  for (const optional<Tensor>* t : {&loss, &colsum})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->scalar_type() == (f64 ? at::kDouble : at::kFloat), what,
+                  ": loss / colsum accumulators must be ", f64 ? "fp64 for fp64 data" : "fp32");
+  if (f64) {
+    a.loss64 = ptr_or_null<double>(loss);
+    a.colsum64 = ptr_or_null<double>(colsum);
+  } else {
+    a.loss = ptr_or_null<float>(loss);
+    a.colsum = ptr_or_null<float>(colsum);
+  }
+  a.loss_slots = (loss.has_value() && loss->defined()) ? static_cast<int>(loss->numel()) : 1;
+}
+
 // ------------------------------------------------------------------------------------ GEMM
 pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C,
                        const optional<Tensor>& bias, const optional<Tensor>& aux, const optional<Tensor>& colsum,
@@ -119,8 +138,10 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   p.alpha = static_cast<float>(alpha);
   p.accumulate = accumulate;
   if (bias.has_value() && bias->defined()) {
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() >= N, "pz::gemm: bias");
-    p.bias = bias->data_ptr<float>();
+    TORCH_CHECK((bias->scalar_type() == at::kFloat || bias->scalar_type() == at::kDouble) && bias->is_contiguous() &&
+                    bias->numel() >= N, "pz::gemm: bias must be fp32 or fp64 [N]");
+    if (bias->scalar_type() == at::kDouble) p.bias64 = bias->data_ptr<double>();
+    else p.bias = bias->data_ptr<float>();
   }
   if (aux.has_value() && aux->defined()) {
     TORCH_CHECK(aux->dim() == 2 && aux->stride(1) == 1 && aux->size(0) >= M && aux->size(1) >= N, "pz::gemm: aux");
@@ -129,8 +150,10 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
     p.aux_dtype = dt_of(*aux);
   }
   if (colsum.has_value() && colsum->defined()) {
-    TORCH_CHECK(colsum->scalar_type() == at::kFloat && colsum->numel() >= N, "pz::gemm: colsum must be fp32 [N]");
-    p.colsum = colsum->data_ptr<float>();
+    TORCH_CHECK((colsum->scalar_type() == at::kFloat || colsum->scalar_type() == at::kDouble) && colsum->numel() >= N,
+                "pz::gemm: colsum must be fp32 or fp64 [N]");
+    if (colsum->scalar_type() == at::kDouble) p.colsum64 = colsum->data_ptr<double>();
+    else p.colsum = colsum->data_ptr<float>();
   }
   p.epi_mode = static_cast<int>(epi_mode);
   p.epi = make_epi(epi_i, epi_f);
@@ -265,9 +288,10 @@ void gemm_update_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, cons
   if (epoch.has_value() && epoch->defined()) o.epoch_ptr = epoch_counter(epoch);
   if (stats_every > 1) TORCH_CHECK(o.epoch_ptr != nullptr, "pz::gemm_update: stats_every > 1 needs the epoch counter");
   if (hp.has_value() && hp->defined()) {
-    TORCH_CHECK(hp->scalar_type() == at::kFloat && hp->is_contiguous() && hp->is_cuda(), "pz::gemm_update: hp table");
+    TORCH_CHECK(hp->scalar_type() == at::kDouble && hp->is_contiguous() && hp->is_cuda(),
+                "pz::gemm_update: hp table (fp64)");
     TORCH_CHECK(o.epoch_ptr != nullptr, "pz::gemm_update: an hp table needs the epoch counter");
-    o.hp = hp->data_ptr<float>();
+    o.hp = hp->data_ptr<double>();
   }
   TORCH_CHECK(pz::gemm_path(p) == 1, "pz::gemm_update: needs an MFMA-eligible bf16 shape (16-B aligned state)");
   at::Tensor ws;
@@ -317,8 +341,7 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
   a.rows_valid = static_cast<int>(rows_valid);
   a.cols = static_cast<int>(logits.size(1));
   a.dtype = dt_of(logits);
-  a.loss = ptr_or_null<float>(loss);
-  a.loss_slots = a.loss != nullptr ? static_cast<int>(loss->numel()) : 1;
+  head_accumulators(a, loss, colsum, a.dtype == pz::DT_F64, "pz::xent_head");
   a.loss_scale = static_cast<float>(loss_scale);
   if (dh.has_value() && dh->defined()) {
     TORCH_CHECK(dh->scalar_type() == logits.scalar_type() && dh->stride(1) == 1, "pz::xent_head: dh");
@@ -326,7 +349,6 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
     a.ld_dh = dh->stride(0);
   }
   a.grad_scale = static_cast<float>(grad_scale);
-  a.colsum = ptr_or_null<float>(colsum);
   if (probs.has_value() && probs->defined()) {
     TORCH_CHECK(probs->scalar_type() == logits.scalar_type() && probs->stride(1) == 1, "pz::xent_head: probs");
     a.probs = probs->data_ptr();
@@ -352,15 +374,13 @@ void mse_head_op(const Tensor& y, const Tensor& target, int64_t rows_valid, cons
   a.rows_valid = static_cast<int>(rows_valid);
   a.cols = static_cast<int>(y.size(1));
   a.dtype = dt_of(y);
-  a.loss = ptr_or_null<float>(loss);
-  a.loss_slots = a.loss != nullptr ? static_cast<int>(loss->numel()) : 1;
+  head_accumulators(a, loss, colsum, a.dtype == pz::DT_F64, "pz::mse_head");
   a.loss_scale = static_cast<float>(loss_scale);
   if (dh.has_value() && dh->defined()) {
     a.dh = dh->data_ptr();
     a.ld_dh = dh->stride(0);
   }
   a.grad_scale = static_cast<float>(grad_scale);
-  a.colsum = ptr_or_null<float>(colsum);
   a.epi = make_epi(ei, ef);
   a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
   PZ_HIP_CHECK(pz::mse_head(a, cur_stream(y)));
@@ -384,10 +404,11 @@ void softmax_bwd_op(const Tensor& g, const Tensor& y, const Tensor& dx) {
 
 void colsum_op(const Tensor& x, const Tensor& out) {
   check_dev(x, "x");
-  TORCH_CHECK(x.is_contiguous() && out.scalar_type() == at::kFloat, "pz::colsum");
+  TORCH_CHECK(x.is_contiguous() && (out.scalar_type() == at::kFloat || out.scalar_type() == at::kDouble),
+              "pz::colsum: fp32 or fp64 output");
   const int cols = static_cast<int>(x.size(-1));
   const int rows = static_cast<int>(x.numel() / std::max<int64_t>(cols, 1));
-  PZ_HIP_CHECK(pz::colsum(x.data_ptr(), dt_of(x), out.data_ptr<float>(), rows, cols, cur_stream(x)));
+  PZ_HIP_CHECK(pz::colsum(x.data_ptr(), dt_of(x), out.data_ptr(), dt_of(out), rows, cols, cur_stream(x)));
 }
 
 void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t seed_lo, int64_t seed_hi,
@@ -478,35 +499,42 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
                        const optional<Tensor>& stats, const optional<Tensor>& hp, const optional<Tensor>& epoch,
                        int64_t stats_every, int64_t max_grid) {
   check_dev(params, "params");
-  TORCH_CHECK(params.scalar_type() == at::kFloat && grads.scalar_type() == at::kFloat, "pz::optimizer_step: fp32 master");
+  const auto rt = params.scalar_type();
+  TORCH_CHECK((rt == at::kFloat || rt == at::kDouble) && grads.scalar_type() == rt,
+              "pz::optimizer_step: fp32 or fp64 master with gradients of the same dtype");
+  for (const optional<Tensor>* t : {&exp_avg, &exp_avg_sq})
+    if (t->has_value() && (*t)->defined())
+      TORCH_CHECK((*t)->scalar_type() == rt, "pz::optimizer_step: Adam moments must match the master dtype");
   pz::OptArgs a{};
-  a.params = params.data_ptr<float>();
-  a.grads = grads.data_ptr<float>();
-  a.exp_avg = ptr_or_null<float>(exp_avg);
-  a.exp_avg_sq = ptr_or_null<float>(exp_avg_sq);
+  a.real = rt == at::kDouble ? pz::DT_F64 : pz::DT_F32;
+  a.params = params.data_ptr();
+  a.grads = grads.data_ptr();
+  a.exp_avg = ptr_or_null<void>(exp_avg);
+  a.exp_avg_sq = ptr_or_null<void>(exp_avg_sq);
   TORCH_CHECK(!adam || (a.exp_avg && a.exp_avg_sq), "pz::optimizer_step: Adam needs moment buffers");
   a.segments = reinterpret_cast<const pz::OptSegment*>(segments.data_ptr());
   a.num_segments = static_cast<int>(num_segments);
   a.block_seg = block_seg.data_ptr<int64_t>();
   a.total_blocks = static_cast<int>(total_blocks);
   a.adam = adam;
-  a.lr = static_cast<float>(lr);
-  a.beta1 = static_cast<float>(beta1);
-  a.beta2 = static_cast<float>(beta2);
-  a.eps = static_cast<float>(eps);
-  a.bias_c1 = static_cast<float>(bias_c1);
-  a.bias_c2_sqrt = static_cast<float>(bias_c2_sqrt);
-  a.grad_scale = static_cast<float>(grad_scale);
-  a.l2_lambda = static_cast<float>(l2);
+  a.lr = lr;
+  a.beta1 = beta1;
+  a.beta2 = beta2;
+  a.eps = eps;
+  a.bias_c1 = bias_c1;
+  a.bias_c2_sqrt = bias_c2_sqrt;
+  a.grad_scale = grad_scale;
+  a.l2_lambda = l2;
   a.stats = ptr_or_null<double>(stats);
   a.stats_every = static_cast<int>(stats_every);
   a.max_grid = static_cast<int>(max_grid);
   if (stats_every > 1) TORCH_CHECK(epoch.has_value() && epoch->defined(), "pz::optimizer_step: stats_every > 1 needs the epoch counter");
   if (epoch.has_value() && epoch->defined()) a.epoch_ptr = epoch_counter(epoch);
   if (hp.has_value() && hp->defined()) {
-    TORCH_CHECK(hp->scalar_type() == at::kFloat && hp->is_contiguous() && hp->is_cuda(), "pz::optimizer_step: hp table");
+    TORCH_CHECK(hp->scalar_type() == at::kDouble && hp->is_contiguous() && hp->is_cuda(),
+                "pz::optimizer_step: hp table (fp64)");
     TORCH_CHECK(epoch.has_value(), "pz::optimizer_step: an hp table needs the epoch counter");
-    a.hp = hp->data_ptr<float>();
+    a.hp = hp->data_ptr<double>();
     a.epoch_ptr = epoch_counter(epoch);
   }
   PZ_HIP_CHECK(pz::optimizer_step(a, cur_stream(params)));
@@ -515,7 +543,9 @@ void optimizer_step_op(const Tensor& params, const Tensor& grads, const optional
 void segment_stats_op(const Tensor& params, const Tensor& segments, const Tensor& block_seg, int64_t num_segments,
                       int64_t total_blocks, const Tensor& stats) {
   check_dev(params, "params");
-  PZ_HIP_CHECK(pz::segment_stats(params.data_ptr<float>(), reinterpret_cast<const pz::OptSegment*>(segments.data_ptr()),
+  TORCH_CHECK(params.scalar_type() == at::kFloat || params.scalar_type() == at::kDouble, "pz::segment_stats: dtype");
+  PZ_HIP_CHECK(pz::segment_stats(params.data_ptr(), params.scalar_type() == at::kDouble ? pz::DT_F64 : pz::DT_F32,
+                                 reinterpret_cast<const pz::OptSegment*>(segments.data_ptr()),
                                  block_seg.data_ptr<int64_t>(), static_cast<int>(num_segments),
                                  static_cast<int>(total_blocks), stats.data_ptr<double>(), cur_stream(params)));
 }
@@ -685,16 +715,23 @@ void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tenso
   TORCH_CHECK(dev_epoch || epoch < costs.numel(), "pz::step_finalize: epoch out of range");
   TORCH_CHECK(ratio_row < 0 || (ratio_row + 1) * nslots <= ratios.numel(), "pz::step_finalize: ratio row out of range");
   TORCH_CHECK(ratio_row != -2 || every >= 1, "pz::step_finalize: ratio rule needs every >= 1");
+  TORCH_CHECK(costs.scalar_type() == at::kDouble, "pz::step_finalize: costs must be fp64");
   pz::FinalizeArgs a{};
-  a.loss = ptr_or_null<float>(loss);
-  a.loss_slots = a.loss != nullptr ? static_cast<int>(loss->numel()) : 1;
+  if (loss.has_value() && loss->defined()) {
+    TORCH_CHECK(loss->scalar_type() == at::kFloat || loss->scalar_type() == at::kDouble, "pz::step_finalize: loss dtype");
+    if (loss->scalar_type() == at::kDouble) a.loss64 = loss->data_ptr<double>();
+    else a.loss = loss->data_ptr<float>();
+    a.loss_slots = static_cast<int>(loss->numel());
+  } else {
+    a.loss_slots = 1;
+  }
   a.loss_div = static_cast<float>(loss_div);
   a.stats_prev = stats_prev.data_ptr<double>();
   a.stats_cur = stats_cur.data_ptr<double>();
   a.slot_numel = slot_numel.data_ptr<double>();
   a.nslots = static_cast<int>(nslots);
   a.l2 = static_cast<float>(l2);
-  a.costs = costs.data_ptr<float>();
+  a.costs = costs.data_ptr<double>();
   a.epoch = static_cast<int>(epoch);
   a.ratios = ratios.data_ptr<float>();
   a.ratio_row = static_cast<int>(ratio_row);

@@ -68,29 +68,45 @@ PZ_DEV void block_loss_flush(float* loss, float v, float* red, int slots) {
   __syncthreads();
   if (threadIdx.x == 0) atomicAdd(loss + (slots > 1 ? blockIdx.x % slots : 0), red[0] + red[1] + red[2] + red[3]);
 }
+// fp64 models: the loss accumulates in double (the reference reports an fp64 cost)
+PZ_DEV void block_loss_flush(double* loss, double v, double* red, int slots) {
+  v = wave_sum_d(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(loss + (slots > 1 ? blockIdx.x % slots : 0), red[0] + red[1] + red[2] + red[3]);
+}
 
-PZ_DEV void block_colsum_flush(float* colsum, const float* cs, int cols) {
+template <typename A>
+PZ_DEV void block_colsum_flush(A* colsum, const A* cs, int cols) {
   __syncthreads();
   for (int c = threadIdx.x; c < cols; c += 256)
-    if (cs[c] != 0.f) atomicAdd(colsum + c, cs[c]);
+    if (cs[c] != A(0)) atomicAdd(colsum + c, cs[c]);
 }
+
+// accumulator pointers of a head: double for fp64 logits (loss64 / colsum64), float otherwise
+template <typename F> PZ_DEV F* head_loss(void* f32, void* f64);
+template <> PZ_DEV float* head_loss<float>(void* f32, void*) { return static_cast<float*>(f32); }
+template <> PZ_DEV double* head_loss<double>(void*, void* f64) { return static_cast<double*>(f64); }
 
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
   a.epi = epi_resolve(a.epi);
-  extern __shared__ float cs_lds[];  // [cols] when a.colsum (LDS column partials)
-  __shared__ float red[4];
+  extern __shared__ __attribute__((aligned(16))) char cs_raw[];
+  F* cs_lds = reinterpret_cast<F*>(cs_raw);  // [cols] when a.colsum (LDS column partials)
+  __shared__ F red[4];
+  F* const loss = head_loss<F>(a.loss, a.loss64);
+  F* const colsum = head_loss<F>(a.colsum, a.colsum64);
   const T* __restrict__ logits = static_cast<const T*>(a.logits);
   T* __restrict__ dh = static_cast<T*>(a.dh);
   T* __restrict__ probs = static_cast<T*>(a.probs);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const bool cs_on = a.colsum != nullptr && dh != nullptr;
+  const bool cs_on = colsum != nullptr && dh != nullptr;
   if (cs_on) {
-    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = 0.f;
+    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = F(0);
     __syncthreads();
   }
-  float loss_acc = 0.f;
+  F loss_acc = F(0);
   for (int rr = 0; rr < kHeadRows / 4; ++rr) {
     const int row = blockIdx.x * kHeadRows + wave * (kHeadRows / 4) + rr;
     if (row >= a.rows) break;
@@ -111,7 +127,7 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
       // loss here, never an out-of-row read
       const bool lab_ok = label >= 0 && label < a.cols;
       const F xlab = lab_ok ? static_cast<F>(ldd<T>(lr, label)) : static_cast<F>(NAN);
-      if (lane == 0) loss_acc += static_cast<float>((lse - xlab) * static_cast<F>(a.loss_scale));
+      if (lane == 0) loss_acc += (lse - xlab) * static_cast<F>(a.loss_scale);
       for (int c = lane; c < a.cols; c += 64) {
         const F pr = fexp(static_cast<F>(ldd<T>(lr, c)) - mx) * inv;
         if (probs != nullptr) std_<T>(probs, static_cast<int64_t>(row) * a.ld_probs + c, static_cast<double>(pr));
@@ -120,15 +136,15 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
           const uint64_t idx = static_cast<uint64_t>(row) * static_cast<uint64_t>(a.idx_ld) + c;
           g = epi_bwd<F>(g, F(0), idx, a.epi);
           std_<T>(dh, static_cast<int64_t>(row) * a.ld_dh + c, static_cast<double>(g));
-          if (cs_on) atomicAdd(&cs_lds[c], static_cast<float>(g));
+          if (cs_on) atomicAdd(&cs_lds[c], g);
         }
       }
     } else if (dh != nullptr) {
       for (int c = lane; c < a.cols; c += 64) std_<T>(dh, static_cast<int64_t>(row) * a.ld_dh + c, 0.0);
     }
   }
-  if (a.loss != nullptr) block_loss_flush(a.loss, loss_acc, red, a.loss_slots);
-  if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
+  if (loss != nullptr) block_loss_flush(loss, loss_acc, red, a.loss_slots);
+  if (cs_on) block_colsum_flush(colsum, cs_lds, a.cols);
 }
 
 // bf16 fast path: every lane holds NCH chunks of 8 logits in registers (one read of the row),
@@ -274,19 +290,22 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) mse_head_kernel(MseArgs a) {
   a.epi = epi_resolve(a.epi);
-  extern __shared__ float cs_lds[];
-  __shared__ float red[4];
+  extern __shared__ __attribute__((aligned(16))) char cs_raw[];
+  F* cs_lds = reinterpret_cast<F*>(cs_raw);
+  __shared__ F red[4];
+  F* const loss = head_loss<F>(a.loss, a.loss64);
+  F* const colsum = head_loss<F>(a.colsum, a.colsum64);
   const T* __restrict__ y = static_cast<const T*>(a.y);
   const T* __restrict__ t = static_cast<const T*>(a.target);
   T* __restrict__ dh = static_cast<T*>(a.dh);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const bool cs_on = a.colsum != nullptr && dh != nullptr;
+  const bool cs_on = colsum != nullptr && dh != nullptr;
   if (cs_on) {
-    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = 0.f;
+    for (int c = threadIdx.x; c < a.cols; c += 256) cs_lds[c] = F(0);
     __syncthreads();
   }
-  float acc = 0.f;
+  F acc = F(0);
   for (int rr = 0; rr < kHeadRows / 4; ++rr) {
     const int64_t r = static_cast<int64_t>(blockIdx.x) * kHeadRows + wave * (kHeadRows / 4) + rr;
     if (r >= a.rows) break;
@@ -295,17 +314,17 @@ __global__ void __launch_bounds__(256) mse_head_kernel(MseArgs a) {
       if (r < a.rows_valid) {
         const F yv = static_cast<F>(ldd<T>(y, r * a.ld_y + c));
         const F d = yv - static_cast<F>(ldd<T>(t, r * a.ld_t + c));
-        acc += static_cast<float>(d * d * static_cast<F>(a.loss_scale));
+        acc += d * d * static_cast<F>(a.loss_scale);
         g = epi_bwd<F>(F(2) * d * static_cast<F>(a.grad_scale), yv, static_cast<uint64_t>(r * a.idx_ld + c), a.epi);
       }
       if (dh != nullptr) {
         std_<T>(dh, r * a.ld_dh + c, static_cast<double>(g));
-        if (cs_on) atomicAdd(&cs_lds[c], static_cast<float>(g));
+        if (cs_on) atomicAdd(&cs_lds[c], g);
       }
     }
   }
-  if (a.loss != nullptr) block_loss_flush(a.loss, acc, red, a.loss_slots);
-  if (cs_on) block_colsum_flush(a.colsum, cs_lds, a.cols);
+  if (loss != nullptr) block_loss_flush(loss, acc, red, a.loss_slots);
+  if (cs_on) block_colsum_flush(colsum, cs_lds, a.cols);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -348,17 +367,18 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const T* __restrict__ 
   }
 }
 
-// column sums of a [rows][cols] matrix into fp32 (atomic per 64-column strip per block)
-template <typename T>
-__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, float* __restrict__ out, int rows,
+// column sums of a [rows][cols] matrix into fp32 (fp64 for fp64 data; atomic per 64-column strip
+// per block)
+template <typename T, typename A>
+__global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, A* __restrict__ out, int rows,
                                                      int cols, int rows_per_block) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
-  float s = 0.f;
+  A s = A(0);
   if (c < cols)
-    for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) s += static_cast<float>(ldd<T>(x, static_cast<int64_t>(r) * cols + c));
-  __shared__ float part[4][64];
+    for (int r = r0 + (threadIdx.x >> 6); r < r1; r += 4) s += static_cast<A>(ldd<T>(x, static_cast<int64_t>(r) * cols + c));
+  __shared__ A part[4][64];
   part[threadIdx.x >> 6][threadIdx.x & 63] = s;
   __syncthreads();
   if (threadIdx.x < 64 && c < cols) atomicAdd(out + c, part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x]);
@@ -497,12 +517,14 @@ constexpr int kMaxLdsCols = 16384;  // 64 KiB of fp32 column partials
 hipError_t xent_head(const XentArgs& in, hipStream_t s) {
   if (in.rows <= 0) return hipSuccess;
   XentArgs a = in;
-  float* colsum_direct = nullptr;
-  if (a.colsum != nullptr && a.cols > kMaxLdsCols) {  // too wide for LDS partials: separate pass
-    colsum_direct = a.colsum;
+  void* colsum_direct = nullptr;
+  const bool acc64 = a.dtype == DT_F64;
+  if ((a.colsum != nullptr || a.colsum64 != nullptr) && a.cols > kMaxLdsCols / (acc64 ? 2 : 1)) {
+    colsum_direct = acc64 ? static_cast<void*>(a.colsum64) : static_cast<void*>(a.colsum);  // separate pass
     a.colsum = nullptr;
+    a.colsum64 = nullptr;
   }
-  const size_t lds = a.colsum != nullptr ? sizeof(float) * a.cols : 0;
+  const size_t lds = (acc64 ? a.colsum64 != nullptr : a.colsum != nullptr) ? (acc64 ? 8 : 4) * a.cols : 0;
   const dim3 grid((a.rows + kHeadRows - 1) / kHeadRows);
   const bool vec = a.dtype == DT_BF16 && a.cols % 8 == 0 && a.ld % 8 == 0 && (a.dh == nullptr || a.ld_dh % 8 == 0) &&
                    (a.probs == nullptr || a.ld_probs % 8 == 0) && a.idx_ld % 2 == 0 &&
@@ -525,7 +547,7 @@ hipError_t xent_head(const XentArgs& in, hipStream_t s) {
   if (colsum_direct != nullptr && a.dh != nullptr) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return colsum(a.dh, a.dtype, colsum_direct, a.rows, a.cols, s);  // ld_dh == cols required
+    return colsum(a.dh, a.dtype, colsum_direct, acc64 ? DT_F64 : DT_F32, a.rows, a.cols, s);  // ld_dh == cols
   }
   return hipGetLastError();
 }
@@ -533,12 +555,14 @@ hipError_t xent_head(const XentArgs& in, hipStream_t s) {
 hipError_t mse_head(const MseArgs& in, hipStream_t s) {
   if (in.rows <= 0 || in.cols <= 0) return hipSuccess;
   MseArgs a = in;
-  float* colsum_direct = nullptr;
-  if (a.colsum != nullptr && a.cols > kMaxLdsCols) {
-    colsum_direct = a.colsum;
+  void* colsum_direct = nullptr;
+  const bool acc64 = a.dtype == DT_F64;
+  if ((a.colsum != nullptr || a.colsum64 != nullptr) && a.cols > kMaxLdsCols / (acc64 ? 2 : 1)) {
+    colsum_direct = acc64 ? static_cast<void*>(a.colsum64) : static_cast<void*>(a.colsum);
     a.colsum = nullptr;
+    a.colsum64 = nullptr;
   }
-  const size_t lds = a.colsum != nullptr ? sizeof(float) * a.cols : 0;
+  const size_t lds = (acc64 ? a.colsum64 != nullptr : a.colsum != nullptr) ? (acc64 ? 8 : 4) * a.cols : 0;
   PZ_DISPATCH_FLOAT(a.dtype, T, {
     using F = typename MathOf<T>::type;
     hipLaunchKernelGGL((mse_head_kernel<T, F>), dim3((a.rows + kHeadRows - 1) / kHeadRows), dim3(256), lds, s, a);
@@ -546,7 +570,7 @@ hipError_t mse_head(const MseArgs& in, hipStream_t s) {
   if (colsum_direct != nullptr && a.dh != nullptr) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return colsum(a.dh, a.dtype, colsum_direct, a.rows, a.cols, s);
+    return colsum(a.dh, a.dtype, colsum_direct, acc64 ? DT_F64 : DT_F32, a.rows, a.cols, s);
   }
   return hipGetLastError();
 }
@@ -571,12 +595,17 @@ hipError_t softmax_bwd(const void* g, const void* y, void* dx, int dtype, int ro
   return hipGetLastError();
 }
 
-hipError_t colsum(const void* x, int dtype, float* out, int rows, int cols, hipStream_t s) {
+hipError_t colsum(const void* x, int dtype, void* out, int out_dtype, int rows, int cols, hipStream_t s) {
   if (rows <= 0 || cols <= 0) return hipSuccess;
   const int rpb = 256;
   dim3 grid((cols + 63) / 64, (rows + rpb - 1) / rpb);
   PZ_DISPATCH_FLOAT(dtype, T, {
-    hipLaunchKernelGGL((colsum_kernel<T>), grid, dim3(256), 0, s, static_cast<const T*>(x), out, rows, cols, rpb);
+    if (out_dtype == DT_F64)
+      hipLaunchKernelGGL((colsum_kernel<T, double>), grid, dim3(256), 0, s, static_cast<const T*>(x),
+                         static_cast<double*>(out), rows, cols, rpb);
+    else
+      hipLaunchKernelGGL((colsum_kernel<T, float>), grid, dim3(256), 0, s, static_cast<const T*>(x),
+                         static_cast<float*>(out), rows, cols, rpb);
   });
   return hipGetLastError();
 }

@@ -88,7 +88,8 @@ __global__ void __launch_bounds__(256) gemm_generic_kernel(const GemmArgs p) {
         const Acc y = ld<AuxT, Acc>(aux, int64_t(m) * p.ldaux + n);
         v = epi_bwd<Acc>(v, y, idx, epi);
       } else {
-        if (p.bias != nullptr) v += static_cast<Acc>(p.bias[n]);
+        if (p.bias64 != nullptr) v += static_cast<Acc>(p.bias64[n]);
+        else if (p.bias != nullptr) v += static_cast<Acc>(p.bias[n]);
         if (p.epi_mode == EPI_FWD) v = epi_fwd<Acc>(v, idx, epi);
       }
       const int64_t off = int64_t(m) * p.ldc + n;
@@ -96,7 +97,8 @@ __global__ void __launch_bounds__(256) gemm_generic_kernel(const GemmArgs p) {
       store_elem<OutT>(Cp, off, static_cast<double>(v));
       colsum += v;
     }
-    if (p.colsum != nullptr && n < p.N) atomicAdd(p.colsum + n, static_cast<float>(colsum));
+    if (p.colsum64 != nullptr && n < p.N) atomicAdd(p.colsum64 + n, static_cast<double>(colsum));
+    else if (p.colsum != nullptr && n < p.N) atomicAdd(p.colsum + n, static_cast<float>(colsum));
   }
 }
 

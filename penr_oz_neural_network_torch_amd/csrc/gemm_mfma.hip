@@ -366,10 +366,10 @@ PZ_DEV void epilogue_opt(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   int epoch = -1;
   if (o.epoch_ptr != nullptr) epoch = *o.epoch_ptr;
   if (o.hp != nullptr) {  // graph-replayed step: this epoch's hyper-parameters
-    const float* h = o.hp + 4 * static_cast<int64_t>(epoch);
-    lr = h[0];
-    bc1 = h[1];
-    bc2s = h[2];
+    const double* h = o.hp + 4 * static_cast<int64_t>(epoch);
+    lr = static_cast<float>(h[0]);
+    bc1 = static_cast<float>(h[1]);
+    bc2s = static_cast<float>(h[2]);
   }
   const bool full = o.stats_every == 1 || (o.stats_every > 1 && (epoch < 0 || epoch % o.stats_every == 0));
   const float step_size = lr / bc1;
@@ -991,6 +991,7 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
 #ifndef PZ_GEMM_LAB
 bool fp8_eligible(const GemmArgs& p) {
   if (p.force_generic || p.in_dtype != DT_FP8 || p.out_dtype != DT_BF16) return false;
+  if (p.bias64 != nullptr || p.colsum64 != nullptr) return false;
   if (!p.a_kc || !p.b_kc || p.accumulate) return false;
   if (p.M < 64 || p.N < 64 || p.K < 64 || p.K % 64 != 0) return false;
   if (p.N % 8 != 0 || p.ldc % 8 != 0 || p.lda % 16 != 0 || p.ldb % 16 != 0) return false;
@@ -1013,6 +1014,7 @@ bool fp8_eligible(const GemmArgs& p) {
 bool mfma_eligible(const GemmArgs& p) {
   if (p.in_dtype == DT_FP8) return fp8_eligible(p);
   if (p.force_generic || p.in_dtype != DT_BF16) return false;
+  if (p.bias64 != nullptr || p.colsum64 != nullptr) return false;  // fp64 models: wide / generic paths
   if (p.out_dtype != DT_BF16 && p.out_dtype != DT_F32) return false;
   if (p.M < 64 || p.N < 64 || p.K < kBK || p.K % kBK != 0) return false;
   if (p.N % 8 != 0 || p.ldc % 8 != 0) return false;

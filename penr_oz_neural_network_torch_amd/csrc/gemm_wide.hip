@@ -189,7 +189,8 @@ __global__ void __launch_bounds__(256) gemm_wide_kernel(const GemmArgs p) {
         if (p.epi_mode == EPI_BWD) {
           v = epi_bwd<T>(v, aux_at(int64_t(m) * p.ldaux + n), idx, epi);
         } else {
-          if (p.bias != nullptr) v += static_cast<T>(p.bias[n]);
+          if (p.bias64 != nullptr) v += static_cast<T>(p.bias64[n]);
+          else if (p.bias != nullptr) v += static_cast<T>(p.bias[n]);
           if (p.epi_mode == EPI_FWD) v = epi_fwd<T>(v, idx, epi);
         }
         const int64_t off = int64_t(m) * p.ldc + n;
@@ -197,10 +198,13 @@ __global__ void __launch_bounds__(256) gemm_wide_kernel(const GemmArgs p) {
         wst<OutT>(Cp, off, static_cast<double>(v));
         cs += static_cast<double>(v);
       }
-    if (p.colsum != nullptr) {  // lanes l, l+16, l+32, l+48 share column n
+    if (p.colsum != nullptr || p.colsum64 != nullptr) {  // lanes l, l+16, l+32, l+48 share column n
       cs += __shfl_xor(cs, 16, 64);
       cs += __shfl_xor(cs, 32, 64);
-      if (lane < 16 && n < p.N) atomicAdd(p.colsum + n, static_cast<float>(cs));
+      if (lane < 16 && n < p.N) {
+        if (p.colsum64 != nullptr) atomicAdd(p.colsum64 + n, cs);
+        else atomicAdd(p.colsum + n, static_cast<float>(cs));
+      }
     }
   }
 }

@@ -1,4 +1,5 @@
-// N6 — fused multi-tensor optimizer step over the flat fp32 master-parameter buffer.
+// N6 — fused multi-tensor optimizer step over the flat master-parameter buffer (fp32, or fp64
+// for fp64 models: the reference's own precision, updated in fp64 like torch.optim.Adam does).
 //
 // Replaces, per parameter, the reference's chain (neural_net_model.py:482-506):
 //   L2 term gradient (autograd of `cost += l2 * sum(w**2)`, weights only)  -> folded into g
@@ -59,10 +60,27 @@ PZ_DEV void block_reduce_add(double v[4], double* dst, bool full = true) {
   }
 }
 
+// the optimizer's view of OptArgs in master precision R (hyper-parameters rounded once)
+template <typename R>
+struct OptView {
+  R* params;
+  R* grads;
+  R* exp_avg;
+  R* exp_avg_sq;
+  R lr, beta1, beta2, eps, bias_c1, bias_c2_sqrt, grad_scale, l2_lambda;
+  PZ_DEV explicit OptView(const OptArgs& a)
+      : params(static_cast<R*>(a.params)), grads(static_cast<R*>(a.grads)), exp_avg(static_cast<R*>(a.exp_avg)),
+        exp_avg_sq(static_cast<R*>(a.exp_avg_sq)), lr(static_cast<R>(a.lr)), beta1(static_cast<R>(a.beta1)),
+        beta2(static_cast<R>(a.beta2)), eps(static_cast<R>(a.eps)), bias_c1(static_cast<R>(a.bias_c1)),
+        bias_c2_sqrt(static_cast<R>(a.bias_c2_sqrt)), grad_scale(static_cast<R>(a.grad_scale)),
+        l2_lambda(static_cast<R>(a.l2_lambda)) {}
+};
+
 // one parameter's update: returns the new value; m / v are Adam's moments (in and out)
-template <bool ADAM>
-PZ_DEV float update_one(const OptArgs& a, float p0, float graw, float l2x2, float step_size, float& m, float& v) {
-  return opt_update<ADAM>(p0, graw, a.grad_scale, l2x2, a.lr, step_size, a.beta1, a.beta2, a.bias_c2_sqrt, a.eps, m, v);
+template <bool ADAM, typename R>
+PZ_DEV R update_one(const OptView<R>& a, R p0, R graw, R l2x2, R step_size, R& m, R& v) {
+  return opt_update<ADAM, R>(p0, graw, a.grad_scale, l2x2, a.lr, step_size, a.beta1, a.beta2, a.bias_c2_sqrt, a.eps, m,
+                             v);
 }
 
 // max |w_new| of the block -> one atomic per block (non-negative floats order like their bits)
@@ -79,12 +97,31 @@ PZ_DEV void block_amax_commit(float m, float* amax) {
 
 // full: the update-ratio sums too (progress epochs only); otherwise just sum(w^2), which the
 // next step's cost needs for its L2 term
-PZ_DEV void add_stats(double st[4], float p0, float p1, bool full) {
+template <typename R>
+PZ_DEV void add_stats(double st[4], R p0, R p1, bool full) {
   st[3] += static_cast<double>(p1) * p1;
   if (full) {
     const double d = static_cast<double>(p1 - p0);
     st[0] += d; st[1] += d * d; st[2] += p1;
   }
+}
+
+// 16-B vectors of R (float4 / double2) for the vectorised segments
+template <typename R> struct Vec;
+template <> struct Vec<float> { using T = float4; static constexpr int N = 4; };
+template <> struct Vec<double> { using T = double2; static constexpr int N = 2; };
+template <typename R>
+PZ_DEV void vld(const R* p, R (&x)[Vec<R>::N]) {
+  const typename Vec<R>::T q = *reinterpret_cast<const typename Vec<R>::T*>(p);
+  if constexpr (Vec<R>::N == 4) { x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w; }
+  else { x[0] = q.x; x[1] = q.y; }
+}
+template <typename R>
+PZ_DEV void vst(R* p, const R (&x)[Vec<R>::N]) {
+  typename Vec<R>::T q;
+  if constexpr (Vec<R>::N == 4) { q.x = x[0]; q.y = x[1]; q.z = x[2]; q.w = x[3]; }
+  else { q.x = x[0]; q.y = x[1]; }
+  *reinterpret_cast<typename Vec<R>::T*>(p) = q;
 }
 
 // Segments whose offset and length are multiples of 4 (every dense weight: ParamStore aligns
@@ -94,61 +131,66 @@ PZ_DEV void add_stats(double st[4], float p0, float p1, bool full) {
 // Grid: min(total_blocks, kOptMaxResident) workgroups loop over the 4096-element work blocks, so
 // a launch that overlaps the MFMA-bound GEMMs (side stream) gets all its workgroups resident
 // beside the GEMM's instead of queueing behind the GEMM's pending ones.
-template <bool ADAM>
-PZ_DEV void optimizer_block(const OptArgs& a, int block, bool full) {
-  const int seg_id = find_segment(a.block_seg, a.num_segments, block);
-  const OptSegment seg = a.segments[seg_id];
-  const int64_t local0 = (static_cast<int64_t>(block) - a.block_seg[seg_id]) * kOptElemsPerBlock;
+template <bool ADAM, typename R>
+PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block, bool full) {
+  constexpr int VN = Vec<R>::N;
+  const int seg_id = find_segment(args.block_seg, args.num_segments, block);
+  const OptSegment seg = args.segments[seg_id];
+  const int64_t local0 = (static_cast<int64_t>(block) - args.block_seg[seg_id]) * kOptElemsPerBlock;
   const bool weight = seg.is_weight != 0;
-  const float l2x2 = weight ? 2.f * a.l2_lambda : 0.f;
-  const float step_size = a.lr / a.bias_c1;
+  const R l2x2 = weight ? R(2) * a.l2_lambda : R(0);
+  const R step_size = a.lr / a.bias_c1;
   const bool stats = seg.stat_slot >= 0;
   double st[4] = {0.0, 0.0, 0.0, 0.0};
   float am = 0.f;  // max |w_new| (fp8 weight scaling, seg.amax)
 
   if (((seg.offset | seg.numel) & 3) == 0) {
 #pragma unroll
-    for (int u = 0; u < kPerThread / 4; ++u) {
-      const int64_t li = local0 + (static_cast<int64_t>(u) * kThreads + threadIdx.x) * 4;
+    for (int u = 0; u < kPerThread / VN; ++u) {
+      const int64_t li = local0 + (static_cast<int64_t>(u) * kThreads + threadIdx.x) * VN;
       if (li >= seg.numel) break;
       const int64_t gi = seg.offset + li;
-      const float4 p0 = *reinterpret_cast<const float4*>(a.params + gi);
-      float g[4];
-      if (seg.grad16 != nullptr) {
-        const uint2 q = *reinterpret_cast<const uint2*>(seg.grad16 + li);
-        g[0] = bf2f(q.x & 0xFFFF); g[1] = bf2f(q.x >> 16); g[2] = bf2f(q.y & 0xFFFF); g[3] = bf2f(q.y >> 16);
+      R p0[VN], g[VN], m[VN] = {}, v[VN] = {}, p1[VN];
+      vld<R>(a.params + gi, p0);
+      if constexpr (VN == 4) {
+        if (seg.grad16 != nullptr) {
+          const uint2 q = *reinterpret_cast<const uint2*>(seg.grad16 + li);
+          g[0] = bf2f(q.x & 0xFFFF); g[1] = bf2f(q.x >> 16); g[2] = bf2f(q.y & 0xFFFF); g[3] = bf2f(q.y >> 16);
+        } else {
+          vld<R>(a.grads + gi, g);
+        }
       } else {
-        const float4 q = *reinterpret_cast<const float4*>(a.grads + gi);
-        g[0] = q.x; g[1] = q.y; g[2] = q.z; g[3] = q.w;
-        if (seg.zero_grad) *reinterpret_cast<float4*>(a.grads + gi) = make_float4(0.f, 0.f, 0.f, 0.f);
+        vld<R>(a.grads + gi, g);
       }
-      float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m;
+      if (seg.zero_grad && seg.grad16 == nullptr) {
+        const R z[VN] = {};
+        vst<R>(a.grads + gi, z);
+      }
       if constexpr (ADAM) {
-        m = *reinterpret_cast<const float4*>(a.exp_avg + gi);
-        v = *reinterpret_cast<const float4*>(a.exp_avg_sq + gi);
+        vld<R>(a.exp_avg + gi, m);
+        vld<R>(a.exp_avg_sq + gi, v);
       }
-      float4 p1;
-      p1.x = update_one<ADAM>(a, p0.x, g[0], l2x2, step_size, m.x, v.x);
-      p1.y = update_one<ADAM>(a, p0.y, g[1], l2x2, step_size, m.y, v.y);
-      p1.z = update_one<ADAM>(a, p0.z, g[2], l2x2, step_size, m.z, v.z);
-      p1.w = update_one<ADAM>(a, p0.w, g[3], l2x2, step_size, m.w, v.w);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) p1[k] = update_one<ADAM, R>(a, p0[k], g[k], l2x2, step_size, m[k], v[k]);
       if constexpr (ADAM) {
-        *reinterpret_cast<float4*>(a.exp_avg + gi) = m;
-        *reinterpret_cast<float4*>(a.exp_avg_sq + gi) = v;
+        vst<R>(a.exp_avg + gi, m);
+        vst<R>(a.exp_avg_sq + gi, v);
       }
-      *reinterpret_cast<float4*>(a.params + gi) = p1;
-      if (seg.shadow != nullptr) {
-        if (seg.shadow_dtype == DT_BF16)
-          *reinterpret_cast<uint2*>(static_cast<uint16_t*>(seg.shadow) + li) =
-              make_uint2(pack_bf2(p1.x, p1.y), pack_bf2(p1.z, p1.w));
-        else
-          *reinterpret_cast<float4*>(static_cast<float*>(seg.shadow) + li) = p1;
+      vst<R>(a.params + gi, p1);
+      if constexpr (VN == 4) {
+        if (seg.shadow != nullptr) {
+          if (seg.shadow_dtype == DT_BF16)
+            *reinterpret_cast<uint2*>(static_cast<uint16_t*>(seg.shadow) + li) =
+                make_uint2(pack_bf2(p1[0], p1[1]), pack_bf2(p1[2], p1[3]));
+          else
+            *reinterpret_cast<float4*>(static_cast<float*>(seg.shadow) + li) = make_float4(p1[0], p1[1], p1[2], p1[3]);
+        }
       }
-      if (stats) {
-        add_stats(st, p0.x, p1.x, full); add_stats(st, p0.y, p1.y, full);
-        add_stats(st, p0.z, p1.z, full); add_stats(st, p0.w, p1.w, full);
+#pragma unroll
+      for (int k = 0; k < VN; ++k) {
+        if (stats) add_stats<R>(st, p0[k], p1[k], full);
+        am = fmaxf(am, fabsf(static_cast<float>(p1[k])));
       }
-      am = fmaxf(am, fmaxf(fmaxf(fabsf(p1.x), fabsf(p1.y)), fmaxf(fabsf(p1.z), fabsf(p1.w))));
     }
   } else {
 #pragma unroll
@@ -156,50 +198,54 @@ PZ_DEV void optimizer_block(const OptArgs& a, int block, bool full) {
       const int64_t li = local0 + static_cast<int64_t>(u) * kThreads + threadIdx.x;
       if (li >= seg.numel) break;
       const int64_t gi = seg.offset + li;
-      const float p0 = a.params[gi];
-      const float graw = seg.grad16 != nullptr ? bf2f(seg.grad16[li]) : a.grads[gi];
-      if (seg.zero_grad) a.grads[gi] = 0.f;
-      float m = 0.f, v = 0.f;
+      const R p0 = a.params[gi];
+      R graw;
+      if constexpr (VN == 4) graw = seg.grad16 != nullptr ? bf2f(seg.grad16[li]) : a.grads[gi];
+      else graw = a.grads[gi];
+      if (seg.zero_grad) a.grads[gi] = R(0);
+      R m = R(0), v = R(0);
       if constexpr (ADAM) {
         m = a.exp_avg[gi];
         v = a.exp_avg_sq[gi];
       }
-      const float p1 = update_one<ADAM>(a, p0, graw, l2x2, step_size, m, v);
+      const R p1 = update_one<ADAM, R>(a, p0, graw, l2x2, step_size, m, v);
       if constexpr (ADAM) {
         a.exp_avg[gi] = m;
         a.exp_avg_sq[gi] = v;
       }
       a.params[gi] = p1;
       if (seg.shadow != nullptr) {
-        if (seg.shadow_dtype == DT_BF16) static_cast<uint16_t*>(seg.shadow)[li] = f2bf(p1);
-        else static_cast<float*>(seg.shadow)[li] = p1;
+        if (seg.shadow_dtype == DT_BF16) static_cast<uint16_t*>(seg.shadow)[li] = f2bf(static_cast<float>(p1));
+        else static_cast<float*>(seg.shadow)[li] = static_cast<float>(p1);
       }
-      if (stats) add_stats(st, p0, p1, full);
-      am = fmaxf(am, fabsf(p1));
+      if (stats) add_stats<R>(st, p0, p1, full);
+      am = fmaxf(am, fabsf(static_cast<float>(p1)));
     }
   }
-  if (stats && a.stats != nullptr) block_reduce_add(st, a.stats + 4 * seg.stat_slot, full);
+  if (stats && args.stats != nullptr) block_reduce_add(st, args.stats + 4 * seg.stat_slot, full);
   if (seg.amax != nullptr) block_amax_commit(am, seg.amax);
 }
 
-template <bool ADAM>
+template <bool ADAM, typename R>
 __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   int epoch = -1;
   if (a.epoch_ptr != nullptr) epoch = *a.epoch_ptr;
   if (a.hp != nullptr) {
-    const float* h = a.hp + 4 * static_cast<int64_t>(epoch);
+    const double* h = a.hp + 4 * static_cast<int64_t>(epoch);
     a.lr = h[0];
     a.bias_c1 = h[1];
     a.bias_c2_sqrt = h[2];
   }
+  const OptView<R> view(a);
   const bool full = a.stats_every == 1 || (a.stats_every > 1 && (epoch < 0 || epoch % a.stats_every == 0));
   for (int b = blockIdx.x; b < a.total_blocks; b += gridDim.x) {
-    optimizer_block<ADAM>(a, b, full);
+    optimizer_block<ADAM, R>(a, view, b, full);
     __syncthreads();  // the block reductions reuse their LDS slots
   }
 }
 
-__global__ void __launch_bounds__(kThreads) segment_stats_kernel(const float* __restrict__ params,
+template <typename R>
+__global__ void __launch_bounds__(kThreads) segment_stats_kernel(const R* __restrict__ params,
                                                                  const OptSegment* segments, const int64_t* block_seg,
                                                                  int nseg, double* stats) {
   const int seg_id = find_segment(block_seg, nseg, blockIdx.x);
@@ -245,14 +291,20 @@ __global__ void step_finalize_kernel(FinalizeArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     double loss = 0.0;
-    if (a.loss != nullptr) {
+    if (a.loss64 != nullptr) {
+      for (int k = 0; k < a.loss_slots; ++k) {
+        loss += a.loss64[k];
+        a.loss64[k] = 0.0;  // ready for the next step's head
+      }
+      loss /= a.loss_div;
+    } else if (a.loss != nullptr) {
       for (int k = 0; k < a.loss_slots; ++k) {
         loss += static_cast<double>(a.loss[k]);
         a.loss[k] = 0.f;  // ready for the next step's head
       }
       loss /= a.loss_div;
     }
-    if (a.epoch < a.n_costs) a.costs[a.epoch] = static_cast<float>(loss + static_cast<double>(a.l2) * l2sum);
+    if (a.epoch < a.n_costs) a.costs[a.epoch] = loss + static_cast<double>(a.l2) * l2sum;
     if (a.epoch_ptr != nullptr) *a.epoch_ptr = a.epoch + 1;
   }
   __syncthreads();
@@ -275,16 +327,25 @@ hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
   }();
   const int cap = a.max_grid > 0 ? a.max_grid : max_grid;
   const int grid = cap > 0 && cap < a.total_blocks ? cap : a.total_blocks;
-  if (a.adam) hipLaunchKernelGGL(optimizer_kernel<true>, dim3(grid), dim3(kThreads), 0, s, a);
-  else hipLaunchKernelGGL(optimizer_kernel<false>, dim3(grid), dim3(kThreads), 0, s, a);
+  if (a.real == DT_F64) {
+    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, double>), dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((optimizer_kernel<false, double>), dim3(grid), dim3(kThreads), 0, s, a);
+  } else {
+    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float>), dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((optimizer_kernel<false, float>), dim3(grid), dim3(kThreads), 0, s, a);
+  }
   return hipGetLastError();
 }
 
-hipError_t segment_stats(const float* params, const OptSegment* segments, const int64_t* block_seg, int num_segments,
-                         int total_blocks, double* stats, hipStream_t s) {
+hipError_t segment_stats(const void* params, int real, const OptSegment* segments, const int64_t* block_seg,
+                         int num_segments, int total_blocks, double* stats, hipStream_t s) {
   if (total_blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL(segment_stats_kernel, dim3(total_blocks), dim3(kThreads), 0, s, params, segments, block_seg,
-                     num_segments, stats);
+  if (real == DT_F64)
+    hipLaunchKernelGGL(segment_stats_kernel<double>, dim3(total_blocks), dim3(kThreads), 0, s,
+                       static_cast<const double*>(params), segments, block_seg, num_segments, stats);
+  else
+    hipLaunchKernelGGL(segment_stats_kernel<float>, dim3(total_blocks), dim3(kThreads), 0, s,
+                       static_cast<const float*>(params), segments, block_seg, num_segments, stats);
   return hipGetLastError();
 }
 

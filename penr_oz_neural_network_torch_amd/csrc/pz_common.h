@@ -220,14 +220,16 @@ PZ_DEV double wave_sum_d(double v) {
 // tensor step (lerp_, mul_/addcmul_, sqrt/div/add_, addcdiv_); SGD = the reference's
 // `p -= lr * grad` (neural_net_model.py:496-507). g = graw * grad_scale + 2*l2*p0 (L2 term).
 // ------------------------------------------------------------------------------------------
-template <bool ADAM>
-PZ_DEV float opt_update(float p0, float graw, float grad_scale, float l2x2, float lr, float step_size, float beta1,
-                        float beta2, float bias_c2_sqrt, float eps, float& m, float& v) {
-  const float g = graw * grad_scale + l2x2 * p0;
+// R = float (fp32 masters) or double (fp64 models: torch.optim.Adam on fp64 tensors computes in
+// fp64; the hyper-parameters arrive as the host's doubles rounded to R)
+template <bool ADAM, typename R>
+PZ_DEV R opt_update(R p0, R graw, R grad_scale, R l2x2, R lr, R step_size, R beta1, R beta2, R bias_c2_sqrt, R eps,
+                    R& m, R& v) {
+  const R g = graw * grad_scale + l2x2 * p0;
   if constexpr (ADAM) {
-    m = m + (1.f - beta1) * (g - m);
-    v = v * beta2 + (1.f - beta2) * g * g;
-    const float denom = sqrtf(v) / bias_c2_sqrt + eps;
+    m = m + (R(1) - beta1) * (g - m);
+    v = v * beta2 + (R(1) - beta2) * g * g;
+    const R denom = sqrt(v) / bias_c2_sqrt + eps;
     return p0 - step_size * (m / denom);
   } else {
     return p0 - lr * g;

@@ -14,12 +14,14 @@ struct XentArgs {
   int rows, rows_valid, cols;
   int dtype;
   float* loss;          // += sum_rows (lse - x_label) * loss_scale   (may be null)
+  double* loss64;       // fp64 logits: the loss accumulates here instead (double)
   int loss_slots;       // > 1: block b adds into loss[b % loss_slots] (the consumer sums them)
   float loss_scale;
   void* dh;             // [rows][ld_dh] gradient wrt the pre-dropout logits (may be null)
   int64_t ld_dh;
   float grad_scale;     // usually 1/global_batch
   float* colsum;        // += column sums of dh (bias gradient), may be null
+  double* colsum64;     // fp64 logits: column sums in double instead
   void* probs;          // optional softmax output [rows][ld_probs]
   int64_t ld_probs;
   EpiSpec epi;          // logits' dropout (drop_pre); act must be NONE
@@ -34,12 +36,14 @@ struct MseArgs {
   int rows, rows_valid, cols;
   int dtype;
   float* loss;
+  double* loss64;       // fp64 outputs: double accumulators (loss64 / colsum64) instead
   int loss_slots;       // > 1: block b adds into loss[b % loss_slots]
   float loss_scale;     // 1 / numel
   void* dh;
   int64_t ld_dh;
   float grad_scale;     // 1 / numel
   float* colsum;
+  double* colsum64;
   EpiSpec epi;          // last stage's epilogue (derivative from y)
   int64_t idx_ld;
 };
@@ -74,7 +78,7 @@ hipError_t xent_head(const XentArgs& a, hipStream_t s);
 hipError_t mse_head(const MseArgs& a, hipStream_t s);
 hipError_t softmax_rows(const void* x, void* y, int dtype, int rows, int cols, hipStream_t s);
 hipError_t softmax_bwd(const void* g, const void* y, void* dx, int dtype, int rows, int cols, hipStream_t s);
-hipError_t colsum(const void* x, int dtype, float* out, int rows, int cols, hipStream_t s);
+hipError_t colsum(const void* x, int dtype, void* out, int out_dtype, int rows, int cols, hipStream_t s);
 hipError_t gather_rows(const GatherArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ optimizer (N6)
@@ -95,24 +99,28 @@ struct OptSegment {
 };
 
 struct OptArgs {
-  float* params;
-  float* grads;                // read; zero_grad segments are reset to 0
-  float* exp_avg;
-  float* exp_avg_sq;
+  // flat master buffers in the master precision `real` (DT_F32, or DT_F64 for fp64 models)
+  void* params;
+  void* grads;                 // read; zero_grad segments are reset to 0
+  void* exp_avg;
+  void* exp_avg_sq;
+  int real;
   const OptSegment* segments;  // device array
   int num_segments;
   const int64_t* block_seg;    // device array: first block index of each segment (+ total)
   int total_blocks;
   int adam;                    // 1 Adam, 0 SGD
-  float lr;
-  float beta1, beta2, eps;
-  float bias_c1, bias_c2_sqrt; // 1 - beta1^t, sqrt(1 - beta2^t)
-  float grad_scale;            // e.g. 1 / world_size
-  float l2_lambda;             // grad += 2*l2*w for weight segments
+  // hyper-parameters as the host's doubles (fp64 models update in fp64, like torch.optim.Adam on
+  // fp64 tensors; fp32 masters round them to float)
+  double lr;
+  double beta1, beta2, eps;
+  double bias_c1, bias_c2_sqrt; // 1 - beta1^t, sqrt(1 - beta2^t)
+  double grad_scale;           // e.g. 1 / world_size
+  double l2_lambda;            // grad += 2*l2*w for weight segments
   double* stats;               // per slot: sum(dw), sum(dw^2), sum(w), sum(w^2)  (accumulated)
   // graph-replayed steps: {lr, bias_c1, bias_c2_sqrt, -} of epoch *epoch_ptr from this table
   // (filled on the host for the whole run, so eager and replayed steps use identical values)
-  const float* hp;
+  const double* hp;
   const int* epoch_ptr;
   // update-ratio sums (sum dw, sum dw^2, sum w): 1 = this launch, 0 = not (only sum w^2, which the
   // next step's L2 cost term needs), k > 1 = when the device epoch (*epoch_ptr) % k == 0
@@ -122,12 +130,13 @@ struct OptArgs {
 
 constexpr int kOptElemsPerBlock = 4096;
 hipError_t optimizer_step(const OptArgs& a, hipStream_t s);
-// sum of squares of each weight segment (for the L2 term before the first update)
-hipError_t segment_stats(const float* params, const OptSegment* segments, const int64_t* block_seg, int num_segments,
+// sum of squares of each weight segment (for the L2 term before the first update); params of dtype `real`
+hipError_t segment_stats(const void* params, int real, const OptSegment* segments, const int64_t* block_seg, int num_segments,
                          int total_blocks, double* stats, hipStream_t s);
 
 struct FinalizeArgs {
   float* loss;              // accumulated loss (summed over ranks when data parallel); reset to 0
+  double* loss64;           // fp64 models: the double accumulators instead
   int loss_slots;           // loss[0..loss_slots) are summed (the heads spread their block adds)
   float loss_div;           // world size
   double* stats_prev;       // [nslots][4] stats of the weights used by this step (zeroed afterwards)
@@ -135,7 +144,7 @@ struct FinalizeArgs {
   const double* slot_numel; // [nslots]
   int nslots;
   float l2;
-  float* costs;             // costs[epoch]
+  double* costs;            // costs[epoch]
   int epoch;
   float* ratios;            // [rows][nslots]
   int ratio_row;            // -1: no progress point this epoch; -2: epoch % every == 0 ? epoch / every : -1

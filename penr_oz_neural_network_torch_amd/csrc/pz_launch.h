@@ -34,7 +34,7 @@ struct GemmOpt {
   int adam;
   double* stats;          // this weight's 4 accumulators: sum(dw), sum(dw^2), sum(w), sum(w^2)
   float* amax;            // optional: max |w_new| (fp8 weight scaling)
-  const float* hp;        // graph-replayed steps: {lr, bias_c1, bias_c2_sqrt, -} of epoch *epoch_ptr
+  const double* hp;       // graph-replayed steps: {lr, bias_c1, bias_c2_sqrt, -} of epoch *epoch_ptr
   const int* epoch_ptr;
   int stats_every;        // as OptArgs::stats_every
   float lr, beta1, beta2, eps, bias_c1, bias_c2_sqrt;
@@ -61,6 +61,10 @@ struct GemmArgs {
   int64_t ldaux;
   int aux_dtype;
   float* colsum;      // [N] fp32: atomically accumulates column sums of the final C values
+  // fp64 models (generic / wide paths only): the bias and the column sums in the master precision
+  // (used instead of bias / colsum when set) — the fp64 fused engine stays exact to fp64 rounding
+  const double* bias64;
+  double* colsum64;
   int epi_mode;
   EpiSpec epi;
   int64_t idx_ld;     // logical row stride used for dropout element indices (usually N)

@@ -83,16 +83,21 @@ struct Comm {
   hipEvent_t ready = nullptr;
   std::array<hipEvent_t, kRing> done{};
   int64_t next = 0;
+  bool closed = false;
+  // serialises all_reduce / wait / destroy on ONE communicator: ticket numbering and the event
+  // ring are shared state, and destroy must not free the comm under a running op
+  std::mutex mu;
   explicit Comm(c10::hip::HIPStream s) : stream(s) {}
 };
 
 std::mutex g_mu;
-std::vector<std::unique_ptr<Comm>> g_comms;
+std::vector<std::shared_ptr<Comm>> g_comms;
 
-Comm& get(int64_t h) {
+// shared ownership: a concurrent destroy drops the table's reference, the op in flight keeps its own
+std::shared_ptr<Comm> get(int64_t h) {
   std::lock_guard<std::mutex> lock(g_mu);
   TORCH_CHECK(h >= 0 && h < static_cast<int64_t>(g_comms.size()) && g_comms[h], "pz rccl: bad communicator handle");
-  return *g_comms[h];
+  return g_comms[h];
 }
 
 ncclDataType_t nccl_type(const at::Tensor& t) {
@@ -123,7 +128,7 @@ int64_t init_op(const at::Tensor& id, int64_t nranks, int64_t rank, bool high_pr
   std::memcpy(&uid, id.contiguous().data_ptr(), sizeof(uid));
   int dev = 0;
   PZ_HIP_OK(hipGetDevice(&dev));
-  auto c = std::make_unique<Comm>(c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(dev)));
+  auto c = std::make_shared<Comm>(c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(dev)));
   c->device = dev;
   c->nranks = static_cast<int>(nranks);
   PZ_NCCL_CHECK(api().init_rank(&c->comm, static_cast<int>(nranks), uid, static_cast<int>(rank)));
@@ -135,7 +140,10 @@ int64_t init_op(const at::Tensor& id, int64_t nranks, int64_t rank, bool high_pr
 }
 
 int64_t all_reduce_op(int64_t h, const at::Tensor& t) {
-  Comm& c = get(h);
+  const std::shared_ptr<Comm> cp = get(h);
+  Comm& c = *cp;
+  std::lock_guard<std::mutex> lock(c.mu);
+  TORCH_CHECK(!c.closed, "pz rccl: communicator destroyed");
   TORCH_CHECK(t.is_cuda() && t.device().index() == c.device, "pz rccl: tensor must live on the communicator's GPU");
   TORCH_CHECK(t.is_contiguous(), "pz rccl: contiguous buckets only");
   const int64_t ticket = c.next++;
@@ -155,7 +163,10 @@ int64_t all_reduce_op(int64_t h, const at::Tensor& t) {
 }
 
 void wait_op(int64_t h, int64_t ticket) {
-  Comm& c = get(h);
+  const std::shared_ptr<Comm> cp = get(h);
+  Comm& c = *cp;
+  std::lock_guard<std::mutex> lock(c.mu);
+  TORCH_CHECK(!c.closed, "pz rccl: communicator destroyed");
   TORCH_CHECK(ticket >= 0 && ticket < c.next && c.next - ticket <= kRing, "pz rccl: stale or unknown bucket ticket");
   ncclResult_t async = ncclSuccess;
   PZ_NCCL_CHECK(api().async_error(c.comm, &async));
@@ -165,12 +176,14 @@ void wait_op(int64_t h, int64_t ticket) {
 }
 
 void destroy_op(int64_t h) {
-  std::unique_ptr<Comm> c;
+  std::shared_ptr<Comm> c;
   {
     std::lock_guard<std::mutex> lock(g_mu);
     TORCH_CHECK(h >= 0 && h < static_cast<int64_t>(g_comms.size()) && g_comms[h], "pz rccl: bad communicator handle");
     c = std::move(g_comms[h]);
   }
+  std::lock_guard<std::mutex> lock(c->mu);  // waits for an op in flight on another thread
+  c->closed = true;
   PZ_HIP_OK(hipStreamSynchronize(c->stream.stream()));
   PZ_NCCL_CHECK(api().destroy(c->comm));
   hipEventDestroy(c->ready);

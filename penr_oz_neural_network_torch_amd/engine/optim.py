@@ -38,8 +38,9 @@ class FusedOptimizer:
         self.adam = torch_opt is not None
         dev = store.device
         n = store.numel
-        self.exp_avg = torch.zeros(n, device=dev, dtype=torch.float32) if self.adam else None
-        self.exp_avg_sq = torch.zeros(n, device=dev, dtype=torch.float32) if self.adam else None
+        dt = store.flat.dtype  # fp32 masters, or fp64 (fp64 models: torch.optim.Adam's fp64 state)
+        self.exp_avg = torch.zeros(n, device=dev, dtype=dt) if self.adam else None
+        self.exp_avg_sq = torch.zeros(n, device=dev, dtype=dt) if self.adam else None
         self.step_count = 0
         if self.adam:
             self._adopt_state()

@@ -14,7 +14,7 @@ HIP kernels with nothing on the host between epochs:
                 -> async RCCL all-reduce of that bucket (data parallel)
                 dX GEMM  (dZ Wᵀ with the previous stage's epilogue derivative + bias colsum fused)
                 | batchnorm_bwd | embedding_bwd
-    optimizer_step (one launch for all params, L2 + 1/world folded in, bf16 shadows refreshed)
+    optimizer_step (one launch for all params, L2 folded in, bf16 shadows refreshed)
     step_finalize  (cost[e], weight_upd_ratio row -> device arrays)
 
 Costs / ratios / progress timestamps are pulled off the device only in :meth:`drain` (end of
@@ -164,19 +164,26 @@ class FusedTrainer:
 
     def __init__(self, model, context: DataParallelContext | None = None):
         native.require()
-        if model.precision.master != torch.float32:
-            raise UnsupportedModel("fused engine needs fp32 master parameters")
+        if model._param_store is None or model._param_store.device.type != "cuda":
+            raise UnsupportedModel("CPU models train under autograd (the reference's own runtime)")
+        if model.precision.master not in (torch.float32, torch.float64):
+            raise UnsupportedModel("fused engine needs fp32 or fp64 master parameters")
         self.model = model
         self.store = model._param_store
         self.dev = self.store.device
-        self.compute = torch.bfloat16 if model.precision.name in ("bfloat16", "fp8") else torch.float32
+        # GEMM operand precision: bf16 (bf16 / fp8 policies, fp32 masters) or the master itself —
+        # fp32 (f32 MFMA) or fp64 (f64 MFMA: the reference's own precision, a REST model created
+        # with device="cuda" and no dtype); fp64 models also keep their gradients, Adam moments,
+        # loss and bias-gradient accumulators and costs in fp64
+        self.master = model.precision.master
+        self.compute = torch.bfloat16 if model.precision.name in ("bfloat16", "fp8") else self.master
         self.ctx = context or get_context()
         self.stages, self.head = compile_stages(model)
         for i, st in enumerate(self.stages):
             st.index = i
         # LOSS_SLOTS loss accumulators after the parameters (inside the exact fp32 DP bucket): the
         # head's blocks spread their adds over them, step_finalize sums them
-        self.grads = torch.zeros(self.store.numel + LOSS_SLOTS, device=self.dev, dtype=torch.float32)
+        self.grads = torch.zeros(self.store.numel + LOSS_SLOTS, device=self.dev, dtype=self.master)
         self.loss_slot = self.grads[self.store.numel:self.store.numel + LOSS_SLOTS]
         # low-precision GEMM copies of the weights, PING-PONG: step t's GEMMs read set `parity`
         # while its optimizer writes set 1-parity — so a weight can be updated as soon as its
@@ -184,7 +191,7 @@ class FusedTrainer:
         self.shadow_sets: list[dict[int, torch.Tensor]] = [{}, {}]
         self.parity = 0
         for st in self.stages:
-            if st.kind == "gemm" and self.compute != torch.float32:
+            if st.kind == "gemm" and self.compute != self.master:
                 for sset in self.shadow_sets:
                     sset[st.seg_w.offset] = torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute)
         # Data parallel: dense weight gradients are written by the dW GEMMs straight in bf16 and
@@ -308,6 +315,7 @@ class FusedTrainer:
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
         self._ov = None
         self._rows = None
+        self._gbatch = 1           # global sample size of the current step (all ranks)
         # hipGraph replay of whole steps (single GPU) when a step is launch-bound: PZ_GRAPHS=auto
         # (default: steps under GRAPH_MAX_FLOP), 1 (always), 0 (never)
         mode = os.environ.get("PZ_GRAPHS", "auto")
@@ -335,13 +343,14 @@ class FusedTrainer:
         inputs = [inp for inp, _ in data]
         targets = [tgt for _, tgt in data]
         first = self.stages[0]
+        host = torch.float64 if self.master == torch.float64 else torch.float32  # fp64 models: exact inputs
         if first.kind == "embed":
             x = torch.tensor(inputs, dtype=torch.float32)
             if x.dim() == 1:
                 x = x.unsqueeze(1)
             self.block = x.shape[1]
         else:
-            x = torch.tensor(inputs, dtype=torch.float32).reshape(len(inputs), -1)
+            x = torch.tensor(inputs, dtype=host).reshape(len(inputs), -1)
             self.block = 1
         lab = torch.tensor([int(t[0]) for t in targets], dtype=torch.int64) if self.head == "softmax" else None
         self._validate(x, lab)
@@ -350,7 +359,7 @@ class FusedTrainer:
             self.labels = lab.to(self.dev)
             self.targets = None
         else:
-            self.targets = torch.tensor(targets, dtype=torch.float32).reshape(len(targets), -1).to(self.dev)
+            self.targets = torch.tensor(targets, dtype=host).reshape(len(targets), -1).to(self.dev)
             self.labels = None
         seed = torch.randint(0, 2 ** 62, (1,)).item()
         self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
@@ -380,13 +389,14 @@ class FusedTrainer:
         softmax head, ``[N, out]`` regression targets otherwise.
         """
         self._validate(inputs, targets.reshape(-1) if self.head == "softmax" else None)
-        self.data = self._table(inputs.to(dtype=torch.float32))
+        host = torch.float64 if self.master == torch.float64 and self.stages[0].kind != "embed" else torch.float32
+        self.data = self._table(inputs.to(dtype=host))
         self.block = self.data.shape[1] if self.stages[0].kind == "embed" else 1
         if self.head == "softmax":
             self.labels = targets.reshape(-1).to(device=self.dev, dtype=torch.int64).contiguous()
             self.targets = None
         else:
-            self.targets = targets.to(device=self.dev, dtype=torch.float32).reshape(len(targets), -1).contiguous()
+            self.targets = targets.to(device=self.dev, dtype=self.master).reshape(len(targets), -1).contiguous()
             self.labels = None
         seed = torch.randint(0, 2 ** 62, (1,)).item() if seed is None else seed
         self.base_seed = (seed & 0xFFFFFFFF, (seed >> 32) & 0xFFFFFFFF)
@@ -634,7 +644,7 @@ class FusedTrainer:
             else:
                 rows.append((lr, 1.0, 1.0, 0.0))
         self._plan = {"epochs": epochs, "every": every, "t0": t0, "lrs": lrs,
-                      "hp": torch.tensor(rows or [(0.0, 1.0, 1.0, 0.0)], dtype=torch.float32, device=self.dev)}
+                      "hp": torch.tensor(rows or [(0.0, 1.0, 1.0, 0.0)], dtype=torch.float64, device=self.dev)}
 
     def _graphs_possible(self) -> bool:
         # single GPU only (collectives are not captured); no per-phase host syncs (PZ_DEBUG_SYNC)
@@ -657,11 +667,15 @@ class FusedTrainer:
         weight-shadow parity into a hipGraph and replayed: the epoch-dependent values (dropout
         keys, sampler seeds, optimizer hyper-parameters, cost slot, ratio row) are then read from
         the device epoch counter, which every step advances in ``step_finalize``."""
-        world = self.ctx.world_size
+        world, rank = self.ctx.world_size, self.ctx.rank
         if sample_size < world:
             raise ValueError(f"sample size {sample_size} is smaller than the {world} data-parallel ranks")
-        # weak sharding: every rank draws sample_size // world rows (the remainder is not drawn)
-        batch = sample_size // world
+        # the global sample is split exactly (reference :441, 460 draw sample_size rows): rank r
+        # draws rows [r*S/W, (r+1)*S/W), the first S % W ranks one more. Every rank scales its
+        # loss and gradients by 1/S (the GLOBAL sample), so the all-reduced sum is the global mean
+        # with no 1/world factor — unequal shards weigh exactly by their share
+        batch = (rank + 1) * sample_size // world - rank * sample_size // world
+        self._gbatch = sample_size
         self._ensure_buffers(batch)
         if not hasattr(self, "costs") or epoch >= self.costs.numel():
             self._alloc_progress(epoch + 1)
@@ -679,7 +693,7 @@ class FusedTrainer:
                      and epoch < plan["epochs"]
                      and want_ratios == (epoch % plan["every"] == 0) and lr == plan["lrs"][epoch]
                      and (not self.opt.adam or self.opt.step_count == plan["t0"] + epoch))
-        gkey = (self.parity, batch, float(dropout), float(l2))
+        gkey = (self.parity, batch, sample_size, float(dropout), float(l2))
         if graphable and gkey in self._warm:
             self._replay(gkey, epoch, lr, batch, dropout, l2, row)
         else:
@@ -723,7 +737,6 @@ class FusedTrainer:
              indices: torch.Tensor | None) -> None:
         """Enqueue one step. ``epoch=None``: hipGraph capture (epoch-dependent values from the
         device counter / tables; the side stream joins the capture stream at the end)."""
-        world = self.ctx.world_size
         capture = epoch is None
         keys = self._keys(epoch)
         ops = torch.ops.pz
@@ -734,7 +747,7 @@ class FusedTrainer:
         if overlap:
             if not capture:
                 self.opt.begin_step(lr)
-            self._ov = (main, l2, 1.0 / world)
+            self._ov = (main, l2, 1.0)  # gradients arrive as the global mean (1/S-scaled heads)
             self._late_stages, self._late_handles = [], []
             self._side_pending = []
 
@@ -823,7 +836,7 @@ class FusedTrainer:
                 self._side_pending = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
-            self.opt.step_group("rest", self.grads, l2, 1.0 / world, 1 - self.parity)
+            self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
             if self.fp8:
                 for st in self._late_stages:
                     self._refresh_fp8_weights(st, 1 - self.parity)
@@ -835,12 +848,12 @@ class FusedTrainer:
                 for key, hs, stages in self._deferred:  # PZ_OPT_DEFER
                     for h in hs:
                         self.ctx.wait_one(h)
-                    self.opt.step_group(key, self.grads, l2, 1.0 / world, 1 - self.parity)
+                    self.opt.step_group(key, self.grads, l2, 1.0, 1 - self.parity)
                     if self.fp8:
                         for st in stages:
                             self._refresh_fp8_weights(st, 1 - self.parity)
                 self._deferred = []
-                self.opt.finalize(self.loss_slot, world, l2, self.costs, -1 if capture else epoch, self.ratios, row,
+                self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
                 ev = torch.cuda.Event(enable_timing=not capture)
                 ev.record(self.opt_stream)
@@ -860,11 +873,11 @@ class FusedTrainer:
         self.ctx.wait_all(handles)
         if record:
             self._finish_record(rec, batch, l2)
-        self.opt.step(self.grads, lr, l2, 1.0 / world, 1 - self.parity)
+        self.opt.step(self.grads, lr, l2, 1.0, 1 - self.parity)
         self.parity = 1 - self.parity
         if self.fp8:
             self._refresh_fp8_weights(parity=self.parity)
-        self.opt.finalize(self.loss_slot, world, l2, self.costs, epoch, self.ratios, row, **fin)
+        self.opt.finalize(self.loss_slot, 1, l2, self.costs, epoch, self.ratios, row, **fin)
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         self._last_event = ev
@@ -958,7 +971,7 @@ class FusedTrainer:
             return
         torch.ops.pz.batchnorm_fwd(*args, 1, 0)
         self.ctx.all_reduce_(st.buffers["partial"])
-        torch.ops.pz.batchnorm_fwd(*args, 2, batch * st.pos_out * self.ctx.world_size)
+        torch.ops.pz.batchnorm_fwd(*args, 2, self._gbatch * st.pos_out)  # rows of the global sample
 
     def _scratch(self, key, like):
         buf = getattr(self, "_scratch_bufs", None)
@@ -981,14 +994,16 @@ class FusedTrainer:
         n = self.model.layers
         if self.head == "softmax":
             probs = self._scratch(("probs",), y) if rec is not None else None
-            ops.xent_head(y, self.lab, batch, self.loss_slot, 1.0 / batch, g, 1.0 / batch,
+            gb = self._gbatch  # loss and gradient of the GLOBAL mean (this rank's share of it)
+            ops.xent_head(y, self.lab, batch, self.loss_slot, 1.0 / gb, g, 1.0 / gb,
                           bias_grad if fuse else None, probs, ei, ef, 0)
             if rec is not None:
                 rec[len(n) - 1] = probs[:batch]
                 rec[("grad", len(n) - 2)] = g[:batch]
         else:
             cols = y.shape[1]
-            ops.mse_head(y, self.tgt, batch, self.loss_slot, 1.0 / (batch * cols), g, 1.0 / (batch * cols),
+            gn = self._gbatch * cols
+            ops.mse_head(y, self.tgt, batch, self.loss_slot, 1.0 / gn, g, 1.0 / gn,
                          bias_grad if fuse else None, ei, ef, 0)
             if rec is not None:
                 rec[("grad", len(n) - 1)] = g[:batch]
@@ -1027,7 +1042,7 @@ class FusedTrainer:
             else:  # synchronised: local parameter grads, then dx from the global sums
                 ops.batchnorm_bwd(*bargs, 1, 0)
                 self.ctx.all_reduce_(st.buffers["partial"])
-                ops.batchnorm_bwd(*bargs, 2, rows_valid * self.ctx.world_size)
+                ops.batchnorm_bwd(*bargs, 2, self._gbatch * st.pos_out)
             del layer
             if rec is not None and before is not None:
                 rec[("grad", before.layers[-1])] = dx[:batch * st.pos_in]
@@ -1157,19 +1172,18 @@ class FusedTrainer:
             gi = rec.get(("grad", i))
             grads.append(gi.detach().clone() if gi is not None else None)
         wgrads = []
-        world = self.ctx.world_size
         for i, layer in enumerate(self.model.layers):
             seg = self.store.segment_for(i, "weights") if layer.weights is not None else None
             if seg is None:
                 wgrads.append(None)
                 continue
-            gview = self._w_grad(seg).float() / world
+            gview = self._w_grad(seg).to(self.master)  # the all-reduced sum is the global mean already
             wgrads.append(gview + (2.0 * l2) * self.store.view(seg))
         self._record = {"activations": acts, "act_grads": grads, "weight_grads": wgrads}
 
     def _alloc_progress(self, epochs: int) -> None:
         points = math.ceil(epochs / max(1, epochs // 100)) + 1
-        self.costs = torch.zeros(max(epochs, 1), device=self.dev, dtype=torch.float32)
+        self.costs = torch.zeros(max(epochs, 1), device=self.dev, dtype=torch.float64)
         self.ratios = torch.zeros(points * max(1, self.opt.nslots), device=self.dev, dtype=torch.float32)
         self._ratio_rows = 0
         self._pending = []

@@ -27,14 +27,15 @@ def _on_gpu(t: Tensor | None) -> bool:
     return t is not None and t.is_cuda
 
 
-# Data-parallel context whose ranks SHARE batchnorm statistics while set (``_train_autograd``
-# sets it for world size > 1): synchronised batchnorm, the global batch is normalised as one
-_BN_SYNC = None
-
-
-def set_bn_sync(ctx) -> None:
-    global _BN_SYNC
-    _BN_SYNC = ctx if ctx is not None and ctx.enabled else None
+def set_bn_sync(layers, ctx) -> None:
+    """Synchronised batchnorm for ONE model's layers: while ``ctx`` (a data-parallel context with
+    world size > 1) is set on its BatchNormLayers, their training forward normalises the global
+    batch (statistics all-reduced over the ranks). Per layer instance, never process-wide: the
+    REST service trains other models in other threads at the same time."""
+    sync = ctx if ctx is not None and ctx.enabled else None
+    for layer in layers:
+        if isinstance(layer, BatchNormLayer):
+            layer.sync = sync
 
 
 def _pf():
@@ -177,6 +178,7 @@ class BatchNormLayer(Layer):
         self.bias = torch.zeros(dim_size, dtype=torch.float64) if have else None
         self.variance = torch.ones(dim_size, dtype=torch.float64) if have else None
         self.mean = torch.zeros(dim_size, dtype=torch.float64) if have else None
+        self.sync = None  # data-parallel context of a synchronised training run (set_bn_sync)
 
     @property
     def params(self) -> list[Tensor]:
@@ -202,7 +204,7 @@ class BatchNormLayer(Layer):
         return {"params": [ref(p) for p in self.params], "eps": self.eps, "momentum": self.momentum}
 
     def forward(self, input_tensor: Tensor) -> Tensor:
-        sync = _BN_SYNC if self.training else None
+        sync = self.sync if self.training else None
         if _on_gpu(self.gain):
             y, rm, rv = _pf().batchnorm(input_tensor, self.gain, self.bias, self.mean, self.variance, self.eps,
                                         self.momentum, self.training, sync=sync)

@@ -361,12 +361,12 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         ctx = context or self._dp_context()
         world, rank = ctx.world_size, ctx.rank
         from . import layers as _layers
-        _layers.set_bn_sync(ctx if world > 1 else None)  # synchronised batchnorm statistics
+        _layers.set_bn_sync(self.layers, ctx if world > 1 else None)  # synchronised batchnorm statistics
         try:
             self._autograd_epochs(data, epochs, learning_rate, sample_size, decay_rate, dropout_rate, l2_lambda,
                                   ctx, sampler)
         finally:
-            _layers.set_bn_sync(None)
+            _layers.set_bn_sync(self.layers, None)
 
     def _autograd_epochs(self, data, epochs, learning_rate, sample_size, decay_rate, dropout_rate, l2_lambda, ctx,
                          sampler):

@@ -144,10 +144,10 @@ class _Linear(torch.autograd.Function):
         wc = w if w.dtype == x2.dtype else w.to(x2.dtype)
         wc = wc.contiguous()
         out = torch.empty(x2.shape[0], wc.shape[1], device=x.device, dtype=x2.dtype)
-        bias32 = None
-        if b is not None:
-            bias32 = b.detach().float().contiguous()
-        gemm(x2, True, wc, False, out, bias=bias32)
+        bias_k = None
+        if b is not None:  # fp64 models add the fp64 bias (the kernels take fp32 or fp64)
+            bias_k = b.detach().to(torch.float64 if x2.dtype == torch.float64 else torch.float32).contiguous()
+        gemm(x2, True, wc, False, out, bias=bias_k)
         ctx.save_for_backward(x2, wc)
         ctx.has_bias = b is not None
         ctx.w_dtype = w.dtype
@@ -170,11 +170,10 @@ class _Linear(torch.autograd.Function):
             gemm(x2, False, g2, False, gw)  # dW = X^T @ dY (K = batch)
             gw = gw.to(ctx.w_dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = torch.zeros(wc.shape[1], device=wc.device, dtype=torch.float32)
+            acc = torch.float64 if x2.dtype == torch.float64 else torch.float32  # fp64 models stay fp64
+            gb = torch.zeros(wc.shape[1], device=wc.device, dtype=acc)
             _ops().colsum(g2, gb)
             gb = gb.to(ctx.b_dtype)
-            if x2.dtype == torch.float64:  # keep fp64 exactness for fp64 models
-                gb = g2.sum(0).to(ctx.b_dtype)
         return gx, gw, gb
 
 
@@ -261,7 +260,7 @@ class _CrossEntropy(torch.autograd.Function):
         check_index_range(labels.reshape(-1), 0, l2.shape[-1], "Target")
         lab = labels.reshape(-1).to(device=l2.device, dtype=torch.int64).contiguous()
         rows = l2.shape[0]
-        loss = torch.zeros(1, device=l2.device, dtype=torch.float32)
+        loss = torch.zeros(1, device=l2.device, dtype=torch.float64 if l2.dtype == torch.float64 else torch.float32)
         dh = torch.empty_like(l2)
         _ops().xent_head(l2, lab, rows, loss, 1.0 / rows, dh, 1.0 / rows, None, None, NO_EPI[0], NO_EPI[1], 0)
         ctx.save_for_backward(dh)
@@ -286,7 +285,7 @@ class _Mse(torch.autograd.Function):
         y2 = y.reshape(-1, shape[-1] if y.dim() > 0 else 1).contiguous()
         t2 = target.to(y.dtype).reshape(y2.shape).contiguous()
         n = y2.numel()
-        loss = torch.zeros(1, device=y.device, dtype=torch.float32)
+        loss = torch.zeros(1, device=y.device, dtype=torch.float64 if y2.dtype == torch.float64 else torch.float32)
         dh = torch.empty_like(y2)
         _ops().mse_head(y2, t2, y2.shape[0], loss, 1.0 / n, dh, 1.0 / n, None, NO_EPI[0], NO_EPI[1], 0)
         ctx.save_for_backward(dh)

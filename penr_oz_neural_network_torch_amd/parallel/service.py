@@ -1,33 +1,34 @@
 """Multi-GPU data-parallel training behind the REST service (reference ``main.py:281-298``).
 
 The reference trains in one worker thread of one process (``run_in_threadpool(model.train, ...)``).
-Here the server process becomes **rank 0 of an N-rank group**: at startup it spawns N-1 worker
-processes (one per further GPU, before this process touches the GPU) and joins them in one
+Here the server process drives an **N-rank train group of its own child processes**: at startup
+it spawns N rank processes (rank r on GPU r; before this process touches the GPU) that join one
 ``torch.distributed`` process group — RCCL over xGMI for GPU models (``gloo`` when rehearsing on
-the CPU). A ``PUT /train/`` on a GPU model then runs on every rank:
+the CPU). The server itself never joins the group, so no collective state ever lives in the
+process that serves HTTP. A ``PUT /train/`` on a GPU model then runs on every rank:
 
-    rank 0 (train thread)                       ranks 1..N-1 (parallel/worker.py)
-    ─────────────────────                       ─────────────────────────────────
-    send {"op": "load", model_id, data, hp} ──► deserialize model_<id> from the shared models/ dir
-                                            ◄── "ok" | error text
-    send "go" (or "abort" if any rank failed)──►
-    model.train(data, **hp) ◄═══ RCCL ═══►      model.train(data, **hp)  (same data, own GPU)
-    (writes the checkpoints: rank 0 only)   ◄── "done" | "failed: ..."
+    server (train thread)                         ranks 0..N-1 (parallel/worker.py)
+    ─────────────────────                         ─────────────────────────────────
+    send {"op": "load", model_id, data, hp} ────► deserialize model_<id> from the shared models/ dir
+                                              ◄── "ok" | error text
+    send "go" (or "abort" if any rank failed) ──►
+    wait, watching the processes                  model.train(data, **hp) ◄═ RCCL ═► (every rank)
+                                              ◄── "done" | "failed: ..."   (rank 0 writes the files)
 
 Inside ``train`` the fused engine shards every epoch's minibatch over the ranks and all-reduces
 the gradient buckets during backward (:mod:`.dist`, :class:`..engine.trainer.FusedTrainer`); the
-model writes its files on rank 0 only. Commands travel on a local authenticated socket, not on the
-process group, so idle workers block on ``recv`` without a collective timeout. One group training
-runs at a time (the group's lock); the process-wide default context stays world size 1, so CPU
-models and inference in the server never issue collectives.
+model writes its checkpoints on rank 0 only, and ``/progress/`` reads them as for any model.
+Commands travel on a local authenticated socket, not on the process group, so idle ranks block
+on ``recv`` without a collective timeout. One group training runs at a time (the group's lock).
 
-Failure handling: a watchdog thread polls the worker processes. A worker that dies
-marks the group lost; if a training is in flight, the default process group is aborted so rank 0's
-pending collectives fail instead of waiting out the collective timeout. A training whose workers
-do not report back (lost worker, rank 0 failed while the others wait in a collective) tears the
-group down (workers killed); the next ``train`` brings a fresh group up (new workers, new
-rendezvous) before it runs. A failure every rank reports cleanly (e.g. a bad request) keeps the
-group. ``status()`` exposes ``lost`` and ``restarts``.
+Failure handling: a watchdog thread polls the rank processes. A rank that exits
+marks the group lost; a training in flight then fails at once — the server stops waiting, kills
+every rank of that group (the survivors may be stuck in a collective) and, since rank 0 may have
+died with it, rewrites the checkpoint's status as ``"Failed"`` itself (no GPU involved). The next
+``train`` brings a fresh group up: new processes, a new file rendezvous in a fresh directory,
+a new process group — nothing is re-initialised inside a process whose group was aborted. Ranks
+that do not answer a command within ``timeout_s`` count as lost too. A failure every rank reports
+cleanly (e.g. a bad request) keeps the group. ``status()`` exposes ``lost`` and ``restarts``.
 
 Configuration: ``PZ_SERVICE_GPUS`` = unset / ``1`` (reference behaviour: no group), ``auto`` (every
 visible GPU) or N. ``PZ_DIST_BACKEND`` overrides the backend (``gloo`` for CPU rehearsals).
@@ -37,8 +38,10 @@ from __future__ import annotations
 import logging
 import os
 import secrets
+import shutil
 import subprocess
 import sys
+import tempfile
 import threading
 import time
 from multiprocessing.connection import Listener
@@ -59,7 +62,7 @@ def requested_world() -> int:
 
 
 class TrainGroup:
-    """Rank 0's handle on the worker ranks (see module docstring)."""
+    """The server's handle on its rank processes (see module docstring)."""
 
     def __init__(self, world: int, backend: str | None = None, timeout_s: float = 600.0):
         import torch
@@ -70,69 +73,63 @@ class TrainGroup:
         self._lock = threading.Lock()
         self._ready = threading.Event()
         self._error: str | None = None
-        self.ctx = None
         self.trainings = 0   # group trainings completed on every rank
         self.restarts = 0    # fresh groups brought up after a failure
         self.conns: list = []
         self.procs: list[subprocess.Popen] = []
-        self._lost: str | None = None      # why the current group is unusable (worker exit, no reply)
+        self._lost: str | None = None      # why the current group is unusable (rank exit, no reply)
         self._in_flight = False
         self._stopping = False
+        self._rdv_dir: str | None = None
         self._start()
         threading.Thread(target=self._watch, name="pz-train-watchdog", daemon=True).start()
 
     # ---------------------------------------------------------------------------------------
     def _start(self) -> None:
-        import socket
-        with socket.socket() as s:
-            s.bind(("127.0.0.1", 0))
-            master_port = s.getsockname()[1]
+        # one generation of the group: its own control socket, its own rendezvous directory (a
+        # file store: no TCP port picked here that someone else could take first)
+        self._rdv_dir = tempfile.mkdtemp(prefix="pz_group_")
         key = secrets.token_bytes(16)
         self._listener = Listener(("127.0.0.1", 0), authkey=key)
         models_dir = os.path.abspath(os.environ.get("PZ_MODELS_DIR", "models"))
-        base = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master_port), WORLD_SIZE=str(self.world),
+        base = dict(os.environ, MASTER_ADDR="127.0.0.1", WORLD_SIZE=str(self.world),
                     LOCAL_WORLD_SIZE=str(self.world), PZ_DIST_BACKEND=self.backend, PZ_MODELS_DIR=models_dir,
+                    PZ_RENDEZVOUS_FILE=os.path.join(self._rdv_dir, "store"),
                     PZ_CTRL_ADDR="%s:%d" % self._listener.address, PZ_CTRL_KEY=key.hex())
         base.pop("PZ_SERVICE_GPUS", None)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         base["PYTHONPATH"] = root + (os.pathsep + base["PYTHONPATH"] if base.get("PYTHONPATH") else "")
-        # workers first: this process must not have initialised the GPU when they are started
-        for r in range(1, self.world):
+        for r in range(self.world):
             env = dict(base, RANK=str(r), LOCAL_RANK=str(r))
             self.procs.append(subprocess.Popen([sys.executable, "-m", "penr_oz_neural_network_torch_amd.parallel.worker"],
                                                env=env, cwd=os.getcwd()))
-        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master_port))
-        threading.Thread(target=self._join, name="pz-train-group", daemon=True).start()
+        threading.Thread(target=self._join, args=(self._listener, self.procs), name="pz-train-group",
+                         daemon=True).start()
 
-    def _join(self) -> None:
-        """Rendezvous (blocks until every worker has imported torch and connected)."""
+    def _join(self, listener, procs) -> None:
+        """Rendezvous: every rank connects, then reports "ready" once its process group is up."""
         try:
-            from datetime import timedelta
-
-            import torch
-            import torch.distributed as dist
-
-            from .dist import DataParallelContext, set_context
             conns: dict[int, object] = {}
-            while len(conns) < self.world - 1:
-                c = self._listener.accept()
-                rank = c.recv()
-                conns[int(rank)] = c
-            self.conns = [conns[r] for r in sorted(conns)]
-            set_context(DataParallelContext())  # everything else in this process stays single-rank
-            if self.backend == "nccl":
-                torch.cuda.set_device(0)
-            dist.init_process_group(self.backend, rank=0, world_size=self.world,
-                                    timeout=timedelta(seconds=self.timeout_s))
-            comm = os.environ.get("PZ_GRAD_COMM_DTYPE")
-            comm_dtype = torch.bfloat16 if comm in ("bf16", "bfloat16") else None
-            self.ctx = DataParallelContext(0, self.world, None, comm_dtype)
-            log.info(f"data-parallel train group up: {self.world} ranks over {self.backend}")
-        except Exception as e:  # pragma: no cover - environment failures
-            self._error = repr(e)
-            log.exception("train group rendezvous failed")
+            while len(conns) < self.world:
+                c = listener.accept()
+                conns[int(c.recv())] = c
+            ordered = [conns[r] for r in range(self.world)]
+            for r, c in enumerate(ordered):
+                if not c.poll(self.timeout_s):
+                    raise RuntimeError(f"rank {r} did not join the process group")
+                msg = c.recv()
+                if msg != "ready":
+                    raise RuntimeError(f"rank {r}: {msg}")
+            if procs is self.procs:
+                self.conns = ordered
+                log.info(f"data-parallel train group up: {self.world} ranks over {self.backend}")
+        except Exception as e:  # rendezvous failure, or the listener closed by a teardown
+            if procs is self.procs:
+                self._error = repr(e)
+                log.exception("train group rendezvous failed")
         finally:
-            self._ready.set()
+            if procs is self.procs:
+                self._ready.set()
 
     # ---------------------------------------------------------------------------------------
     @property
@@ -146,28 +143,17 @@ class TrainGroup:
                 "lost": self._lost, "restarts": self.restarts}
 
     def _watch(self) -> None:
-        """Worker-exit watchdog: mark the group lost; abort in-flight collectives on rank 0."""
+        """Rank-exit watchdog: mark the group lost (an in-flight training notices at once)."""
         while not self._stopping:
             gen = self.procs  # the list object is replaced on restart: ignore exits of a torn-down group
-            for r, p in enumerate(list(gen), 1):
+            for r, p in enumerate(list(gen)):
                 if p.poll() is not None and self._lost is None and not self._stopping and gen is self.procs:
-                    self._lost = f"worker rank {r} exited with code {p.returncode}"
+                    self._lost = f"rank {r} exited with code {p.returncode}"
                     log.error("data-parallel group lost: %s", self._lost)
-                    if self._in_flight:
-                        self._abort_collectives()
             time.sleep(0.2)
 
-    def _abort_collectives(self) -> None:
-        try:
-            import torch.distributed as dist
-            from torch.distributed.distributed_c10d import _abort_process_group
-            if dist.is_initialized():
-                _abort_process_group()
-        except Exception:  # gloo: the dead peer's sockets already fail the pending collectives
-            log.debug("process group abort unavailable", exc_info=True)
-
     def _teardown(self) -> None:
-        """Stop (or kill) the workers and drop the process group (failure path and shutdown)."""
+        """Stop the ranks (cleanly, or killed when the group is lost) and drop this generation."""
         lost = self._lost is not None
         for c in self.conns:
             try:
@@ -183,16 +169,14 @@ class TrainGroup:
                 p.wait(timeout=30)
             except subprocess.TimeoutExpired:  # pragma: no cover
                 p.kill()
-        try:
-            import torch.distributed as dist
-            if self._ready.is_set() and self._error is None and dist.is_initialized():
-                dist.destroy_process_group()
-        except Exception:  # pragma: no cover - an aborted group may refuse a clean destroy
-            log.debug("destroy_process_group after failure", exc_info=True)
+                p.wait()
         self._listener.close()
+        if self._rdv_dir is not None:
+            shutil.rmtree(self._rdv_dir, ignore_errors=True)
+            self._rdv_dir = None
 
     def restart(self) -> None:
-        """Replace a lost group: kill what is left of it, spawn fresh workers, rendezvous again."""
+        """Replace a lost group by a fresh generation of rank processes."""
         log.warning("restarting the data-parallel train group (%s)", self._lost or self._error)
         self._lost = self._lost or "restart"
         self._teardown()
@@ -207,6 +191,36 @@ class TrainGroup:
     def wait_ready(self, timeout: float | None = None) -> bool:
         return self._ready.wait(timeout) and self._error is None
 
+    def _collect(self, timeout: float | None) -> list:
+        """One reply per rank; ``None`` for a rank that did not answer (closed, or ``timeout`` s
+        passed). Stops early once the watchdog marks the group lost."""
+        out: list = [None] * len(self.conns)
+        waiting = set(range(len(self.conns)))
+        deadline = None if timeout is None else time.monotonic() + timeout
+        while waiting and self._lost is None:
+            for r in sorted(waiting):
+                c = self.conns[r]
+                try:
+                    if c.poll(0.05):
+                        out[r] = c.recv()
+                        waiting.discard(r)
+                except (EOFError, OSError):
+                    waiting.discard(r)
+            if deadline is not None and time.monotonic() > deadline:
+                break
+        return out
+
+    def _lose(self, why: str, model_id: str | None = None) -> None:
+        self._lost = self._lost or why
+        log.error("data-parallel training lost its group: %s", self._lost)
+        self._teardown()
+        if model_id is not None:  # rank 0 owned the files and may have died with the group
+            try:
+                from ..utils import checkpoint as ckpt
+                ckpt.set_status(model_id, "Failed")
+            except Exception:  # pragma: no cover - keep the original failure
+                log.exception(f"could not mark model {model_id} failed")
+
     def train(self, model, data, hp: dict) -> None:
         """Run ``model.train(data, **hp)`` on every rank (called from the service's train thread)."""
         with self._lock:
@@ -215,45 +229,46 @@ class TrainGroup:
             if not self.wait_ready(self.timeout_s):
                 raise RuntimeError(f"data-parallel train group unavailable: {self._error or 'rendezvous timeout'}")
             if not self.healthy:
-                raise RuntimeError(f"data-parallel train group lost: {self._lost or 'a worker process has exited'}")
+                raise RuntimeError(f"data-parallel train group lost: {self._lost or 'a rank process has exited'}")
             cmd = {"op": "load", "model_id": model.model_id, "data": data, "hp": hp}
             for c in self.conns:
                 c.send(cmd)
-            replies = [c.recv() for c in self.conns]
-            failed = [f"rank {r + 1}: {m}" for r, m in enumerate(replies) if m != "ok"]
+            replies = self._collect(self.timeout_s)  # a rank stuck in deserialize must not hang us
+            if self._lost is not None or any(m is None for m in replies):
+                self._lose("a rank did not answer the load command")
+                raise RuntimeError(f"data-parallel train group lost: {self._lost}")
+            failed = [f"rank {r}: {m}" for r, m in enumerate(replies) if m != "ok"]
             for c in self.conns:
                 c.send("abort" if failed else "go")
             if failed:
-                raise RuntimeError("data-parallel workers could not load the model: " + "; ".join(failed))
-            model._context = self.ctx
-            err = None
+                raise RuntimeError("data-parallel ranks could not load the model: " + "; ".join(failed))
             self._in_flight = True
             try:
-                model.train(data, **hp)
-            except Exception as e:
-                err = e
+                results = self._collect(None)  # until every rank reported, or the group is lost
             finally:
-                model._context = None
                 self._in_flight = False
-            # workers report "done" / "failed: ..."; no reply (dead worker, or workers stuck in a
-            # collective rank 0 left) means the group is unusable: tear it down now
-            results = []
-            for c in self.conns:
-                wait = self.timeout_s if err is None else 15.0
-                try:
-                    results.append(c.recv() if c.poll(wait) else None)
-                except (EOFError, OSError):
-                    results.append(None)
-            if any(m is None for m in results) or self._lost is not None:
-                self._lost = self._lost or "a worker did not report the end of the training"
-                log.error("data-parallel training lost its group: %s", self._lost)
-                self._teardown()
-            bad = [f"rank {r + 1}: {m}" for r, m in enumerate(results) if m != "done"]
-            if err is not None:
-                raise err
+            if self._lost is not None or any(m is None for m in results):
+                self._lose("a rank did not report the end of the training", model.model_id)
+                raise RuntimeError(f"data-parallel training lost its group: {self._lost}")
+            self._refresh(model)
+            bad = [f"rank {r}: {m}" for r, m in enumerate(results) if m != "done"]
             if bad:
-                raise RuntimeError("data-parallel workers failed: " + "; ".join(bad))
+                raise RuntimeError("data-parallel training failed: " + "; ".join(bad))
             self.trainings += 1
+
+    @staticmethod
+    def _refresh(model) -> None:
+        """The caller's model object mirrors what rank 0 persisted (status, progress, stats)."""
+        try:
+            from ..utils import checkpoint as ckpt
+            meta = ckpt.load_meta(model.model_id)
+        except Exception:  # pragma: no cover - informational only
+            return
+        model.progress = meta.get("progress", model.progress)
+        model.avg_cost = meta.get("average_cost", model.avg_cost)
+        model.avg_cost_history = meta.get("average_cost_history", model.avg_cost_history)
+        model.stats = meta.get("stats", model.stats)
+        model.status = meta.get("status", model.status)
 
     def shutdown(self) -> None:
         self._stopping = True

@@ -1,9 +1,10 @@
 """Worker rank of the REST service's data-parallel train group (see :mod:`.service`).
 
-Started by the server process with RANK / WORLD_SIZE / MASTER_* / PZ_CTRL_ADDR / PZ_CTRL_KEY in its
-environment. It binds its GPU (``LOCAL_RANK``), connects the control socket, joins the process
-group and then serves ``load`` → (``go`` | ``abort``) → ``train`` commands until ``stop``. It reads
-the same ``models/`` directory as rank 0 and never writes it (only rank 0 persists).
+Started by the server process with RANK / WORLD_SIZE / PZ_RENDEZVOUS_FILE / PZ_CTRL_ADDR /
+PZ_CTRL_KEY in its environment. It binds its GPU (``LOCAL_RANK``), connects the control socket,
+joins the process group (file rendezvous in the group generation's own directory), reports
+``ready`` and then serves ``load`` → (``go`` | ``abort``) → ``train`` commands until ``stop``. Every
+rank reads the shared ``models/`` directory; only rank 0 writes it.
 """
 from __future__ import annotations
 
@@ -29,8 +30,16 @@ def main() -> int:
     conn.send(rank)
     if backend == "nccl":
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % torch.cuda.device_count())
-    dist.init_process_group(backend, rank=rank, world_size=world,
-                            timeout=timedelta(seconds=float(os.environ.get("PZ_DIST_TIMEOUT_S", "600"))))
+    if backend == "nccl":
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    try:
+        dist.init_process_group(backend, init_method="file://" + os.environ["PZ_RENDEZVOUS_FILE"], rank=rank,
+                                world_size=world,
+                                timeout=timedelta(seconds=float(os.environ.get("PZ_DIST_TIMEOUT_S", "600"))))
+    except Exception as e:
+        conn.send(f"{type(e).__name__}: {e}")
+        return 1
+    conn.send("ready")
     from penr_oz_neural_network_torch_amd.models import NeuralNetworkModel
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext, set_context
     comm = os.environ.get("PZ_GRAD_COMM_DTYPE")

@@ -174,17 +174,34 @@ def _to_cpu(obj):
 
 
 def _stamp(path: str) -> list[int]:
+    """Identity of one written version of the main file: size, mtime and inode (every atomic
+    write renames a fresh temporary file into place)."""
     st = os.stat(path)
-    return [st.st_size, st.st_mtime_ns]
+    return [st.st_size, st.st_mtime_ns, st.st_ino]
+
+
+def _previous_stamp(model_id: str):
+    try:
+        with open(meta_path(model_id), "r", encoding="utf-8") as f:
+            return json.load(f).get("main_stamp")
+    except (OSError, ValueError):
+        return None
 
 
 def save(model_id: str, skeleton: dict, optimizer_state: dict | None) -> None:
     os.makedirs(models_dir(), exist_ok=True)
     path = model_path(model_id)
+    before = _previous_stamp(model_id)
     _atomic_write_text(path, render_json(skeleton))
     log.info(f"Model saved successfully: {path}")
+    stamp = _stamp(path)
+    if stamp == before:
+        # a coarse-timestamp filesystem gave an equal-size rewrite the old mtime AND the old inode
+        # number came back: nudge the mtime so the old sidecar can never pass for this version
+        os.utime(path, ns=(stamp[1], stamp[1] + 1))
+        stamp = _stamp(path)
     meta = {k: skeleton[k] for k in META_KEYS if k in skeleton}
-    meta["main_stamp"] = _stamp(path)
+    meta["main_stamp"] = stamp
     _atomic_write_text(meta_path(model_id), json.dumps(meta))
     if optimizer_state is not None:
         opath = optimizer_path(model_id)
@@ -309,10 +326,29 @@ def load_meta(model_id: str) -> dict:
         pass
     from ..ops import native
     if native.has_host_ops() and os.environ.get("PZ_NATIVE_JSON", "1") != "0":
-        return json.loads(torch.ops.pz.json_skip_keys(path, list(BIG_KEYS)))
+        try:
+            return json.loads(torch.ops.pz.json_skip_keys(path, list(BIG_KEYS)))
+        except RuntimeError:
+            if not os.path.exists(path):  # deleted between the stat and the native open: 404, not 500
+                raise FileNotFoundError(2, "No such file or directory", path) from None
+            raise
     with open(path, "r", encoding="utf-8") as f:
         data = json.load(f)
     return {k: data[k] for k in META_KEYS if k in data}
+
+
+def set_status(model_id: str, status: str) -> None:
+    """Rewrite a checkpoint with another ``status`` (and nothing else changed) WITHOUT building a
+    model: parameters are parsed to host tensors and rendered back (exact round trip), nothing is
+    placed on a GPU. The REST service marks a data-parallel training "Failed" this way when the
+    rank that owns the files died with it."""
+    wait_pending(model_id)
+    data = read_model_data(model_path(model_id))
+    for layer in data.get("layers", []):
+        if isinstance(layer, dict) and isinstance(layer.get("params"), list):
+            layer["params"] = [TensorRef(p) if isinstance(p, torch.Tensor) else p for p in layer["params"]]
+    data["status"] = status
+    save(model_id, data, None)
 
 
 def delete(model_id: str) -> None:

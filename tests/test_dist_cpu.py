@@ -113,6 +113,55 @@ def test_gloo_data_parallel_training_equals_single_process(tmp_path, world, opti
             torch.testing.assert_close(v, wv, rtol=tol, atol=tol * 1e-2)
 
 
+def _concurrent_rank(rank, world, port, out_dir):
+    """Rank 0 trains a LOCAL batchnorm model in a second thread while the group training (also
+    batchnorm, synchronised over the ranks) is in flight: the local model must not pick up the
+    group's synchronisation (it was a process-wide global)."""
+    import threading
+    os.environ.update(PZ_RENDEZVOUS_FILE=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
+    from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
+    init_from_env("gloo")
+    model, data = _dp_model("adam", True)
+    local_out = {}
+    started = threading.Event()
+
+    def local():
+        started.wait()
+        lm, ldata = _dp_model("stochastic", True)
+        lm._train_autograd(ldata, 30, 0.05, 16, 0.9, 0.0, 1e-3, context=DataParallelContext(),
+                           sampler=torch.Generator().manual_seed(5))
+        local_out["params"] = [p.detach().clone() for p in lm.params]
+        local_out["sync"] = [getattr(l, "sync", None) for l in lm.layers if l.algo == "batchnorm"]
+
+    t = threading.Thread(target=local) if rank == 0 else None
+    if t is not None:
+        t.start()
+    started.set()
+    model._train_autograd(data, 30, 0.05, 32, 0.9, 0.0, 1e-3, sampler=torch.Generator().manual_seed(21))
+    if t is not None:
+        t.join()
+        torch.save({"local": local_out["params"], "sync_none": all(s is None for s in local_out["sync"]),
+                    "group_cleared": all(getattr(l, "sync", None) is None for l in model.layers)},
+                   os.path.join(out_dir, "conc.pt"))
+    shutdown()
+
+
+def test_batchnorm_sync_is_per_model_under_concurrent_training(tmp_path):
+    mp.start_processes(_concurrent_rank, args=(2, str(tmp_path / "rdv"), str(tmp_path)), nprocs=2,
+                       start_method="spawn")
+    got = torch.load(tmp_path / "conc.pt", weights_only=True)
+    assert got["sync_none"] and got["group_cleared"]
+    from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
+    lm, ldata = _dp_model("stochastic", True)
+    lm._train_autograd(ldata, 30, 0.05, 16, 0.9, 0.0, 1e-3, context=DataParallelContext(),
+                       sampler=torch.Generator().manual_seed(5))
+    for a, b in zip(got["local"], lm.params):  # exactly the standalone run: no foreign all-reduce
+        assert torch.equal(a, b.detach())
+
+
 def _native_rank(rank, world, port, out_dir):
     """The native-communicator plumbing of parallel/dist.py (unique-id broadcast from rank 0, init
     self-check, bucket tickets, reduced-precision buckets, shutdown) over gloo, with the RCCL ops of

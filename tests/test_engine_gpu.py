@@ -79,6 +79,113 @@ def test_dense_step_matches_reference(optimizer, dtype, tol):
         assert abs(a - b) < 0.05 * b + 1e-6 if dtype == "bfloat16" else abs(a - b) < 1e-3 * b + 1e-7
 
 
+@pytest.mark.parametrize("optimizer", ["stochastic", "adam"])
+@pytest.mark.parametrize("dtype", ["float32", "bfloat16"])
+def test_dropout_step_matches_fp64_reimplementation(optimizer, dtype):
+    """Dropout semantics at the step level: one fused step at
+    dropout_rate 0.3 vs an fp64 torch re-implementation of the reference epoch that applies the
+    kernels' keep masks to EVERY hidden layer output (reference neural_net_model.py:393-395) —
+    the ReLU output, the pre-tanh linear output, the tanh output and the logits that feed the
+    softmax / cross-entropy head (:400-403) — each kept element scaled by 1/(1-p)."""
+    from tests.helpers import keep_mask
+    sizes = [128, 256, 192, 64]
+    algos = ["relu", "tanh", "softmax"]  # -> linear relu linear tanh linear softmax
+    gpu, cpu = _pair(sizes, algos, optimizer, dtype)
+    assert cpu.algos == ["linear", "relu", "linear", "tanh", "linear", "softmax"]
+    hidden = [i for i, layer in enumerate(cpu.layers) if layer.hidden]
+    assert hidden == [1, 2, 3, 4]
+    n, S, p = 2000, 512, 0.3
+    g = torch.Generator().manual_seed(5)
+    inputs = torch.randn(n, sizes[0], generator=g)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    tr = FusedTrainer(gpu)
+    tr.load_tensors(inputs, labels, seed=11)
+    tr.begin(1)
+    lr, l2 = 0.02, 0.001
+    tr.step(0, lr, S, p, l2, want_ratios=False, record=False)
+    (_, cost, _, _), = tr.drain()
+    picked = tr.picked[:S].cpu()
+    x = inputs[picked].double()
+    y = labels[picked]
+    lo, hi = tr.base_seed
+    widths = {1: sizes[1], 2: sizes[2], 3: sizes[2], 4: sizes[3]}
+    masks = {lid: torch.from_numpy(keep_mask(S * w, lo, hi, lid, p, epoch=0).reshape(S, w)).double()
+             for lid, w in widths.items()}
+    for m in masks.values():  # the masks really drop ~p of every hidden output
+        assert abs(1.0 - m.mean().item() - p) < 0.02
+    s = 1.0 / (1.0 - p)
+    for q in cpu.params:
+        q.requires_grad_()
+    if cpu.optimizer is not None:
+        for grp in cpu.optimizer.param_groups:
+            grp["lr"] = lr
+    L = cpu.layers
+    z0 = x @ L[0].weights + L[0].bias
+    a1 = torch.relu(z0) * masks[1] * s
+    z2 = (a1 @ L[2].weights + L[2].bias) * masks[2] * s
+    a3 = torch.tanh(z2) * masks[3] * s
+    logits = (a3 @ L[4].weights + L[4].bias) * masks[4] * s
+    ref = torch.nn.functional.cross_entropy(logits, y) + l2 * sum((w ** 2).sum() for w in cpu.weights)
+    ref.backward()
+    if cpu.optimizer is not None:
+        cpu.optimizer.step()
+    else:
+        for q in cpu.params:
+            q.data -= lr * q.grad
+    ctol = 1e-4 if dtype == "float32" else 3e-2
+    assert abs(cost - ref.item()) < ctol * max(1.0, abs(ref.item())), (cost, ref.item())
+    for pg, pc in zip(gpu.params, cpu.params):
+        d = (pg.detach().double().cpu() - pc.detach()).abs()
+        if optimizer == "adam":  # first Adam step ~ lr*sign(g): compare in distribution
+            assert (d > 0.1 * lr).double().mean().item() < (0.002 if dtype == "float32" else 0.05)
+        else:
+            tol = 2e-4 if dtype == "float32" else 3e-2
+            scale = pc.detach().abs().max().item()
+            assert d.max().item() < tol * max(scale, 1e-3) + (1e-3 if dtype == "bfloat16" else 1e-6), d.max()
+
+
+@pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
+def test_fp64_fused_step_matches_reference(optimizer):
+    """fp64 on the fused engine: the precision a REST model created with
+    device="cuda" and no dtype gets. f64 MFMA GEMMs, fp64 heads / bias gradients / Adam: one step
+    equals the CPU reference step to fp64 rounding (rtol 1e-10), the cost to 1e-12."""
+    sizes = [256, 512, 256, 128]
+    algos = ["relu", "tanh", "softmax"]
+    gpu, cpu = _pair(sizes, algos, optimizer, "float64")
+    tr = FusedTrainer(gpu)
+    assert tr.compute == torch.float64 and tr.grads.dtype == torch.float64 and not tr.shadow_sets[0]
+    n, S = 3000, 1024
+    g = torch.Generator().manual_seed(1)
+    inputs = torch.randn(n, sizes[0], generator=g, dtype=torch.float64)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    data = [(inputs[i].tolist(), [int(labels[i])]) for i in range(n)]
+    tr.load_data(data)
+    assert tr.data.dtype == torch.float64
+    tr.begin(1)
+    lr, l2 = 0.01, 0.001
+    tr.step(0, lr, S, 0.0, l2, want_ratios=True, record=False)
+    (_, cost, ratios, _), = tr.drain()
+    picked = tr.picked[:S].cpu()
+    prev = [w.clone().detach() for w in cpu.weights]
+    cpu_cost = _cpu_step(cpu, inputs[picked], [[int(labels[i])] for i in picked], lr, l2)
+    assert abs(cost - cpu_cost) <= 1e-12 * max(1.0, abs(cpu_cost)), (cost, cpu_cost)
+    for pg, pc in zip(gpu.params, cpu.params):
+        torch.testing.assert_close(pg.detach().cpu(), pc.detach(), rtol=1e-10, atol=1e-12)
+    ref_ratios = [((w - pw).std() / (w.std() + 1e-8)).item() for pw, w in zip(prev, cpu.weights)]
+    for a, b in zip(ratios, ref_ratios):
+        assert abs(a - b) <= 1e-6 * b + 1e-9  # ratios leave the device as fp32
+
+
+def test_fp64_model_train_uses_fused_engine(models_tmpdir):
+    """A default-precision GPU model (fp64) trains through the fused engine, not autograd."""
+    torch.manual_seed(0)
+    model = NeuralNetworkModel("f64", [9, 18, 9], activation_algos=["relu", "softmax"], device="cuda")
+    assert model.precision.name == "float64" and model._fused_trainer() is not None
+    data = [([float((i + j) % 3 - 1) for j in range(9)], [i % 9]) for i in range(model.training_buffer_size)]
+    model.train(data, epochs=3, learning_rate=0.01, batch_size=64)
+    assert model.status == "Trained" and all(p.get("dtype") == "float64" for p in model.progress)
+
+
 def test_embedding_batchnorm_step_matches_reference():
     sizes = [27, 10, 30, 64, 27]
     algos = ["embedding", "linear", "batchnorm", "tanh", "linear", "softmax"]

@@ -1,6 +1,6 @@
 """The REST service's multi-rank train group (parallel/service.py) on the CPU: ``PUT /train/``
-drives a 2-rank gloo data-parallel training (this pytest process is rank 0, one worker process
-is started by the app's lifespan) — the code path an 8-GPU node runs over RCCL."""
+drives a 2-rank gloo data-parallel training (two rank processes started by the app's lifespan;
+the server process never joins the group) — the code path an 8-GPU node runs over RCCL."""
 import time
 
 import pytest
@@ -76,9 +76,10 @@ def _health_group(client):
 
 
 def test_group_recovers_from_lost_workers(models_tmpdir, monkeypatch):
-    """a worker that dies (idle, or in the middle of a training) is detected by the
-    watchdog; an in-flight training fails promptly instead of waiting out the collective timeout,
-    and the next ``PUT /train/`` brings a fresh group up (new worker, new rendezvous) and trains."""
+    """a rank that dies (idle, or in the middle of a training) is detected by the
+    watchdog; an in-flight training fails promptly instead of waiting out the collective timeout
+    (the checkpoint reads "Failed" although the rank that writes it died), and the next
+    ``PUT /train/`` brings a fresh group up (new processes, new rendezvous) and trains."""
     from penr_oz_neural_network_torch_amd.parallel import service
     monkeypatch.setenv("PZ_SERVICE_GPUS", "2")
     monkeypatch.setenv("PZ_DIST_BACKEND", "gloo")
@@ -91,8 +92,8 @@ def test_group_recovers_from_lost_workers(models_tmpdir, monkeypatch):
         short = {"model_id": "ft", "training_data": data, "epochs": 3, "batch_size": 8}
         group = service.get_group()
 
-        # 1) idle worker killed: the watchdog marks the group lost, the next training restarts it
-        group.procs[0].kill()
+        # 1) idle rank 1 killed: the watchdog marks the group lost, the next training restarts it
+        group.procs[1].kill()
         t0 = time.time()
         while _health_group(client)["lost"] is None:
             assert time.time() - t0 < 10, "watchdog did not notice the dead worker"
@@ -103,7 +104,8 @@ def test_group_recovers_from_lost_workers(models_tmpdir, monkeypatch):
         g = _wait_trainings(client, 1)
         assert g["healthy"] and g["restarts"] == 1 and g["trainings"] == 1
 
-        # 2) worker killed in the middle of a training: prompt failure, then a fresh group
+        # 2) rank 0 (the checkpoint writer) killed in the middle of a training: prompt failure,
+        #    status "Failed" written by the server, then a fresh group
         long = dict(short, epochs=200000)
         assert client.put("/train/", json=long).status_code == 202
         _wait(client, "ft", ("Training",))
@@ -121,4 +123,4 @@ def test_group_recovers_from_lost_workers(models_tmpdir, monkeypatch):
         assert _wait(client, "ft", ("Trained",))["status"] == "Trained"
         g = _health_group(client)
         assert g["healthy"] and g["restarts"] == 2 and g["trainings"] == 2
-        assert group.procs[0] is not victim and group.procs[0].poll() is None
+        assert group.procs[0] is not victim and all(p.poll() is None for p in group.procs)
