@@ -46,8 +46,8 @@ __global__ void __launch_bounds__(256) bn_col_sums_kernel(const T* __restrict__ 
 }
 
 template <typename P>
-__global__ void bn_finalize_kernel(const double* partial, int n, int cols, P* running_mean, P* running_var, float eps,
-                                   float momentum, int training, double* save_mean, double* save_invstd) {
+__global__ void bn_finalize_kernel(const double* partial, int n, int cols, P* running_mean, P* running_var, double eps,
+                                   double momentum, int training, double* save_mean, double* save_invstd) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= cols) return;
   double mean, var;

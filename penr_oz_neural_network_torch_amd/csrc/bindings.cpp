@@ -68,6 +68,8 @@ pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
   e.act = pz::ACT_NONE;
   e.scale = 1.f;
   e.inv_scale = 1.f;
+  e.scale64 = 1.0;
+  e.inv_scale64 = 1.0;
   if (ei.size() >= 7) {  // [act, drop_pre, drop_post, key_pre, key_post, thresh16, drop_all]
     e.act = static_cast<int>(ei[0]);
     e.drop_pre = ei[1] != 0;
@@ -83,6 +85,8 @@ pz::EpiSpec make_epi(at::IntArrayRef ei, at::ArrayRef<double> ef) {
   if (ef.size() >= 2) {
     e.scale = static_cast<float>(ef[0]);
     e.inv_scale = static_cast<float>(ef[1]);
+    e.scale64 = ef[0];
+    e.inv_scale64 = ef[1];
   }
   return e;
 }
@@ -116,8 +120,10 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "pz::gemm: 2-D operands expected");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "pz::gemm: unit inner stride expected");
   TORCH_CHECK(A.scalar_type() == B.scalar_type() ||
-                  (A.scalar_type() == at::kFloat8_e5m2 && B.scalar_type() == at::kFloat8_e4m3fn),
-              "pz::gemm: A/B dtype mismatch (mixed fp8: e5m2 A x e4m3 B only)");
+                  (A.scalar_type() == at::kFloat8_e5m2 && B.scalar_type() == at::kFloat8_e4m3fn) ||
+                  (A.scalar_type() == at::kFloat8_e4m3fn && B.scalar_type() == at::kFloat8_e5m2 && !a_kc && !b_kc),
+              "pz::gemm: A/B dtype mismatch (mixed fp8: e5m2 A x e4m3 B, or the [K][M] e4m3 x [K][N] e5m2 "
+              "weight gradient)");
   TORCH_CHECK(a_kc ? (A.size(0) >= M && A.size(1) >= K) : (A.size(0) >= K && A.size(1) >= M), "pz::gemm: A shape");
   TORCH_CHECK(b_kc ? (B.size(0) >= N && B.size(1) >= K) : (B.size(0) >= K && B.size(1) >= N), "pz::gemm: B shape");
   TORCH_CHECK(C.size(0) >= M && C.size(1) >= N, "pz::gemm: C shape");
@@ -196,18 +202,21 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
              at::ArrayRef<double> epi_f, double alpha, bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld,
              bool force_generic, const optional<Tensor>& mask, const optional<Tensor>& scale_a,
              const optional<Tensor>& scale_b, const optional<Tensor>& out8, const optional<Tensor>& out8_qscale,
-             const optional<Tensor>& amax) {
+             const optional<Tensor>& amax, int64_t max_split) {
   check_dev(A, "A");
   auto p = gemm_args(A, a_kc, B, b_kc, C, bias, aux, colsum, epi_mode, epi_i, epi_f, alpha, accumulate, M, N, K, idx_ld,
                      force_generic, mask);
   p.scale_a = f32_scalar_ptr(scale_a, "scale_a");
   p.scale_b = f32_scalar_ptr(scale_b, "scale_b");
   p.a_fmt = A.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
-  TORCH_CHECK(B.scalar_type() != at::kFloat8_e5m2, "pz::gemm: e5m2 is supported for the A operand (gradients) only");
+  p.b_fmt = B.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
+  TORCH_CHECK(p.b_fmt == 0 || (!a_kc && !b_kc), "pz::gemm: an e5m2 B operand needs the M/N-contiguous dW layout");
   if (out8.has_value() && out8->defined()) {
-    TORCH_CHECK(out8->scalar_type() == at::kFloat8_e4m3fn && out8->dim() == 2 && out8->stride(1) == 1 &&
-                    out8->size(0) >= M && out8->size(1) >= N,
-                "pz::gemm: out8 must be float8_e4m3fn [M, N]");
+    TORCH_CHECK((out8->scalar_type() == at::kFloat8_e4m3fn || out8->scalar_type() == at::kFloat8_e5m2) &&
+                    out8->dim() == 2 && out8->stride(1) == 1 && out8->size(0) >= M && out8->size(1) >= N,
+                "pz::gemm: out8 must be float8_e4m3fn (forward) or float8_e5m2 (backward) [M, N]");
+    p.out8_fmt = out8->scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
+    TORCH_CHECK(p.out8_fmt == (epi_mode == 2 ? 1 : 0), "pz::gemm: out8 is e4m3 for EPI_FWD, e5m2 for EPI_BWD");
     p.out8 = static_cast<uint8_t*>(out8->data_ptr());
     p.ldout8 = out8->stride(0);
     p.out8_qscale = f32_scalar_ptr(out8_qscale, "out8_qscale");
@@ -220,7 +229,9 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
   TORCH_CHECK((p.out8 == nullptr && p.in_dtype != pz::DT_FP8) || pz::gemm_path(p) == 1,
               "pz::gemm: fp8 operands / outputs need an MFMA-eligible shape");
   at::Tensor ws;  // split-K slabs: from the caching allocator, stream-ordered reuse is safe
-  const int64_t ws_floats = pz::gemm_split_ws_floats(p);
+  // max_split == 1: no split-K (a GEMM that runs concurrently with others: its tile count need
+  // not fill the CUs on its own, and it skips the in-launch reduction)
+  const int64_t ws_floats = max_split == 1 ? 0 : pz::gemm_split_ws_floats(p);
   if (ws_floats > 0) {
     ws = at::empty({ws_floats}, A.options().dtype(at::kFloat));
     p.split_k = pz::gemm_split(p);
@@ -342,13 +353,13 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
   a.cols = static_cast<int>(logits.size(1));
   a.dtype = dt_of(logits);
   head_accumulators(a, loss, colsum, a.dtype == pz::DT_F64, "pz::xent_head");
-  a.loss_scale = static_cast<float>(loss_scale);
+  a.loss_scale = loss_scale;
   if (dh.has_value() && dh->defined()) {
     TORCH_CHECK(dh->scalar_type() == logits.scalar_type() && dh->stride(1) == 1, "pz::xent_head: dh");
     a.dh = dh->data_ptr();
     a.ld_dh = dh->stride(0);
   }
-  a.grad_scale = static_cast<float>(grad_scale);
+  a.grad_scale = grad_scale;
   if (probs.has_value() && probs->defined()) {
     TORCH_CHECK(probs->scalar_type() == logits.scalar_type() && probs->stride(1) == 1, "pz::xent_head: probs");
     a.probs = probs->data_ptr();
@@ -375,12 +386,12 @@ void mse_head_op(const Tensor& y, const Tensor& target, int64_t rows_valid, cons
   a.cols = static_cast<int>(y.size(1));
   a.dtype = dt_of(y);
   head_accumulators(a, loss, colsum, a.dtype == pz::DT_F64, "pz::mse_head");
-  a.loss_scale = static_cast<float>(loss_scale);
+  a.loss_scale = loss_scale;
   if (dh.has_value() && dh->defined()) {
     a.dh = dh->data_ptr();
     a.ld_dh = dh->stride(0);
   }
-  a.grad_scale = static_cast<float>(grad_scale);
+  a.grad_scale = grad_scale;
   a.epi = make_epi(ei, ef);
   a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
   PZ_HIP_CHECK(pz::mse_head(a, cur_stream(y)));
@@ -589,8 +600,8 @@ void batchnorm_fwd_op(const Tensor& x, const Tensor& y, const Tensor& gain, cons
   a.param_dtype = dt_of(gain);
   a.running_mean = running_mean.data_ptr();
   a.running_var = running_var.data_ptr();
-  a.eps = static_cast<float>(eps);
-  a.momentum = static_cast<float>(momentum);
+  a.eps = eps;
+  a.momentum = momentum;
   a.training = training;
   a.save_mean = save_mean.data_ptr<double>();
   a.save_invstd = save_invstd.data_ptr<double>();
@@ -730,7 +741,7 @@ void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tenso
   a.stats_cur = stats_cur.data_ptr<double>();
   a.slot_numel = slot_numel.data_ptr<double>();
   a.nslots = static_cast<int>(nslots);
-  a.l2 = static_cast<float>(l2);
+  a.l2 = l2;
   a.costs = costs.data_ptr<double>();
   a.epoch = static_cast<int>(epoch);
   a.ratios = ratios.data_ptr<float>();
@@ -817,7 +828,7 @@ TORCH_LIBRARY(pz, m) {
   m.def("gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor(a!) C, Tensor? bias, Tensor? aux, Tensor(b!)? colsum, "
         "int epi_mode, int[] epi_i, float[] epi_f, float alpha, bool accumulate, int M, int N, int K, int idx_ld, "
         "bool force_generic, Tensor(c!)? mask=None, Tensor? scale_a=None, Tensor? scale_b=None, "
-        "Tensor(d!)? out8=None, Tensor? out8_qscale=None, Tensor(e!)? amax=None) -> ()");
+        "Tensor(d!)? out8=None, Tensor? out8_qscale=None, Tensor(e!)? amax=None, int max_split=0) -> ()");
   m.def("gemm_update(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor grad, int M, int N, int K, float alpha, "
         "Tensor(a!) params, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor(d!)? shadow, Tensor(e!)? stats, "
         "Tensor(f!)? amax, bool adam, float lr, float beta1, float beta2, float eps, float bias_c1, "

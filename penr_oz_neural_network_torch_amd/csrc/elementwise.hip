@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
       se = wave_sum(se);
       xl = wave_sum(xl);
       const float inv = 1.f / se;
-      if (lane == 0) loss_acc += (mx + __logf(se) - xl) * a.loss_scale;
+      if (lane == 0) loss_acc += (mx + __logf(se) - xl) * static_cast<float>(a.loss_scale);
 #pragma unroll
       for (int j = 0; j < NCH; ++j) {
         if (!ok[j]) continue;
@@ -232,7 +232,7 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           pr[e] = v[j][e] * inv;
-          g[e] = (pr[e] - (c0 + e == label ? 1.f : 0.f)) * a.grad_scale;
+          g[e] = (pr[e] - (c0 + e == label ? 1.f : 0.f)) * static_cast<float>(a.grad_scale);
         }
         if (probs != nullptr)
           *reinterpret_cast<uint4*>(probs + static_cast<int64_t>(row) * a.ld_probs + c0) =

@@ -135,6 +135,21 @@ PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], u32x2_t bits, int nlane) {
   }
 }
 
+// 8 fp32 -> 8 e5m2 bytes (OCP bf8, saturating at +-57344): the backward's dZ copy
+PZ_DEV u32x2_t to_e5m2x8(const float (&x)[8], float qs) {
+  u32x2_t out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = fminf(fmaxf(x[4 * h + q] * qs, -57344.f), 57344.f);
+    int w = __builtin_amdgcn_cvt_pk_bf8_f32(c[0], c[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(c[2], c[3], w, true);
+    out[h] = static_cast<uint32_t>(w);
+  }
+  return out;
+}
+
 // 8 fp32 -> 8 e4m3 bytes (OCP, saturating at +-448)
 PZ_DEV u32x2_t to_e4m3x8(const float (&x)[8], float qs) {
   u32x2_t out;
@@ -264,7 +279,8 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   }
   __syncthreads();
   uint16_t* __restrict__ Cp = static_cast<uint16_t*>(p.C);
-  const bool want8 = !bwd && p.out8 != nullptr;
+  // fp8 copy of the stored bf16 tile: e4m3 activations (forward) / e5m2 dZ (backward)
+  const bool want8 = p.out8 != nullptr && (bwd ? p.out8_fmt == 1 : p.out8_fmt == 0);
   const float qs = want8 ? *p.out8_qscale : 1.f;
   float amax = 0.f;
 #pragma unroll
@@ -292,7 +308,8 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
           x[2 * q + 1] = bf2f(v[q] >> 16);
           amax = fmaxf(amax, fmaxf(fabsf(x[2 * q]), fabsf(x[2 * q + 1])));
         }
-        *reinterpret_cast<u32x2_t*>(p.out8 + static_cast<int64_t>(gm) * p.ldout8 + gn) = to_e4m3x8(x, qs);
+        *reinterpret_cast<u32x2_t*>(p.out8 + static_cast<int64_t>(gm) * p.ldout8 + gn) =
+            bwd ? to_e5m2x8(x, qs) : to_e4m3x8(x, qs);
       }
     }
     if (!bwd && use_mask) {  // 4 neighbouring chunks of a row -> one 4-byte store (not 4 byte stores)

@@ -224,13 +224,57 @@ PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int c
   }
 }
 
+// M/N-contiguous fp8 operand ([K][rows] bytes in memory; the weight-gradient GEMM's activations
+// and output gradients): k rows [k0, k0+KROWS) x bytes [col0, col0+RB) -> slot [KROWS][RB]. The
+// 16-B chunk of k-row kr is XOR-ed with (kr & 7) << 1, so the transposing 8-bit reads below
+// (8 k-rows x 16 bytes per 16-lane group, two groups per 32-lane bank half) are conflict-free.
+PZ_DEV int swz_mn8(int krow) { return (krow & 7) << 1; }
+template <int RB, int NW, int KROWS>
+PZ_DEV void stage_mn8(int64_t ld16, int col0, int k0, PZ_LDS char* tile, int wave, int lane, i32x4_t rs) {
+  constexpr int CHUNKS = RB / 16;
+  constexpr int ROWS_PER = 1024 / RB;
+  constexpr int INSTR = (KROWS * RB) / (1024 * NW);
+  static_assert(INSTR >= 1 && INSTR * 1024 * NW == KROWS * RB, "fp8 M/N-contiguous stage split");
+#pragma unroll
+  for (int i = 0; i < INSTR; ++i) {
+    const int kbase = (wave * INSTR + i) * ROWS_PER;
+    const int kr = kbase + lane / CHUNKS;
+    const int chunk = (lane % CHUNKS) ^ swz_mn8(kr);
+    const uint32_t voff = (static_cast<uint32_t>(kr) * static_cast<uint32_t>(ld16)) * 2u +
+                          static_cast<uint32_t>(col0 + chunk * 16);
+    blds16<0>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * static_cast<uint32_t>(ld16) * 2u),
+              lds_addr(tile + kbase * RB));
+  }
+}
+
+typedef int i32x2_t __attribute__((ext_vector_type(2)));
+typedef int i32x8_t __attribute__((ext_vector_type(8)));
+// 32x32x64 f8 MFMA operand from an [64 k][RB] fp8 slot: lane l holds column col32 + (l & 31),
+// k bytes [32 (l >> 5), +32) — four ds_read_b64_tr_b8 (per 16-lane group: 8 k-rows x 16 columns,
+// lane 2q+p addresses k-row q, bytes 8p..8p+7 of the group's 16; lane i receives column i)
+template <int RB>
+PZ_DEV i32x8_t frag_mn8(const PZ_LDS char* tile, int col32, int lane) {
+  const int q = (lane & 15) >> 1;
+  const int col = col32 + 16 * ((lane >> 4) & 1) + 8 * (lane & 1);
+  const int chunk = col >> 4, within = col & 15;
+  i32x8_t out;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = 32 * (lane >> 5) + 8 * i + q;
+    const PZ_LDS char* a = tile + k * RB + ((chunk ^ swz_mn8(k)) << 4) + within;
+    const i32x2_t r = __builtin_amdgcn_ds_read_tr8_b64_v2i32((PZ_LDS i32x2_t*)(a));
+    out[2 * i] = r[0];
+    out[2 * i + 1] = r[1];
+  }
+  return out;
+}
+
 template <int BK = 32>
 PZ_DEV i16x8_t frag_kc(const PZ_LDS char* tile, int row, int chunk) {
   const int slot = chunk ^ swz_kc<BK>(row);
   return *reinterpret_cast<const PZ_LDS i16x8_t*>(tile + row * (BK * 2) + slot * 16);
 }
 
-typedef int i32x8_t __attribute__((ext_vector_type(8)));
 PZ_DEV i32x8_t cat_frag(i16x8_t lo, i16x8_t hi) {
   const i32x4_t a = __builtin_bit_cast(i32x4_t, lo), b = __builtin_bit_cast(i32x4_t, hi);
   return i32x8_t{a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
@@ -480,10 +524,16 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // VAR 9: A in e5m2 (bf8: gradients, wide range), B in e4m3 — the backward dX GEMM
   // dZ8 · W8ᵀ of the fp8 policy, with the backward (EPI_BWD) epilogues
   // VAR 10 / 11: VAR 8 / 9 with buffer-addressed staging DMA
-  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11 || VAR == 12 || VAR == 13;
+  // VAR 14: the fp8 weight-gradient GEMM dW = X8ᵀ · dZ8 — e4m3 activations (A) x e5m2 output
+  // gradients (B), BOTH M/N-contiguous ([K][M] / [K][N] bytes, K = batch rows), staged as k-row
+  // images and read with the transposing ds_read_b64_tr_b8 (no transposed copies), bf16 output
+  constexpr bool F8_MN = VAR == 14;
+  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11 || VAR == 12 || VAR == 13 || F8_MN;
   constexpr bool F8_BWD = VAR == 9 || VAR == 11 || VAR == 13;
   constexpr int F8_FMT_A = F8_BWD ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
-  static_assert(!F8 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "fp8: K-contiguous in, bf16 out");
+  constexpr int F8_FMT_B = F8_MN ? 1 : 0;
+  static_assert(!F8 || ((F8_MN ? (!A_KC && !B_KC) : (A_KC && B_KC)) && std::is_same<OutT, uint16_t>::value),
+                "fp8: K-contiguous in (M/N-contiguous for VAR 14), bf16 out");
   // VAR 41 (lab A/B): bf16 on v_mfma_f32_32x32x16_bf16 (32x32 accumulator tiles, the fp8 layout)
   constexpr bool M32 = VAR == 41;
   static_assert(!M32 || (A_KC && B_KC && std::is_same<OutT, uint16_t>::value), "M32: K-contiguous in, bf16 out");
@@ -526,8 +576,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 #pragma unroll
           for (int j = 0; j < TN8; ++j)  // issued as mfma(B, A): cbsz = B's format, blgp = A's;
                                          // E8M0 block scales 127 = 1.0
-            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[kb][j], f.a[kb][i], acc[i][j], 0, F8_FMT_A,
-                                                                         0, 127, 0, 127);
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(f.b[kb][j], f.a[kb][i], acc[i][j], F8_FMT_B,
+                                                                         F8_FMT_A, 0, 127, 0, 127);
     } else {
 #pragma unroll
       for (int kb = 0; kb < KB; ++kb)
@@ -551,6 +601,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 #pragma unroll
         for (int i = 0; i < TM8; ++i) f.a[ks][i] = frag_kc(ta, wm * C::WTM + i * 32 + (lane & 31), (lane >> 5) + 2 * ks);
       }
+    } else if constexpr (F8_MN) {  // transposing 8-bit reads of the [64 k][256 B] images (KB == 1)
+#pragma unroll
+      for (int j = 0; j < TN8; ++j) f.b[0][j] = frag_mn8<BN>(tb, wn * C::WTN + j * 32, lane);
+#pragma unroll
+      for (int i = 0; i < TM8; ++i) f.a[0][i] = frag_mn8<BM>(ta, wm * C::WTM + i * 32, lane);
     } else if constexpr (F8) {  // lane l: row l&31, K bytes [32*(l>>5), +32) of K-step kb = 16-B chunks
                                 // 4kb + 2h, 4kb + 2h + 1
       const int h2 = 2 * (lane >> 5);
@@ -612,13 +667,15 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   auto stage_a_t = [&](int kt, auto team, int tw) {
     constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES;
-    if constexpr (A_KC) stage_kc<BM, TEAM, BK, BUF_A, POL, FULL_KC>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
+    if constexpr (F8_MN) stage_mn8<BM, TEAM, 64>(lda, m0, (kt0 + kt) * 64, base, tw, lane, rs_a);
+    else if constexpr (A_KC) stage_kc<BM, TEAM, BK, BUF_A, POL, FULL_KC>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
     else stage_mn<BM, TEAM, BK, BUF_A, POL>(A, lda, m0, p.M, (kt0 + kt) * BK, base, tw, lane, rs_a);
   };
   auto stage_b_t = [&](int kt, auto team, int tw) {
     constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B, POL, FULL_KC>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
+    if constexpr (F8_MN) stage_mn8<BN, TEAM, 64>(ldb, n0, (kt0 + kt) * 64, base, tw, lane, rs_b);
+    else if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B, POL, FULL_KC>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
     else stage_mn<BN, TEAM, BK, BUF_B, POL>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
   };
   auto stage_a = [&](int kt) { stage_a_t(kt, std::integral_constant<int, NWD>{}, wave); };
@@ -952,6 +1009,8 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
 
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  if (!p.a_kc && !p.b_kc)  // e4m3 x e5m2 weight gradient (fp8_eligible: full 256-tiles, buffer-addressable)
+    return launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14>(p, s);
   // PZ_GEMM_F8BUF=1: buffer-addressed staging DMA (VAR 10 / 11), A/B
   static const bool f8buf = [] {
     const char* e = getenv("PZ_GEMM_F8BUF");
@@ -989,9 +1048,22 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
 }  // namespace
 
 #ifndef PZ_GEMM_LAB
+bool fp8_dw_eligible(const GemmArgs& p) {  // VAR 14: X8ᵀ (e4m3) · dZ8 (e5m2), both M/N-contiguous
+  if (p.a_fmt != 0 || p.b_fmt != 1 || p.epi_mode != EPI_STORE || p.accumulate) return false;
+  if (p.bias != nullptr || p.colsum != nullptr || p.mask != nullptr || p.out8 != nullptr || p.aux != nullptr) return false;
+  if (p.M % 256 != 0 || p.N % 256 != 0 || p.K % 64 != 0 || p.K < 64) return false;
+  if (p.lda % 16 != 0 || p.ldb % 16 != 0 || p.ldc % 8 != 0) return false;
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al16(p.A) || !al16(p.B) || !al16(p.C)) return false;
+  constexpr int64_t kLim = int64_t(1) << 32;  // buffer-addressed staging
+  return static_cast<int64_t>(p.K) * p.lda < kLim && static_cast<int64_t>(p.K) * p.ldb < kLim;
+}
+
 bool fp8_eligible(const GemmArgs& p) {
   if (p.force_generic || p.in_dtype != DT_FP8 || p.out_dtype != DT_BF16) return false;
   if (p.bias64 != nullptr || p.colsum64 != nullptr) return false;
+  if (!p.a_kc && !p.b_kc) return fp8_dw_eligible(p);
+  if (p.b_fmt != 0) return false;
   if (!p.a_kc || !p.b_kc || p.accumulate) return false;
   if (p.M < 64 || p.N < 64 || p.K < 64 || p.K % 64 != 0) return false;
   if (p.N % 8 != 0 || p.ldc % 8 != 0 || p.lda % 16 != 0 || p.ldb % 16 != 0) return false;
@@ -1000,7 +1072,8 @@ bool fp8_eligible(const GemmArgs& p) {
   if (p.idx_ld % 2 != 0) return false;
   if (p.bias != nullptr && !al16(p.bias)) return false;
   // e4m3 x e4m3: forward stages; e5m2 (A, gradients) x e4m3 (B): backward dX stages only
-  if ((p.a_fmt == 1) != (p.epi_mode == EPI_BWD) || (p.a_fmt == 1 && p.out8 != nullptr)) return false;
+  if ((p.a_fmt == 1) != (p.epi_mode == EPI_BWD)) return false;
+  if (p.out8 != nullptr && p.out8_fmt != (p.epi_mode == EPI_BWD ? 1 : 0)) return false;
   if (p.epi_mode == EPI_BWD && p.mask == nullptr &&
       (p.aux == nullptr || p.aux_dtype != DT_BF16 || p.ldaux % 8 != 0 || (reinterpret_cast<uintptr_t>(p.aux) & 15)))
     return false;
@@ -1036,7 +1109,8 @@ bool mfma_eligible(const GemmArgs& p) {
   }
   if (p.out_dtype == DT_BF16 && p.accumulate) return false;
   if (p.bias != nullptr && !al16(p.bias)) return false;
-  if (p.out8 != nullptr && (p.out_dtype != DT_BF16 || p.epi_mode == EPI_BWD || p.ldout8 % 8 != 0 ||
+  if (p.out8 != nullptr && (p.out_dtype != DT_BF16 || p.out8_fmt != (p.epi_mode == EPI_BWD ? 1 : 0) ||
+                            (p.epi_mode != EPI_BWD && p.epi_mode != EPI_FWD) || p.ldout8 % 8 != 0 ||
                             (reinterpret_cast<uintptr_t>(p.out8) & 7) != 0 || p.out8_qscale == nullptr))
     return false;
   if (p.mask != nullptr) {
@@ -1057,8 +1131,10 @@ int gemm_split(const GemmArgs& p) {
     return e ? atoi(e) : 1;
   }();
   static const bool forced_tile = getenv("PZ_GEMM_TILE") != nullptr;
-  // fp8 skinny shapes run better as 128x128 tiles (measured: split-K 256x256 -4%)
-  if (mode == 0 || forced_tile || p.in_dtype == DT_FP8 || !mfma_eligible(p)) return 1;
+  // fp8 skinny shapes run better as 128x128 tiles (measured: split-K 256x256 -4%); the fp8
+  // weight-gradient GEMM (both operands M/N-contiguous, 256-tiles only) splits like bf16
+  const bool f8_dw = p.in_dtype == DT_FP8 && !p.a_kc && !p.b_kc;
+  if (mode == 0 || forced_tile || (p.in_dtype == DT_FP8 && !f8_dw) || !mfma_eligible(p)) return 1;
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   constexpr int kFill = 240;
   if (tiles >= kFill || prefer_128(p)) return 1;

@@ -116,26 +116,35 @@ PZ_DEV bool epi_keep(const EpiSpec& e, uint32_t key, uint64_t idx) {
 }
 
 // forward: x = producing-op output (bias already added), idx = logical element index
+// dropout scale in the math precision F: the fp64 kernels use the exact double (F.dropout's
+// 1/(1-p) in fp64), the fp32 ones the float
+template <typename F> PZ_DEV F epi_scale(const EpiSpec& e) { return F(e.scale); }
+template <> PZ_DEV double epi_scale<double>(const EpiSpec& e) { return e.scale64; }
+template <typename F> PZ_DEV F epi_inv_scale(const EpiSpec& e) { return F(e.inv_scale); }
+template <> PZ_DEV double epi_inv_scale<double>(const EpiSpec& e) { return e.inv_scale64; }
+
 template <typename F>
 PZ_DEV F epi_fwd(F x, uint64_t idx, const EpiSpec& e) {
-  if (e.drop_pre) x = epi_keep(e, e.key_pre, idx) ? x * F(e.scale) : F(0);
+  const F sc = epi_scale<F>(e);
+  if (e.drop_pre) x = epi_keep(e, e.key_pre, idx) ? x * sc : F(0);
   x = act_fwd(x, e.act);
-  if (e.drop_post) x = epi_keep(e, e.key_post, idx) ? x * F(e.scale) : F(0);
+  if (e.drop_post) x = epi_keep(e, e.key_post, idx) ? x * sc : F(0);
   return x;
 }
 
 // backward: g = dLoss/dy, y = stored stage output; returns dLoss/dx (x as in epi_fwd)
 template <typename F>
 PZ_DEV F epi_bwd(F g, F y, uint64_t idx, const EpiSpec& e) {
+  const F sc = epi_scale<F>(e);
   if (e.drop_post) {
     if (!epi_keep(e, e.key_post, idx)) return F(0);
-    g *= F(e.scale);
-    y *= F(e.inv_scale);
+    g *= sc;
+    y *= epi_inv_scale<F>(e);
   }
   if (e.act != ACT_NONE) g *= act_grad_from_out(y, e.act);
   if (e.drop_pre) {
     if (!epi_keep(e, e.key_pre, idx)) return F(0);
-    g *= F(e.scale);
+    g *= sc;
   }
   return g;
 }

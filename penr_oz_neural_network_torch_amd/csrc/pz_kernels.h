@@ -16,10 +16,10 @@ struct XentArgs {
   float* loss;          // += sum_rows (lse - x_label) * loss_scale   (may be null)
   double* loss64;       // fp64 logits: the loss accumulates here instead (double)
   int loss_slots;       // > 1: block b adds into loss[b % loss_slots] (the consumer sums them)
-  float loss_scale;
+  double loss_scale;    // doubles: exact for fp64 models (fp32 kernels round them once)
   void* dh;             // [rows][ld_dh] gradient wrt the pre-dropout logits (may be null)
   int64_t ld_dh;
-  float grad_scale;     // usually 1/global_batch
+  double grad_scale;    // usually 1/global_batch
   float* colsum;        // += column sums of dh (bias gradient), may be null
   double* colsum64;     // fp64 logits: column sums in double instead
   void* probs;          // optional softmax output [rows][ld_probs]
@@ -38,10 +38,10 @@ struct MseArgs {
   float* loss;
   double* loss64;       // fp64 outputs: double accumulators (loss64 / colsum64) instead
   int loss_slots;       // > 1: block b adds into loss[b % loss_slots]
-  float loss_scale;     // 1 / numel
+  double loss_scale;    // 1 / numel
   void* dh;
   int64_t ld_dh;
-  float grad_scale;     // 1 / numel
+  double grad_scale;    // 1 / numel
   float* colsum;
   double* colsum64;
   EpiSpec epi;          // last stage's epilogue (derivative from y)
@@ -143,7 +143,7 @@ struct FinalizeArgs {
   const double* stats_cur;  // [nslots][4] stats of the update just applied
   const double* slot_numel; // [nslots]
   int nslots;
-  float l2;
+  double l2;
   double* costs;            // costs[epoch]
   int epoch;
   float* ratios;            // [rows][nslots]
@@ -174,7 +174,7 @@ struct BnArgs {
   int param_dtype;        // DT_F32 or DT_F64 for gain/bias/running stats
   void* running_mean;     // [cols] updated in training mode
   void* running_var;
-  float eps, momentum;
+  double eps, momentum;   // doubles: fp64 models keep the reference's exact EMA / eps
   int training;
   double* save_mean;      // [cols] workspace: statistics used by this pass
   double* save_invstd;    // [cols]

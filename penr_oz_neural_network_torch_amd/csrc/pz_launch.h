@@ -78,11 +78,13 @@ struct GemmArgs {
   // per-tensor factors *scale_a * *scale_b (nullptr = 1) on top of alpha
   const float* scale_a;
   const float* scale_b;
-  int a_fmt;  // fp8 A operand format: 0 = e4m3, 1 = e5m2 (gradients; B stays e4m3)
+  int a_fmt;  // fp8 A operand format: 0 = e4m3, 1 = e5m2 (gradients of the dX GEMM)
+  int b_fmt;  // fp8 B operand format: 1 = e5m2 only for the weight-gradient GEMM X8ᵀ · dZ8
   // EPI_FWD extra output: e4m3 copy of C, out8[m*ldout8 + n] = sat(C * *out8_qscale), and the
   // running max |C| (atomicMax into *amax, which the caller zeroes) for delayed scaling
   uint8_t* out8;
   int64_t ldout8;
+  int out8_fmt;  // 0: e4m3 (EPI_FWD activations), 1: e5m2 (EPI_BWD: dZ for the next fp8 dW GEMM)
   const float* out8_qscale;
   float* amax;
   // split-K (set by the launcher, gemm_split()): K is cut into split_k slices computed by

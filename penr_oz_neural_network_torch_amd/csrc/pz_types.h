@@ -21,6 +21,8 @@ struct EpiSpec {
   uint32_t thresh16;  // drop element iff its 16-bit draw < thresh16  (thresh16 = round(p * 65536))
   float scale;        // 1 / (1 - p)
   float inv_scale;    // (1 - p)
+  double scale64;     // the same in double: fp64 kernels (fp64 models) drop out exactly like F.dropout
+  double inv_scale64;
   int drop_all;       // p >= 1: every element is dropped
   // Graph-replayed steps: keys above are per (seed, layer) only and the kernel mixes in the
   // epoch read from this device counter (epoch_key). nullptr: the keys are final (eager steps

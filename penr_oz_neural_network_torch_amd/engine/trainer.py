@@ -32,6 +32,7 @@ from __future__ import annotations
 import math
 import os
 import time
+from contextlib import nullcontext as _nullcontext
 from dataclasses import dataclass, field
 from datetime import datetime, timedelta
 
@@ -263,6 +264,20 @@ class FusedTrainer:
         # a GEMM's pending ones); within noise of priority 0 (profiles/r2_ab_opt_sched.txt)
         prio = int(os.environ.get("PZ_OPT_PRIO", "0"))
         self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
+        # PZ_DW_STREAM=1: the weight-gradient GEMMs of every layer but the first run on a stream of
+        # their own, concurrently with the dX GEMM chain (the critical path): a dW GEMM needs only
+        # dZ and the stage input, and nothing in the backward waits for it — its workgroups fill
+        # the CUs the dX chain's tiles leave idle (tile-count tails, epilogues) instead of running
+        # as a serial launch of its own
+        self.dw_stream = (torch.cuda.Stream(device=self.dev) if self.overlap and
+                          os.environ.get("PZ_DW_STREAM", "0") == "1" else None)
+        self._dw_done: list = []
+        self._g8_done: dict = {}  # stage index -> the dZ tensor whose e5m2 copy is current this step
+        self._g8_epi_ready: set = set()  # stages whose epilogue-written e5m2 dZ scale is calibrated
+        self._run_epoch = None
+        # PZ_FP8_DW=0: bf16 weight-gradient GEMMs under the fp8 policy
+        self._fp8_dw_on = os.environ.get("PZ_FP8_DW", "1") != "0"
+        self._dw_split = int(os.environ.get("PZ_DW_SPLIT", "1"))  # side-stream dW: 1 = no split-K
         # one launch per GEMM weight except the first layer's, which comes last anyway and
         # shares the final launch with the small accumulated parameters (biases, BN, embedding)
         gemm_w = [st.seg_w.offset for st in self.stages if st.kind == "gemm"]
@@ -483,6 +498,8 @@ class FusedTrainer:
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             self.opt_stream.wait_event(ready)
+            for ev in self._dw_done:  # gradients computed on the dW stream (PZ_DW_STREAM)
+                self.opt_stream.wait_event(ev)
             if self._pf_args is not None:
                 self._prefetch()
             for key, handles, stages in items:
@@ -554,6 +571,19 @@ class FusedTrainer:
                 continue
             st.fp8_bwd = True
             st.buffers["g8"] = torch.empty(st.buffers["g"].shape, device=self.dev, dtype=torch.float8_e5m2)
+        # fp8 dW for fp8 stages whose dZ is NOT quantised for a dX GEMM (the first layer): the next
+        # stage's fused dX GEMM writes dZ's e5m2 copy from its epilogue (delayed scaling), so the
+        # weight-gradient GEMM runs on e4m3 x e5m2 without a separate quantisation pass
+        for i, st in enumerate(self.stages):
+            st.g8_from_epi = False
+            nxt = self.stages[i + 1] if i + 1 < len(self.stages) else None
+            if (not self._fp8_dw_on or st.kind != "gemm" or not st.fp8 or getattr(st, "fp8_bwd", False)
+                    or nxt is None or nxt.kind != "gemm" or not st.has_epi or st.out_width % 256
+                    or st.in_width % 256 or rows_b % 64):
+                continue
+            st.g8_from_epi = True
+            st.buffers["g8"] = torch.empty(st.buffers["g"].shape, device=self.dev, dtype=torch.float8_e5m2)
+        self._g8_epi_ready = set()
         self.data8 = None
         if self.x8 is not None:
             # first-layer input: the device-resident dataset is quantised to e4m3 ONCE with a static
@@ -738,6 +768,7 @@ class FusedTrainer:
         """Enqueue one step. ``epoch=None``: hipGraph capture (epoch-dependent values from the
         device counter / tables; the side stream joins the capture stream at the end)."""
         capture = epoch is None
+        self._run_epoch = epoch  # None while a hipGraph is captured
         keys = self._keys(epoch)
         ops = torch.ops.pz
         main = torch.cuda.current_stream(self.dev)
@@ -750,6 +781,7 @@ class FusedTrainer:
             self._ov = (main, l2, 1.0)  # gradients arrive as the global mean (1/S-scaled heads)
             self._late_stages, self._late_handles = [], []
             self._side_pending = []
+            self._dw_done = []
 
         # (no zeroing pass: the previous step's update kernel reset the accumulated-gradient region
         # as it read it, and its step_finalize the loss slots)
@@ -811,6 +843,7 @@ class FusedTrainer:
         # ---------------- backward
         self._phase("pz.backward")
         handles = []
+        self._g8_done = {}  # this step's e5m2 dZ copies are produced anew
         g = last.buffers["g"]
         for si in range(len(self.stages) - 1, -1, -1):
             st = self.stages[si]
@@ -834,6 +867,9 @@ class FusedTrainer:
             if self._side_pending:  # (merged side updates not flushed by their last layer)
                 self._opt_async(self._side_pending)
                 self._side_pending = []
+            for ev in self._dw_done:  # every dW GEMM (and its stage-buffer reads) before the tail
+                main.wait_event(ev)
+            self._dw_done = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
@@ -1060,10 +1096,27 @@ class FusedTrainer:
             chunks = 1
         mine = []
         rows = w_grad.shape[0] // chunks
-        for c in range(chunks):
-            sl = slice(c * rows, (c + 1) * rows)
-            PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False, w_grad[sl] if chunks > 1 else w_grad)
-            mine.append(self.ctx.all_reduce_async(w_grad[sl] if chunks > 1 else w_grad))
+        f8 = self._fp8_dw(st, g, w_grad) if chunks == 1 else None
+        side = self.dw_stream is not None and before is not None and self._ov is not None
+        if side:  # PZ_DW_STREAM: concurrent with this layer's dX GEMM and the rest of the chain
+            ready = torch.cuda.Event()
+            ready.record(torch.cuda.current_stream(self.dev))
+            self.dw_stream.wait_event(ready)
+        with torch.cuda.stream(self.dw_stream) if side else _nullcontext():
+            for c in range(chunks):
+                sl = slice(c * rows, (c + 1) * rows)
+                if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
+                    x8, sx, g8, sg = f8
+                    PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg,
+                            max_split=self._dw_split if side else 0)
+                else:
+                    PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False,
+                            w_grad[sl] if chunks > 1 else w_grad, max_split=self._dw_split if side else 0)
+                mine.append(self.ctx.all_reduce_async(w_grad[sl] if chunks > 1 else w_grad))
+            if side:
+                done = torch.cuda.Event()
+                done.record(self.dw_stream)
+                self._dw_done.append(done)
         handles.extend(mine)
         # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
         # unless the GEMMs read the fp32 master itself (float32 policy)
@@ -1084,6 +1137,40 @@ class FusedTrainer:
                 self._opt_async(self._side_pending)
                 self._side_pending = []
         return out
+
+    def _quantize_g8(self, st: Stage, g):
+        """dZ of an fp8 stage -> its e5m2 copy (delayed scaling; the first step calibrates on its
+        own amax), once per step: the dW GEMM and the dX GEMM of the stage both consume it."""
+        g8 = st.buffers["g8"]
+        if self._g8_done.get(st.index) is g:
+            return g8
+        k, ops = st.index, torch.ops.pz
+        if not self._g8_calibrated:  # first step: current scaling from this gradient
+            ops.amax_abs(g, self.gamax[k:k + 1])
+            ops.scale_update(self.gamax[k:k + 1], self.gqs[k], 2.0, True, 57344.0)
+        ops.quantize_rows(g, g8, self.gqs[k], self.gamax[k:k + 1])
+        self._g8_done[st.index] = g
+        return g8
+
+    def _fp8_dw(self, st: Stage, g, w_grad):
+        """fp8 weight-gradient operands (BASELINE config 5): the stage input's e4m3 copy (written by
+        the previous GEMM's epilogue, or the gathered e4m3 dataset rows) and dZ's e5m2 copy, both
+        M/N-contiguous, with their dequantisation factors — or None (bf16 dW)."""
+        if not (self.fp8 and st.fp8 and self._fp8_dw_on):
+            return None
+        if getattr(st, "g8_from_epi", False):  # dZ's e5m2 copy came from the dX epilogue this step
+            if self._g8_done.get(st.index) is not g:
+                return None
+        elif not getattr(st, "fp8_bwd", False):
+            return None
+        i = st.index
+        x8, sx = (self.x8, self.xqs[1:2]) if i == 0 else (self.stages[i - 1].buffers.get("y8"), self.aqs[i - 1, 1:2])
+        if x8 is None or w_grad.dtype != torch.bfloat16:
+            return None
+        g8 = st.buffers["g8"]
+        if PF.gemm_path(x8, False, g8, False, w_grad) != "mfma":
+            return None
+        return x8, sx, self._quantize_g8(st, g), self.gqs[i, 1:2]
 
     def _dw_update(self, st: Stage, x_in, g) -> None:
         """dW GEMM + the weight's optimizer update in one launch (fuse_opt). The update writes the
@@ -1112,19 +1199,27 @@ class FusedTrainer:
             colsum = self.store.view(before.seg_b, self.grads) if (before.kind == "gemm" and before.seg_b is not None) \
                 else None
             mask = before.buffers.get("mask")
+            # the receiving stage's fp8 dW wants dZ in e5m2: written by this epilogue once its
+            # delayed scale is calibrated (first step: the amax of the bf16 dZ, below)
+            b = before.index
+            kw8 = {}
+            if getattr(before, "g8_from_epi", False) and b in self._g8_epi_ready:
+                kw8 = dict(out8=before.buffers["g8"], out8_qscale=self.gqs[b, 0:1], amax=self.gamax[b:b + 1])
             if getattr(st, "fp8_bwd", False):  # e5m2 dZ x e4m3 W on the scaled fp8 MFMA
-                k, g8 = st.index, st.buffers["g8"]
-                ops = torch.ops.pz
-                if not self._g8_calibrated:  # first step: current scaling from this gradient
-                    ops.amax_abs(g, self.gamax[k:k + 1])
-                    ops.scale_update(self.gamax[k:k + 1], self.gqs[k], 2.0, True, 57344.0)
-                ops.quantize_rows(g, g8, self.gqs[k], self.gamax[k:k + 1])
+                k, g8 = st.index, self._quantize_g8(st, g)
                 PF.gemm(g8, True, self.w8n[st.seg_w.offset], True, dx,
                         aux=None if mask is not None else before.buffers["y"], colsum=colsum, mode=PF.EPI_BWD,
-                        epi=(ei, ef), mask=mask, scale_a=self.gqs[k, 1:2], scale_b=self.wqs[st.w8_index, 1:2])
-                return dx, True
-            PF.gemm(g, True, self._w(st), True, dx, aux=None if mask is not None else before.buffers["y"],
-                    colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask)
+                        epi=(ei, ef), mask=mask, scale_a=self.gqs[k, 1:2], scale_b=self.wqs[st.w8_index, 1:2],
+                        **kw8)
+            else:
+                PF.gemm(g, True, self._w(st), True, dx, aux=None if mask is not None else before.buffers["y"],
+                        colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask, **kw8)
+            if kw8:
+                self._g8_done[b] = dx
+            elif getattr(before, "g8_from_epi", False) and rec is None and self._ov is not None \
+                    and self._run_epoch is not None:  # eager step: calibrate the delayed scale
+                torch.ops.pz.amax_abs(dx, self.gamax[b:b + 1])
+                self._g8_epi_ready.add(b)
             return dx, True
         no_epi_prev = before.kind in ("gemm",) and not before.has_epi and rec is None
         colsum = None

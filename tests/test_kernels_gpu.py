@@ -186,6 +186,25 @@ def test_gemm_fp8_e5m2_backward(native_lib, M, N, K):
     assert (out.double() - exact).abs().max().item() < 0.15 * exact.abs().max().item()
 
 
+@pytest.mark.parametrize("M,N,K", [(256, 256, 64), (512, 768, 320), (8192, 1024, 8192), (1024, 8192, 8192)])
+def test_gemm_fp8_weight_gradient(native_lib, M, N, K):
+    """fp8 dW (BASELINE config 5): dW[in, out] = X8ᵀ dZ8 with e4m3 activations X8 [K=batch, M] and
+    e5m2 output gradients dZ8 [K, N], BOTH M/N-contiguous (transposing 8-bit LDS reads, no
+    transposed copies), dequant scales, bf16 output; the skinny shapes run split-K. Checked
+    against fp64 on the same quantised values."""
+    x8 = (torch.randn(K, M, device=DEV) * 4).to(torch.float8_e4m3fn)
+    g8 = (torch.randn(K, N, device=DEV) * 1000).to(torch.float8_e5m2)
+    sa = torch.tensor([0.25], device=DEV)
+    sb = torch.tensor([1.0 / 4096], device=DEV)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert PF.gemm_path(x8, False, g8, False, out) == "mfma"
+    PF.gemm(x8, False, g8, False, out, scale_a=sa, scale_b=sb)
+    ref = (x8.double().t() @ g8.double()) * (0.25 / 4096)
+    err = (out.double() - ref).abs()
+    # bf16 output rounding (2^-8 relative) on top of an fp32-accumulated exact product
+    assert (err <= 2.0 ** -8 * ref.abs() + 1e-6 * ref.abs().max()).all(), err.max().item()
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (4096 + 64, 4096, 512), (256, 1024, 8192), (4096, 4096, 512)])
 def test_gemm_fp8_forward(native_lib, M, N, K):
     """e4m3 x e4m3 (v_mfma_scale_f32_32x32x64_f8f6f4) + dequant scales + fused stage epilogue +
