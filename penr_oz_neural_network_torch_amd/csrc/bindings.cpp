@@ -141,6 +141,8 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   p.b_kc = b_kc;
   p.in_dtype = dt_of(A);
   p.out_dtype = dt_of(C);
+  p.a_fmt = A.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;  // fp8 operand formats (gemm_path sees them too)
+  p.b_fmt = B.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
   p.alpha = static_cast<float>(alpha);
   p.accumulate = accumulate;
   if (bias.has_value() && bias->defined()) {
@@ -208,8 +210,6 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
                      force_generic, mask);
   p.scale_a = f32_scalar_ptr(scale_a, "scale_a");
   p.scale_b = f32_scalar_ptr(scale_b, "scale_b");
-  p.a_fmt = A.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
-  p.b_fmt = B.scalar_type() == at::kFloat8_e5m2 ? 1 : 0;
   TORCH_CHECK(p.b_fmt == 0 || (!a_kc && !b_kc), "pz::gemm: an e5m2 B operand needs the M/N-contiguous dW layout");
   if (out8.has_value() && out8->defined()) {
     TORCH_CHECK((out8->scalar_type() == at::kFloat8_e4m3fn || out8->scalar_type() == at::kFloat8_e5m2) &&

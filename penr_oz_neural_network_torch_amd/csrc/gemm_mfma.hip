@@ -498,8 +498,25 @@ PZ_DEV void epilogue_opt(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   }
 }
 
+// tools/gemm_stamps.hip (diagnostic build only): per-workgroup s_memrealtime stamps at the phase
+// boundaries (entry, first K step landed, main loop done, epilogue start, end) + XCC id into the
+// lab's debug buffer p.dbg — where a tile's time goes (guide §7, in-kernel stamps)
+#ifdef PZ_GEMM_STAMPS
+#define PZ_STAMP(i)                                                                                        \
+  do {                                                                                                     \
+    if (threadIdx.x == 0) {                                                                                \
+      uint64_t* st_ = p.dbg + 8 * static_cast<int64_t>(blockIdx.x);                                       \
+      st_[i] = __builtin_amdgcn_s_memrealtime();                                                           \
+      if ((i) == 0) st_[7] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11))); \
+    }                                                                                                      \
+  } while (0)
+#else
+#define PZ_STAMP(i) do {} while (0)
+#endif
+
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
+  PZ_STAMP(0);
   constexpr int BK = var_bk<VAR>();
   constexpr int KB = BK / 32;  // 32-deep MFMA K blocks per ring slot
   using C = Cfg<BM, BN, WM, WN, var_ns<VAR>(), BK>;
@@ -729,6 +746,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     stage(0, 0);
     wait_vm<0>();
     barrier();
+    PZ_STAMP(1);
     if (grp == 1) {
       if ((VAR == 21 || VAR == 31) && nk > 1) stage_b_t(1, T4{}, tw);
       barrier();
@@ -746,6 +764,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
       barrier();
     }
     if (grp == 0) barrier();
+    PZ_STAMP(2);
   } else {
 #pragma unroll
   for (int s = 0; s < NS - 1; ++s)
@@ -861,6 +880,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // ---------------------------------------------------------------- epilogue
   // static_for (not #pragma unroll): the acc array must only ever be indexed by compile-time
   // constants or it is demoted to scratch (guide §5.4 rule 20)
+  PZ_STAMP(3);
   OutT* __restrict__ Cp = static_cast<OutT*>(p.C);
   const AuxT* __restrict__ aux = static_cast<const AuxT*>(p.aux);
   const int g4 = 4 * (lane >> 4);
@@ -898,6 +918,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     }
   });
   }
+#ifdef PZ_GEMM_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's stores have left this CU
+  __syncthreads();
+  PZ_STAMP(4);
+#endif
 }
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>

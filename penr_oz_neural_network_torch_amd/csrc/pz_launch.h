@@ -94,6 +94,7 @@ struct GemmArgs {
   float* ws;       // [tiles * split_k][BM * BN] fp32
   int* counters;   // [tiles], zero; reset by the last arriver
   GemmOpt opt;     // EPI_OPT only
+  uint64_t* dbg;   // diagnostic phase stamps (tools/gemm_stamps.hip builds only); nullptr otherwise
 };
 
 // split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().

@@ -32,7 +32,6 @@ from __future__ import annotations
 import math
 import os
 import time
-from contextlib import nullcontext as _nullcontext
 from dataclasses import dataclass, field
 from datetime import datetime, timedelta
 
@@ -264,20 +263,11 @@ class FusedTrainer:
         # a GEMM's pending ones); within noise of priority 0 (profiles/r2_ab_opt_sched.txt)
         prio = int(os.environ.get("PZ_OPT_PRIO", "0"))
         self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
-        # PZ_DW_STREAM=1: the weight-gradient GEMMs of every layer but the first run on a stream of
-        # their own, concurrently with the dX GEMM chain (the critical path): a dW GEMM needs only
-        # dZ and the stage input, and nothing in the backward waits for it — its workgroups fill
-        # the CUs the dX chain's tiles leave idle (tile-count tails, epilogues) instead of running
-        # as a serial launch of its own
-        self.dw_stream = (torch.cuda.Stream(device=self.dev) if self.overlap and
-                          os.environ.get("PZ_DW_STREAM", "0") == "1" else None)
-        self._dw_done: list = []
         self._g8_done: dict = {}  # stage index -> the dZ tensor whose e5m2 copy is current this step
         self._g8_epi_ready: set = set()  # stages whose epilogue-written e5m2 dZ scale is calibrated
         self._run_epoch = None
         # PZ_FP8_DW=0: bf16 weight-gradient GEMMs under the fp8 policy
         self._fp8_dw_on = os.environ.get("PZ_FP8_DW", "1") != "0"
-        self._dw_split = int(os.environ.get("PZ_DW_SPLIT", "1"))  # side-stream dW: 1 = no split-K
         # one launch per GEMM weight except the first layer's, which comes last anyway and
         # shares the final launch with the small accumulated parameters (biases, BN, embedding)
         gemm_w = [st.seg_w.offset for st in self.stages if st.kind == "gemm"]
@@ -498,8 +488,6 @@ class FusedTrainer:
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             self.opt_stream.wait_event(ready)
-            for ev in self._dw_done:  # gradients computed on the dW stream (PZ_DW_STREAM)
-                self.opt_stream.wait_event(ev)
             if self._pf_args is not None:
                 self._prefetch()
             for key, handles, stages in items:
@@ -781,7 +769,6 @@ class FusedTrainer:
             self._ov = (main, l2, 1.0)  # gradients arrive as the global mean (1/S-scaled heads)
             self._late_stages, self._late_handles = [], []
             self._side_pending = []
-            self._dw_done = []
 
         # (no zeroing pass: the previous step's update kernel reset the accumulated-gradient region
         # as it read it, and its step_finalize the loss slots)
@@ -867,9 +854,6 @@ class FusedTrainer:
             if self._side_pending:  # (merged side updates not flushed by their last layer)
                 self._opt_async(self._side_pending)
                 self._side_pending = []
-            for ev in self._dw_done:  # every dW GEMM (and its stage-buffer reads) before the tail
-                main.wait_event(ev)
-            self._dw_done = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
@@ -1097,26 +1081,17 @@ class FusedTrainer:
         mine = []
         rows = w_grad.shape[0] // chunks
         f8 = self._fp8_dw(st, g, w_grad) if chunks == 1 else None
-        side = self.dw_stream is not None and before is not None and self._ov is not None
-        if side:  # PZ_DW_STREAM: concurrent with this layer's dX GEMM and the rest of the chain
-            ready = torch.cuda.Event()
-            ready.record(torch.cuda.current_stream(self.dev))
-            self.dw_stream.wait_event(ready)
-        with torch.cuda.stream(self.dw_stream) if side else _nullcontext():
-            for c in range(chunks):
-                sl = slice(c * rows, (c + 1) * rows)
-                if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
-                    x8, sx, g8, sg = f8
-                    PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg,
-                            max_split=self._dw_split if side else 0)
-                else:
-                    PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False,
-                            w_grad[sl] if chunks > 1 else w_grad, max_split=self._dw_split if side else 0)
-                mine.append(self.ctx.all_reduce_async(w_grad[sl] if chunks > 1 else w_grad))
-            if side:
-                done = torch.cuda.Event()
-                done.record(self.dw_stream)
-                self._dw_done.append(done)
+        # (measured, not kept: these dW GEMMs on a stream of their own beside the dX chain, without
+        # split-K: the concurrent GEMMs stretch each other, mlp4 1.26 vs 1.23 ms —
+        # profiles/r3_ab_dw_stream.txt)
+        for c in range(chunks):
+            sl = slice(c * rows, (c + 1) * rows)
+            if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
+                x8, sx, g8, sg = f8
+                PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
+            else:
+                PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False, w_grad[sl] if chunks > 1 else w_grad)
+            mine.append(self.ctx.all_reduce_async(w_grad[sl] if chunks > 1 else w_grad))
         handles.extend(mine)
         # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
         # unless the GEMMs read the fp32 master itself (float32 policy)

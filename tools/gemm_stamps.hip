@@ -1,0 +1,185 @@
+// Where a GEMM tile's time goes: builds the library's gemm_mfma kernel with PZ_GEMM_STAMPS (per
+// workgroup s_memrealtime stamps at entry / first K step landed / main loop done / epilogue start /
+// end, 10 ns resolution) and prints, for the mlp4 step's shapes with the trainer's REAL epilogues,
+// the median per-phase time of a workgroup and how the workgroups were spread over time
+// (dispatch waves). Diagnostic build only; the library never compiles the stamps.
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I penr_oz_neural_network_torch_amd/csrc \
+//         tools/gemm_stamps.hip -o scratch/gemm_stamps && scratch/gemm_stamps [case ...]
+#define PZ_GEMM_LAB 1
+#define PZ_GEMM_STAMPS 1
+#include "../penr_oz_neural_network_torch_amd/csrc/gemm_mfma.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+using namespace pz;
+
+#define CK(x)                                                                         \
+  do {                                                                                \
+    hipError_t e_ = (x);                                                              \
+    if (e_ != hipSuccess) {                                                           \
+      printf("HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__);   \
+      exit(1);                                                                        \
+    }                                                                                 \
+  } while (0)
+
+__global__ void fill_bf16(uint16_t* p, int64_t n, uint32_t seed) {
+  for (int64_t i = blockIdx.x * static_cast<int64_t>(blockDim.x) + threadIdx.x; i < n;
+       i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const uint32_t h = mix32(mix32(static_cast<uint32_t>(i) ^ seed) + static_cast<uint32_t>(i >> 32));
+    p[i] = f2bf(static_cast<float>(h >> 8) * (2.f / 16777216.f) - 1.f);
+  }
+}
+
+typedef hipError_t (*LaunchFn)(const GemmArgs&, hipStream_t);
+
+struct Case {
+  const char* name;
+  int M, N, K;
+  bool akc, bkc, f32out;
+  int mode;  // 0 plain store, 1 stage-0 forward (bias, ReLU, dropout, bitmask), 2 drop-ReLU-drop forward,
+             // 3 backward (bitmask ReLU derivative, dropout scales, bias-grad column sums)
+  int split;
+  LaunchFn fn;
+};
+
+static double med(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return v.empty() ? 0.0 : v[v.size() / 2];
+}
+
+int main(int argc, char** argv) {
+  const int B = 8192;
+  using F = LaunchFn;
+  std::vector<Case> cases = {
+      {"fwd_L1_store", B, 4096, 1024, true, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1", B, 4096, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L2", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"dX_L3_store", B, 4096, 1024, true, true, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
+      {"dX_L3", B, 4096, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
+      {"dX_L2", B, 4096, 4096, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
+      {"fwd_L3", B, 1024, 4096, true, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"dW_L3", 4096, 1024, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
+      {"dW_L1", 1024, 4096, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
+      {"dW_L2", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
+  };
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  for (const Case& c : cases) {
+    if (argc > 1) {
+      bool want = false;
+      for (int i = 1; i < argc; ++i) want |= strcmp(argv[i], c.name) == 0;
+      if (!want) continue;
+    }
+    const int64_t na = static_cast<int64_t>(c.M) * c.K, nb = static_cast<int64_t>(c.N) * c.K;
+    const int64_t nc = static_cast<int64_t>(c.M) * c.N;
+    uint16_t *A, *Bm, *C;
+    float *bias, *colsum;
+    uint8_t* mask;
+    CK(hipMalloc(&A, na * 2));
+    CK(hipMalloc(&Bm, nb * 2));
+    CK(hipMalloc(&C, nc * 2));
+    CK(hipMalloc(&bias, c.N * 4));
+    CK(hipMalloc(&colsum, c.N * 4));
+    const int64_t ldmask = (c.N + 63) / 64 * 8;
+    CK(hipMalloc(&mask, c.M * ldmask));
+    CK(hipMemset(bias, 0, c.N * 4));
+    CK(hipMemset(colsum, 0, c.N * 4));
+    CK(hipMemset(mask, 0x5A, c.M * ldmask));
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, A, na, 12345u);
+    hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, Bm, nb, 777u);
+    GemmArgs p{};
+    p.A = A; p.B = Bm; p.C = C;
+    p.M = c.M; p.N = c.N; p.K = c.K;
+    p.lda = c.akc ? c.K : c.M;
+    p.ldb = c.bkc ? c.K : c.N;
+    p.ldc = c.N;
+    p.a_kc = c.akc; p.b_kc = c.bkc;
+    p.in_dtype = DT_BF16;
+    p.out_dtype = DT_BF16;
+    p.alpha = 1.f;
+    p.idx_ld = c.N;
+    p.epi_mode = EPI_STORE;
+    EpiSpec e{};
+    e.act = ACT_NONE;
+    e.scale = e.scale64 = 1.25f;
+    e.inv_scale = e.inv_scale64 = 0.8f;
+    e.thresh16 = 13107;  // p = 0.2
+    e.key_pre = 0x1234567u;
+    e.key_post = 0x89abcdefu;
+    if (c.mode == 1) {  // stage 0: bias, ReLU, dropout after the ReLU, bitmask for the dX GEMM
+      p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; e.drop_post = 1; p.mask = mask; p.ldmask = ldmask;
+    } else if (c.mode == 2) {  // hidden ReLU stage: dropout, ReLU, dropout (+ bitmask)
+      p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; e.drop_pre = 1; e.drop_post = 1; p.mask = mask;
+      p.ldmask = ldmask;
+    } else if (c.mode == 3) {  // backward through a ReLU stage read from its bitmask + bias grad
+      p.epi_mode = EPI_BWD; e.act = ACT_RELU; e.drop_pre = 1; e.drop_post = 1; p.mask = mask; p.ldmask = ldmask;
+      p.colsum = colsum;
+    }
+    p.epi = e;
+    const int tiles = ((c.M + 255) / 256) * ((c.N + 255) / 256);
+    const int nwg = tiles * c.split;
+    p.split_k = c.split;
+    float* ws = nullptr;
+    const int64_t slab_floats = c.split > 1 ? static_cast<int64_t>(tiles) * c.split * 65536 : 0;
+    if (slab_floats) CK(hipMalloc(&ws, slab_floats * 4));
+    int* counters;
+    CK(hipMalloc(&counters, tiles * 4));
+    CK(hipMemset(counters, 0, tiles * 4));
+    uint64_t* stamps;
+    CK(hipMalloc(&stamps, static_cast<int64_t>(nwg) * 64));
+    CK(hipMemset(stamps, 0, static_cast<int64_t>(nwg) * 64));
+    p.ws = ws;
+    p.counters = counters;
+    p.dbg = stamps;
+    for (int w = 0; w < 5; ++w) CK(c.fn(p, st));  // warm-up (clocks, caches)
+    CK(hipMemsetAsync(stamps, 0, static_cast<int64_t>(nwg) * 64, st));
+    CK(hipStreamSynchronize(st));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0, st));
+    CK(c.fn(p, st));
+    CK(hipEventRecord(e1, st));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<uint64_t> h(static_cast<size_t>(nwg) * 8);
+    CK(hipMemcpy(h.data(), stamps, h.size() * 8, hipMemcpyDeviceToHost));
+    uint64_t t0 = ~0ull, t1 = 0;
+    for (int w = 0; w < nwg; ++w) {
+      t0 = std::min(t0, h[8 * w + 0]);
+      t1 = std::max(t1, std::max(h[8 * w + 4], h[8 * w + 2]));
+    }
+    std::vector<double> pro, loop, red, epi, tot, start;
+    for (int w = 0; w < nwg; ++w) {
+      const uint64_t* s = &h[8 * w];
+      const bool finished = s[4] != 0;  // non-last split-K slices return before stamp 4
+      pro.push_back((s[1] - s[0]) * 0.01);
+      loop.push_back((s[2] - s[1]) * 0.01);
+      start.push_back((s[0] - t0) * 0.01);
+      if (finished) {
+        red.push_back((s[3] - s[2]) * 0.01);
+        epi.push_back((s[4] - s[3]) * 0.01);
+        tot.push_back((s[4] - s[0]) * 0.01);
+      }
+    }
+    std::vector<double> st_sorted = start;
+    std::sort(st_sorted.begin(), st_sorted.end());
+    const double flop = 2.0 * c.M * c.N * c.K;
+    printf("%-13s %5d WGs  kernel %.1f us (%.0f TF/s)  span %.1f us | per WG median: prologue %.2f  main loop %.2f "
+           "(%.3f us/K-step)  split-K %.2f  epilogue %.2f  total %.2f | start p50 %.1f p90 %.1f max %.1f us\n",
+           c.name, nwg, ms * 1e3, flop / (ms * 1e-3) / 1e12, (t1 - t0) * 0.01, med(pro), med(loop),
+           med(loop) / (c.K / 64 / c.split), med(red), med(epi), med(tot), st_sorted[st_sorted.size() / 2],
+           st_sorted[st_sorted.size() * 9 / 10], st_sorted.back());
+    fflush(stdout);
+    CK(hipFree(A)); CK(hipFree(Bm)); CK(hipFree(C)); CK(hipFree(bias)); CK(hipFree(colsum)); CK(hipFree(mask));
+    if (ws) CK(hipFree(ws));
+    CK(hipFree(counters)); CK(hipFree(stamps));
+  }
+  return 0;
+}
