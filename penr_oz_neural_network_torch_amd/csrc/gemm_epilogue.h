@@ -277,6 +277,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 #pragma unroll
         for (int o = 1; o < L::RED; o <<= 1) cs[j][r] += __shfl_xor(cs[j][r], o, 64);
   }
+  PZ_STAMP(5);  // (diagnostic builds: stage math + LDS image writes done, wave 0)
   __syncthreads();
   uint16_t* __restrict__ Cp = static_cast<uint16_t*>(p.C);
   // fp8 copy of the stored bf16 tile: e4m3 activations (forward) / e5m2 dZ (backward)
@@ -323,6 +324,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
             byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
     }
   }
+  PZ_STAMP(6);  // (stores issued)
   if (want8 && p.amax != nullptr) {  // one atomic per workgroup (same-address atomics serialise)
     amax = wave_max(amax);
     constexpr int NW = WM * WN;

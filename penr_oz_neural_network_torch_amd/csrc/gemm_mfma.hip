@@ -47,7 +47,7 @@ constexpr int kBK = 32;  // K depth of one ring slot (BK64 variants: two of thes
 // Per-variant ring geometry: VAR 20/21/30/31 stage 64-deep K steps into two 64 KiB slots (one
 // MFMA interval = 64 MFMAs per wave, half the barriers per FLOP of the 32-deep ring)
 template <int VAR> constexpr int var_bk() {
-  return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31 || VAR == 12 || VAR == 13) ? 64 : 32;
+  return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31 || VAR == 32 || VAR == 12 || VAR == 13) ? 64 : 32;
 }
 template <int VAR> constexpr int var_ns() { return VAR == 5 ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4); }
 
@@ -395,6 +395,22 @@ PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int split, int& tm, i
   tn = in_group / gsz;
 }
 
+// tools/gemm_stamps.hip (diagnostic build only): per-workgroup s_memrealtime stamps at the phase
+// boundaries (entry, first K step landed, main loop done, epilogue start, end) + XCC id into the
+// lab's debug buffer p.dbg — where a tile's time goes (guide §7, in-kernel stamps)
+#ifdef PZ_GEMM_STAMPS
+#define PZ_STAMP(i)                                                                                        \
+  do {                                                                                                     \
+    if (threadIdx.x == 0) {                                                                                \
+      uint64_t* st_ = p.dbg + 8 * static_cast<int64_t>(blockIdx.x);                                       \
+      st_[i] = __builtin_amdgcn_s_memrealtime();                                                           \
+      if ((i) == 0) st_[7] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11))); \
+    }                                                                                                      \
+  } while (0)
+#else
+#define PZ_STAMP(i) do {} while (0)
+#endif
+
 #include "gemm_epilogue.h"
 
 // EPI_OPT: the tile's accumulators are a block of the weight gradient g = alpha*AB; instead of
@@ -498,21 +514,6 @@ PZ_DEV void epilogue_opt(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   }
 }
 
-// tools/gemm_stamps.hip (diagnostic build only): per-workgroup s_memrealtime stamps at the phase
-// boundaries (entry, first K step landed, main loop done, epilogue start, end) + XCC id into the
-// lab's debug buffer p.dbg — where a tile's time goes (guide §7, in-kernel stamps)
-#ifdef PZ_GEMM_STAMPS
-#define PZ_STAMP(i)                                                                                        \
-  do {                                                                                                     \
-    if (threadIdx.x == 0) {                                                                                \
-      uint64_t* st_ = p.dbg + 8 * static_cast<int64_t>(blockIdx.x);                                       \
-      st_[i] = __builtin_amdgcn_s_memrealtime();                                                           \
-      if ((i) == 0) st_[7] = static_cast<uint64_t>(__builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11))); \
-    }                                                                                                      \
-  } while (0)
-#else
-#define PZ_STAMP(i) do {} while (0)
-#endif
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
@@ -667,11 +668,11 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
   // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
   // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
-  constexpr bool BUF_A = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 31);
-  constexpr bool BUF_B = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 31);
+  constexpr bool BUF_A = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 32);
+  constexpr bool BUF_B = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 32);
   constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
   // VAR 30/31: full row tiles of the K-contiguous operands (use_bk64 checks M % BM, N % BN)
-  constexpr bool FULL_KC = VAR == 30 || VAR == 31 || VAR == 12 || VAR == 13;
+  constexpr bool FULL_KC = VAR == 30 || VAR == 31 || VAR == 32 || VAR == 12 || VAR == 13;
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
   const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;
@@ -788,6 +789,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     };
     wait_step(min(nk, NS - 1) - 1);  // step 0 landed
     barrier();
+    PZ_STAMP(1);
     if (grp == 1) barrier();
     for (int t = 0; t < nk; ++t) {
       if (VAR != 2 && t + NS - 1 < nk) stage(t + NS - 1, (t + NS - 1) % NS);
@@ -813,8 +815,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
       barrier();
     }
     if (grp == 0) barrier();
+    PZ_STAMP(2);
     if constexpr (PF) wait_vm<0>();  // no prefetch DMA may outlive the workgroup's LDS
-  } else
+  } else {
+  PZ_STAMP(1);  // (4-wave tiles: before the first wait)
   for (int t = 0; t < nk; ++t) {
     // slot t landed: everything newer than step t (at most NS-2 steps) may stay in flight
     wait_newer<C::G, NS - 2>(min(nk - 1, t + NS - 2) - t);
@@ -825,12 +829,70 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
     read_frags(t % NS, f);
     mfma_step(f);
   }
+  PZ_STAMP(2);
+  }
   }  // BK
 
   // ---------------------------------------------------------------- split-K reduction
-  // (guide "In-launch split-K reduction": plain slab stores, vmcnt(0), barrier, ONE agent-scope
-  // release + relaxed ticket; the last arriver acquires, sums the other slabs, runs the epilogue)
-  if (split > 1) {
+  // Write-through hand-off (MI355X_MICROARCH "publish-large" / "splitk-seam", hand-off table row
+  // 1): every slice stores its fp32 slab with `sc1` (write-through) 16-B buffer stores, drains
+  // them (vmcnt(0)), joins a barrier, and ONE lane takes a relaxed agent-scope ticket; the slice
+  // whose add returned split-1 sums the other slabs with `sc1` loads (after a barrier its waves
+  // join) and runs the epilogue. No release fence (its L2 write-back of every dirty line of the
+  // XCD cost ~2.7x the publish, measured 19-23 us of a split-K GEMM's 85-95 us) and no acquire.
+  // VAR 32 (lab A/B) keeps the plain-store + release/acquire form.
+  constexpr bool WT_SLABS = VAR != 32;
+  if (split > 1 && WT_SLABS) {
+    constexpr int CH = ACC32 ? TM8 * TN8 * 4 : C::TM * C::TN;  // f32x4 chunks per lane
+    const int tid = threadIdx.x;
+    auto get_chunk = [&](auto cc) -> f32x4_t {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (ACC32) {
+        constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
+        return f32x4_t{acc[i][j][q], acc[i][j][q + 1], acc[i][j][q + 2], acc[i][j][q + 3]};
+      } else {
+        return acc[c / C::TN][c % C::TN];
+      }
+    };
+    auto add_chunk = [&](auto cc, f32x4_t v) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (ACC32) {
+        constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
+        acc[i][j][q] += v[0]; acc[i][j][q + 1] += v[1]; acc[i][j][q + 2] += v[2]; acc[i][j][q + 3] += v[3];
+      } else {
+        acc[c / C::TN][c % C::TN] += v;
+      }
+    };
+    constexpr int kSlabBytes = BM * BN * 4;
+    // one descriptor per tile's slab group (split x 256 KiB: 32-bit offsets always suffice)
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.ws + static_cast<int64_t>(tile_id) * split * (BM * BN), 0,
+                                                      split * kSlabBytes, 0x00020000);
+    constexpr int kSc1 = 16;  // cache-policy bit sc1
+    static_for<CH>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, get_chunk(cc)), rs,
+                                             slice * kSlabBytes + (c * C::NT + tid) * 16, 0, kSc1);
+    });
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    PZ_LDS int* flag = (PZ_LDS int*)(smem);
+    if (tid == 0) {
+      const int prev = __hip_atomic_fetch_add(p.counters + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = prev == split - 1;
+      if (prev == split - 1) p.counters[tile_id] = 0;  // ready for the next launch
+    }
+    __syncthreads();
+    if (*flag == 0) return;  // block-uniform: another slice finishes this tile
+    for (int sl = 0; sl < split; ++sl) {
+      if (sl == slice) continue;
+      static_for<CH>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        add_chunk(cc, __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                       rs, sl * kSlabBytes + (c * C::NT + tid) * 16, 0, kSc1)));
+      });
+    }
+  }
+  if (split > 1 && !WT_SLABS) {
     constexpr int CH = ACC32 ? TM8 * TN8 * 4 : C::TM * C::TN;  // f32x4 chunks per lane
     const int tid = threadIdx.x;
     auto get_chunk = [&](auto cc) -> f32x4_t {

@@ -42,9 +42,10 @@ struct Case {
   int M, N, K;
   bool akc, bkc, f32out;
   int mode;  // 0 plain store, 1 stage-0 forward (bias, ReLU, dropout, bitmask), 2 drop-ReLU-drop forward,
-             // 3 backward (bitmask ReLU derivative, dropout scales, bias-grad column sums)
+             // 3 backward (bitmask ReLU derivative, dropout scales, bias-grad column sums), 4-6 see below
   int split;
   LaunchFn fn;
+  int f8 = 0;  // 0 bf16, 1 e4m3 x e4m3 (forward), 2 e5m2 x e4m3 (backward dX), 3 e4m3 x e5m2 (dW)
 };
 
 static double med(std::vector<double> v) {
@@ -66,6 +67,28 @@ int main(int argc, char** argv) {
       {"dW_L3", 4096, 1024, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
       {"dW_L1", 1024, 4096, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
       {"dW_L2", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
+      // A/B: the split-K slabs published with plain stores + release / acquire fences (VAR 32)
+      {"fwd_L3_rel", B, 1024, 4096, true, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 32>},
+      {"dW_L3_rel", 4096, 1024, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 32>},
+      // epilogue breakdown on fwd_L1: 4 = bias + ReLU + bitmask (no dropout), 5 = bias + ReLU +
+      // dropout (no bitmask), 6 = drop-ReLU-drop without the bitmask
+      {"fwd_L1_nodrop", B, 4096, 1024, true, false, false, 4, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1_nomask", B, 4096, 1024, true, false, false, 5, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1_drd", B, 4096, 1024, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1_relu", B, 4096, 1024, true, false, false, 7, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1_bias", B, 4096, 1024, true, false, false, 8, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1_fwd0", B, 4096, 1024, true, false, false, 9, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1_drd_nm", B, 4096, 1024, true, false, false, 6, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      // the fp8 policy's GEMMs (mlp8192 [1024, 8192, 1024], batch 8192); operand bytes are
+      // arbitrary (timing only)
+      {"f8_fwd_L1_st", B, 8192, 1024, true, true, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>, 1},
+      {"f8_fwd_L1", B, 8192, 1024, true, true, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>, 1},
+      {"f8_fwd_L1_b64", B, 8192, 1024, true, true, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 12>, 1},
+      {"f8_fwd_L2", B, 1024, 8192, true, true, false, 0, 1, (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>, 1},
+      {"f8_dX_L2", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>, 2},
+      {"f8_dX_L2_b64", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 13>, 2},
+      {"f8_dW_L2", 8192, 1024, B, false, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14>, 3},
+      {"f8_dW_L1", 1024, 8192, B, false, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14>, 3},
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -99,7 +122,9 @@ int main(int argc, char** argv) {
     p.ldb = c.bkc ? c.K : c.N;
     p.ldc = c.N;
     p.a_kc = c.akc; p.b_kc = c.bkc;
-    p.in_dtype = DT_BF16;
+    p.in_dtype = c.f8 ? DT_FP8 : DT_BF16;
+    p.a_fmt = c.f8 == 2 ? 1 : 0;
+    p.b_fmt = c.f8 == 3 ? 1 : 0;
     p.out_dtype = DT_BF16;
     p.alpha = 1.f;
     p.idx_ld = c.N;
@@ -116,12 +141,25 @@ int main(int argc, char** argv) {
     } else if (c.mode == 2) {  // hidden ReLU stage: dropout, ReLU, dropout (+ bitmask)
       p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; e.drop_pre = 1; e.drop_post = 1; p.mask = mask;
       p.ldmask = ldmask;
+    } else if (c.mode == 4) {
+      p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; p.mask = mask; p.ldmask = ldmask;
+    } else if (c.mode == 5) {
+      p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; e.drop_post = 1;
+    } else if (c.mode == 6) {
+      p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; e.drop_pre = 1; e.drop_post = 1;
+    } else if (c.mode == 7) {
+      p.epi_mode = EPI_FWD; e.act = ACT_RELU;
+    } else if (c.mode == 8) {
+      p.epi_mode = EPI_FWD; p.bias = bias;
+    } else if (c.mode == 9) {
+      p.epi_mode = EPI_FWD;
     } else if (c.mode == 3) {  // backward through a ReLU stage read from its bitmask + bias grad
       p.epi_mode = EPI_BWD; e.act = ACT_RELU; e.drop_pre = 1; e.drop_post = 1; p.mask = mask; p.ldmask = ldmask;
       p.colsum = colsum;
     }
     p.epi = e;
-    const int tiles = ((c.M + 255) / 256) * ((c.N + 255) / 256);
+    const int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8> ? 128 : 256;
+    const int tiles = ((c.M + bm - 1) / bm) * ((c.N + bm - 1) / bm);
     const int nwg = tiles * c.split;
     p.split_k = c.split;
     float* ws = nullptr;
@@ -155,7 +193,7 @@ int main(int argc, char** argv) {
       t0 = std::min(t0, h[8 * w + 0]);
       t1 = std::max(t1, std::max(h[8 * w + 4], h[8 * w + 2]));
     }
-    std::vector<double> pro, loop, red, epi, tot, start;
+    std::vector<double> pro, loop, red, epi, tot, start, emath, eissue, edrain;
     for (int w = 0; w < nwg; ++w) {
       const uint64_t* s = &h[8 * w];
       const bool finished = s[4] != 0;  // non-last split-K slices return before stamp 4
@@ -165,6 +203,11 @@ int main(int argc, char** argv) {
       if (finished) {
         red.push_back((s[3] - s[2]) * 0.01);
         epi.push_back((s[4] - s[3]) * 0.01);
+        if (s[5] && s[6]) {
+          emath.push_back((s[5] - s[3]) * 0.01);
+          eissue.push_back((s[6] - s[5]) * 0.01);
+          edrain.push_back((s[4] - s[6]) * 0.01);
+        }
         tot.push_back((s[4] - s[0]) * 0.01);
       }
     }
@@ -176,6 +219,7 @@ int main(int argc, char** argv) {
            c.name, nwg, ms * 1e3, flop / (ms * 1e-3) / 1e12, (t1 - t0) * 0.01, med(pro), med(loop),
            med(loop) / (c.K / 64 / c.split), med(red), med(epi), med(tot), st_sorted[st_sorted.size() / 2],
            st_sorted[st_sorted.size() * 9 / 10], st_sorted.back());
+    if (!emath.empty()) printf("    epilogue (wave 0): stage math + LDS image %.2f  image read + stores issued %.2f  store drain %.2f\n", med(emath), med(eissue), med(edrain));
     fflush(stdout);
     CK(hipFree(A)); CK(hipFree(Bm)); CK(hipFree(C)); CK(hipFree(bias)); CK(hipFree(colsum)); CK(hipFree(mask));
     if (ws) CK(hipFree(ws));
