@@ -94,6 +94,36 @@ PZ_DEV void dropout_relu_dropout_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, ui
   }
 }
 
+// EK_RELU's single pass: keep = (drop_pre ? pre bit : 1) & (drop_post ? post bit : 1), then
+// y = keep ? (act(z) * m1) * m2 : 0. With a positive scale, act(z * m1) == act(z) * m1 for act in
+// {NONE, ReLU}, so this equals the separate passes bit for bit when the host passes (m1, m2) =
+// (scale^2, 1) for ReLU with both dropouts (the combined form above) and (pre scale or 1, post
+// scale or 1) otherwise (multiplying by 1 is exact)
+template <class L>
+PZ_DEV void relu_dropout_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, uint32_t pr_row, bool relu, float m1, float m2) {
+  const uint32_t th = e.thresh16;
+#pragma unroll
+  for (int j = 0; j < L::COLS; ++j) {
+    const uint32_t pr = pr_row + static_cast<uint32_t>(L::n_off(j) / 2);
+    uint32_t keep = e.drop_all ? 0u : 0xFu;
+    if (e.drop_pre) {
+      const uint32_t a0 = mix32(pr ^ e.key_pre), a1 = mix32((pr + 1u) ^ e.key_pre);
+      keep &= ((a0 & 0xFFFFu) >= th ? 1u : 0u) | ((a0 >> 16) >= th ? 2u : 0u) | ((a1 & 0xFFFFu) >= th ? 4u : 0u) |
+              ((a1 >> 16) >= th ? 8u : 0u);
+    }
+    if (e.drop_post) {
+      const uint32_t c0 = mix32(pr ^ e.key_post), c1 = mix32((pr + 1u) ^ e.key_post);
+      keep &= ((c0 & 0xFFFFu) >= th ? 1u : 0u) | ((c0 >> 16) >= th ? 2u : 0u) | ((c1 & 0xFFFFu) >= th ? 4u : 0u) |
+              ((c1 >> 16) >= th ? 8u : 0u);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float x = relu ? fmaxf(v[j][r], 0.f) : v[j][r];
+      v[j][r] = ((keep >> r) & 1u) ? (x * m1) * m2 : 0.f;
+    }
+  }
+}
+
 template <int COLS>
 PZ_DEV void act_fwd_row(f32x4_t (&v)[COLS], int act) {
 #define PZ_ACT_LOOP(expr)                                                       \
@@ -165,7 +195,18 @@ PZ_DEV u32x2_t to_e4m3x8(const float (&x)[8], float qs) {
   return out;
 }
 
-template <int BM, int BN, int WM, int WN, class L, bool FWD_ONLY = false, class Acc>
+// Compile-time epilogue kinds. The generic epilogue (EK_ANY) carries every transform — sigmoid /
+// tanh with IEEE reciprocals, both dropout forms, aux-tile derivatives — unrolled over the tile's
+// rows: ~20k instructions, and it measured ~5 us per tile of instruction-fetch stalls with EVERY
+// transform switched off (tools/gemm_stamps.hip: stage-math phase 8.6 us in EPI_FWD with nothing
+// enabled vs 3.3 us in EPI_STORE). The MLP's stages use three shapes, each specialised to only the
+// code it runs (host: epi_kind()):
+//   EK_STORE    alpha * acc -> bf16 (weight gradients)
+//   EK_RELU     EPI_FWD with act NONE / RELU: bias, dropout pre / post, ReLU bitmask, fp8 copy
+//   EK_BWD_MASK EPI_BWD through a ReLU stage from its bitmask: dropout scales, column sums, e5m2 copy
+constexpr int EK_ANY = 0, EK_STORE = 1, EK_RELU = 2, EK_BWD_MASK = 3;
+
+template <int BM, int BN, int WM, int WN, class L, bool FWD_ONLY = false, int EK = EK_ANY, class Acc>
 PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0, int n0, int wm, int wn, int lane,
                          float alpha) {
   constexpr int NT = WM * WN * 64;
@@ -177,12 +218,14 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   static_assert(WTN == 64, "the ReLU bitmask epilogue assumes 64-column wave tiles");
   const int tid = threadIdx.x;
   const int my_row = tid / CHUNKS_PER_ROW, my_chunk = tid % CHUNKS_PER_ROW;
-  const bool bwd = !FWD_ONLY && p.epi_mode == EPI_BWD;  // FWD_ONLY: no colsum / backward code
+  // FWD_ONLY: no colsum / backward code
+  const bool bwd = EK == EK_BWD_MASK || (EK == EK_ANY && !FWD_ONLY && p.epi_mode == EPI_BWD);
   const EpiSpec e = epi_resolve(p.epi);  // graph-replayed steps: epoch from the device counter
   const int ml0 = wm * WTM + L::m_lane(lane);  // + MSTEP*i
   const int nlane = L::n_lane(lane);
   const int nl0 = wn * WTN + nlane;            // + n_off(j)
-  const bool use_mask = p.mask != nullptr;
+  const bool use_mask = EK == EK_BWD_MASK || (EK != EK_STORE && p.mask != nullptr);
+  constexpr bool kColsum = !FWD_ONLY && (EK == EK_ANY || EK == EK_BWD_MASK);
 
   // ReLU bitmask (EPI_BWD): 8 bytes per accumulator row, issued before the barrier so the
   // loads fly while the slower waves finish their last MFMAs
@@ -198,7 +241,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   }
 
   __syncthreads();  // every wave is done reading the ring
-  if (bwd && !use_mask) {
+  if (EK == EK_ANY && bwd && !use_mask) {
     const uint16_t* __restrict__ aux = static_cast<const uint16_t*>(p.aux);
     u32x4_t v[PASSES];
 #pragma unroll
@@ -220,14 +263,19 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 #pragma unroll
   for (int j = 0; j < COLS; ++j) {
     const int n = n0 + nl0 + L::n_off(j);
-    bias4[j] = (!bwd && p.bias != nullptr && n < p.N) ? *reinterpret_cast<const f32x4_t*>(p.bias + n)
-                                                       : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    bias4[j] = ((EK == EK_ANY || EK == EK_RELU) && !bwd && p.bias != nullptr && n < p.N)
+                   ? *reinterpret_cast<const f32x4_t*>(p.bias + n)
+                   : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
   f32x4_t cs[COLS];
 #pragma unroll
   for (int j = 0; j < COLS; ++j) cs[j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   const uint64_t col0 = static_cast<uint64_t>(n0 + nl0);
   const float bwd_scale = (e.drop_post ? e.scale : 1.f) * (e.drop_pre ? e.scale : 1.f);
+  const bool relu_on = e.act == ACT_RELU;
+  const bool both = e.drop_pre && e.drop_post;
+  const float rd_m1 = relu_on && both ? e.scale * e.scale : (e.drop_pre ? e.scale : 1.f);
+  const float rd_m2 = relu_on && both ? 1.f : (e.drop_post ? e.scale : 1.f);
   static_for<ROWS>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
     const int ml = ml0 + L::MSTEP * i;
@@ -236,7 +284,10 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     f32x4_t v[COLS];
 #pragma unroll
     for (int j = 0; j < COLS; ++j) v[j] = L::get(acc, i, j) * alpha + bias4[j];
-    if (!bwd) {
+    if constexpr (EK == EK_STORE) {
+    } else if constexpr (EK == EK_RELU) {  // (dispatcher: EPI_FWD, act NONE or RELU)
+      relu_dropout_row<L>(v, e, pr_row, relu_on, rd_m1, rd_m2);
+    } else if (!bwd) {
       if (p.epi_mode == EPI_FWD) {
         if (e.drop_pre && e.drop_post && e.act == ACT_RELU && !e.drop_all) {
           dropout_relu_dropout_row<L>(v, e, pr_row);
@@ -246,13 +297,13 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
           if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
         }
       }
-    } else if (use_mask) {
+    } else if (EK == EK_BWD_MASK || use_mask) {
       // ReLU stage: y > 0  <=>  kept by drop_post AND kept by drop_pre AND z > 0, so the whole
       // derivative chain is one bit times the dropout scales — no hashes in the backward
       act_bwd_mask_row<L>(v, mbits[i], nlane);
 #pragma unroll
       for (int j = 0; j < COLS; ++j) v[j] *= bwd_scale;
-    } else {
+    } else if constexpr (EK == EK_ANY) {
       if (e.drop_post) dropout_row<L>(v, e, e.key_post, pr_row);
       if (e.act != ACT_NONE) act_bwd_row<BN, L>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
       if (e.drop_pre) dropout_row<L>(v, e, e.key_pre, pr_row);
@@ -261,7 +312,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     for (int j = 0; j < COLS; ++j)
       *reinterpret_cast<PZ_LDS u32x2_t*>(smem + cimg_off<BN>(ml, nl0 + L::n_off(j))) =
           u32x2_t{pack_bf2(v[j][0], v[j][1]), pack_bf2(v[j][2], v[j][3])};
-    if (!FWD_ONLY && p.colsum != nullptr && m0 + ml < p.M) {
+    if (kColsum && p.colsum != nullptr && m0 + ml < p.M) {
 #pragma unroll
       for (int j = 0; j < COLS; ++j) cs[j] += v[j];
     }
@@ -269,7 +320,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   });
   // column sums: reduce across the lanes now, issue the atomics after the tile is stored — the
   // barrier below would otherwise wait (vmcnt(0)) for every contended atomic to come back
-  if (!FWD_ONLY && p.colsum != nullptr) {
+  if (kColsum && p.colsum != nullptr) {
 #pragma unroll
     for (int j = 0; j < COLS; ++j)
 #pragma unroll
@@ -281,7 +332,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   __syncthreads();
   uint16_t* __restrict__ Cp = static_cast<uint16_t*>(p.C);
   // fp8 copy of the stored bf16 tile: e4m3 activations (forward) / e5m2 dZ (backward)
-  const bool want8 = p.out8 != nullptr && (bwd ? p.out8_fmt == 1 : p.out8_fmt == 0);
+  const bool want8 = EK != EK_STORE && p.out8 != nullptr && (bwd ? p.out8_fmt == 1 : p.out8_fmt == 0);
   const float qs = want8 ? *p.out8_qscale : 1.f;
   float amax = 0.f;
 #pragma unroll
@@ -339,7 +390,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       atomicMax(reinterpret_cast<unsigned int*>(p.amax), __float_as_uint(m));
     }
   }
-  if (!FWD_ONLY && p.colsum != nullptr) {
+  if (kColsum && p.colsum != nullptr) {
     // the WM waves that share a column range meet in LDS (the image has been read out), then ONE
     // atomic per tile column, 64 consecutive columns per wave instruction: the full-rate atomic
     // shape (256 contiguous bytes), instead of 4-lane instructions from every wave (measured:

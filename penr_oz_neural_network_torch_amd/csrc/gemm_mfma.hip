@@ -515,8 +515,9 @@ PZ_DEV void epilogue_opt(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 }
 
 
-template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR, int EK = EK_ANY>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
+  static_assert(EK == EK_ANY || std::is_same<OutT, uint16_t>::value, "specialised epilogues: bf16 output");
   PZ_STAMP(0);
   constexpr int BK = var_bk<VAR>();
   constexpr int KB = BK / 32;  // 32-deep MFMA K blocks per ring slot
@@ -948,10 +949,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   const int g4 = 4 * (lane >> 4);
   if constexpr (ACC32) {
     const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
-    if constexpr (F8_BWD || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
-    else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    if constexpr (F8_BWD || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true, EK>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
   } else if constexpr (std::is_same<OutT, uint16_t>::value) {
-    epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
+    epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
   } else if (p.epi_mode == EPI_OPT) {
     epilogue_opt<C>(p, acc, smem, m0, n0, wm, wn, lane);
   } else {
@@ -987,10 +988,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
 #endif
 }
 
-template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR>
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR, int EK = EK_ANY>
 hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
   using C = Cfg<BM, BN, WM, WN, var_ns<VAR>(), var_bk<VAR>()>;
-  auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR>;
+  auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR, EK>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -1058,6 +1059,36 @@ bool use_bk64(const GemmArgs& p, bool buf) {
   return !off && buf && full && p.K % 64 == 0 && (p.K / 64) % split == 0;
 }
 
+// which specialised epilogue (gemm_epilogue.h: EK_*) covers these arguments
+int epi_kind(const GemmArgs& p) {
+  static const bool off = [] {  // PZ_GEMM_EK=0: the generic epilogue everywhere (A/B)
+    const char* e = getenv("PZ_GEMM_EK");
+    return e != nullptr && atoi(e) == 0;
+  }();
+  if (off || p.out_dtype != DT_BF16 || p.accumulate) return EK_ANY;
+  if (p.epi_mode == EPI_STORE && p.bias == nullptr && p.colsum == nullptr && p.mask == nullptr && p.out8 == nullptr)
+    return EK_STORE;
+  if (p.epi_mode == EPI_FWD && (p.epi.act == ACT_NONE || p.epi.act == ACT_RELU) && p.colsum == nullptr)
+    return EK_RELU;
+  if (p.epi_mode == EPI_BWD && p.mask != nullptr && p.epi.act == ACT_RELU) return EK_BWD_MASK;
+  return EK_ANY;
+}
+
+// the MLP's three GEMM layouts on the 64-deep ring, each with its stage's specialised epilogue:
+// forward X·W (K-contiguous x N-contiguous), dX = dZ·Wᵀ (both K-contiguous), dW = Xᵀ·dZ (both
+// M/N-contiguous); anything else takes the generic epilogue
+template <typename OutT, typename AuxT, int VAR>
+hipError_t launch_bk64_256(const GemmArgs& p, hipStream_t s) {
+  if constexpr (std::is_same<OutT, uint16_t>::value) {
+    const int ek = epi_kind(p);
+    if (p.a_kc && !p.b_kc && ek == EK_RELU) return launch_cfg<256, 256, 2, 4, true, false, OutT, AuxT, VAR, EK_RELU>(p, s);
+    if (p.a_kc && p.b_kc && ek == EK_BWD_MASK)
+      return launch_cfg<256, 256, 2, 4, true, true, OutT, AuxT, VAR, EK_BWD_MASK>(p, s);
+    if (!p.a_kc && !p.b_kc && ek == EK_STORE) return launch_cfg<256, 256, 2, 4, false, false, OutT, AuxT, VAR, EK_STORE>(p, s);
+  }
+  return launch_layout<256, 256, 2, 4, OutT, AuxT, VAR>(p, s);
+}
+
 template <typename OutT, typename AuxT>
 hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   auto tiles = [&](int bm, int bn) { return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
@@ -1071,7 +1102,7 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     return e ? atoi(e) : 0;
   }();
   if (p.split_k > 1) {  // slabs sized for 256x256
-    if (bk64) return launch_layout<256, 256, 2, 4, OutT, AuxT, 30>(p, s);
+    if (bk64) return launch_bk64_256<OutT, AuxT, 30>(p, s);
     if (buf) return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
     return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
   }
@@ -1084,7 +1115,7 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   }
   // buffer-addressed LDS-DMA (VAR 6; +2..12% on the step's shapes, tools/gemm_lab)
   if (tiles(256, 256) >= kFill) {
-    if (bk64) return launch_layout<256, 256, 2, 4, OutT, AuxT, 30>(p, s);
+    if (bk64) return launch_bk64_256<OutT, AuxT, 30>(p, s);
     return buf ? launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s) : launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
   }
   if (!prefer_128(p) && tiles(256, 128) >= kFill) {
@@ -1096,8 +1127,10 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
 
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  if (!p.a_kc && !p.b_kc)  // e4m3 x e5m2 weight gradient (fp8_eligible: full 256-tiles, buffer-addressable)
-    return launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14>(p, s);
+  if (!p.a_kc && !p.b_kc)  // e4m3 x e5m2 weight gradient (fp8_eligible: full 256-tiles, buffer-addressable,
+                          // plain store)
+    return launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14, EK_STORE>(p, s);
+  const int ek = epi_kind(p);
   // PZ_GEMM_F8BUF=1: buffer-addressed staging DMA (VAR 10 / 11), A/B
   static const bool f8buf = [] {
     const char* e = getenv("PZ_GEMM_F8BUF");
@@ -1117,14 +1150,21 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   if (bk64)
     return p.a_fmt == 1 ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 13>(p, s)
                         : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 12>(p, s);
+  const bool big = tiles >= 240 || p.split_k > 1;
   if (p.a_fmt == 1) {  // e5m2 x e4m3 (backward dX)
-    if (tiles >= 240 || p.split_k > 1)
+    if (!buf && ek == EK_BWD_MASK)
+      return big ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9, EK_BWD_MASK>(p, s)
+                 : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 9, EK_BWD_MASK>(p, s);
+    if (big)
       return buf ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 11>(p, s)
                  : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>(p, s);
     return buf ? launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 11>(p, s)
                : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 9>(p, s);
   }
-  if (tiles >= 240 || p.split_k > 1)
+  if (!buf && ek == EK_RELU)
+    return big ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8, EK_RELU>(p, s)
+               : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, EK_RELU>(p, s);
+  if (big)
     return buf ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 10>(p, s)
                : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
   return buf ? launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 10>(p, s)

@@ -56,39 +56,29 @@ static double med(std::vector<double> v) {
 int main(int argc, char** argv) {
   const int B = 8192;
   using F = LaunchFn;
+  // the library's dispatch (gemm_mfma.hip: launch_bk64_256 / launch_fp8): each stage's GEMM with its
+  // specialised epilogue (EK_*); *_gen = the same GEMM on the generic epilogue (A/B)
+  constexpr int R = EK_RELU, S = EK_STORE, M = EK_BWD_MASK, G = EK_ANY;
   std::vector<Case> cases = {
-      {"fwd_L1_store", B, 4096, 1024, true, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L1", B, 4096, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L2", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"dX_L3_store", B, 4096, 1024, true, true, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
-      {"dX_L3", B, 4096, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
-      {"dX_L2", B, 4096, 4096, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
-      {"fwd_L3", B, 1024, 4096, true, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"dW_L3", 4096, 1024, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
-      {"dW_L1", 1024, 4096, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
-      {"dW_L2", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30>},
-      // A/B: the split-K slabs published with plain stores + release / acquire fences (VAR 32)
-      {"fwd_L3_rel", B, 1024, 4096, true, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 32>},
-      {"dW_L3_rel", 4096, 1024, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 32>},
-      // epilogue breakdown on fwd_L1: 4 = bias + ReLU + bitmask (no dropout), 5 = bias + ReLU +
-      // dropout (no bitmask), 6 = drop-ReLU-drop without the bitmask
-      {"fwd_L1_nodrop", B, 4096, 1024, true, false, false, 4, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L1_nomask", B, 4096, 1024, true, false, false, 5, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L1_drd", B, 4096, 1024, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L1_relu", B, 4096, 1024, true, false, false, 7, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L1_bias", B, 4096, 1024, true, false, false, 8, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L1_fwd0", B, 4096, 1024, true, false, false, 9, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
-      {"fwd_L1_drd_nm", B, 4096, 1024, true, false, false, 6, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+      {"fwd_L1", B, 4096, 1024, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwd_L1_gen", B, 4096, 1024, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, G>},
+      {"fwd_L2", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwd_L3", B, 1024, 4096, true, false, false, 11, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"dX_L3", B, 4096, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30, M>},
+      {"dX_L3_gen", B, 4096, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30, G>},
+      {"dX_L2", B, 4096, 4096, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30, M>},
+      {"dW_L3", 4096, 1024, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, S>},
+      {"dW_L1", 1024, 4096, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, S>},
+      {"dW_L2", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, S>},
+      {"dW_L2_gen", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, G>},
       // the fp8 policy's GEMMs (mlp8192 [1024, 8192, 1024], batch 8192); operand bytes are
       // arbitrary (timing only)
-      {"f8_fwd_L1_st", B, 8192, 1024, true, true, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>, 1},
-      {"f8_fwd_L1", B, 8192, 1024, true, true, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>, 1},
-      {"f8_fwd_L1_b64", B, 8192, 1024, true, true, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 12>, 1},
-      {"f8_fwd_L2", B, 1024, 8192, true, true, false, 0, 1, (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>, 1},
-      {"f8_dX_L2", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>, 2},
-      {"f8_dX_L2_b64", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 13>, 2},
-      {"f8_dW_L2", 8192, 1024, B, false, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14>, 3},
-      {"f8_dW_L1", 1024, 8192, B, false, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14>, 3},
+      {"f8_fwd_L1", B, 8192, 1024, true, true, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8, R>, 1},
+      {"f8_fwd_L1_gen", B, 8192, 1024, true, true, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8, G>, 1},
+      {"f8_fwd_L2", B, 1024, 8192, true, true, false, 11, 1, (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, R>, 1},
+      {"f8_dX_L2", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9, M>, 2},
+      {"f8_dX_L2_gen", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9, G>, 2},
+      {"f8_dW_L2", 8192, 1024, B, false, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14, S>, 3},
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -147,6 +137,8 @@ int main(int argc, char** argv) {
       p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; e.drop_post = 1;
     } else if (c.mode == 6) {
       p.epi_mode = EPI_FWD; p.bias = bias; e.act = ACT_RELU; e.drop_pre = 1; e.drop_post = 1;
+    } else if (c.mode == 11) {  // logits stage: bias + dropout of the linear output, no activation
+      p.epi_mode = EPI_FWD; p.bias = bias; e.drop_pre = 1;
     } else if (c.mode == 7) {
       p.epi_mode = EPI_FWD; e.act = ACT_RELU;
     } else if (c.mode == 8) {
@@ -158,7 +150,7 @@ int main(int argc, char** argv) {
       p.colsum = colsum;
     }
     p.epi = e;
-    const int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8> ? 128 : 256;
+    const int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, R> ? 128 : 256;
     const int tiles = ((c.M + bm - 1) / bm) * ((c.N + bm - 1) / bm);
     const int nwg = tiles * c.split;
     p.split_k = c.split;
