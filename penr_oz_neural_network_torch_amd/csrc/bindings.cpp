@@ -199,12 +199,28 @@ const float* f32_scalar_ptr(const optional<Tensor>& t, const char* what) {
   return t->data_ptr<float>();
 }
 
+// a folded fp8 scale update (pz_kernels.h ScaleUpd) riding on another launch
+pz::ScaleUpd scale_upd(const optional<Tensor>& amax, const optional<Tensor>& qs, double headroom, double maxval) {
+  pz::ScaleUpd su{};
+  if (!amax.has_value() || !amax->defined()) return su;
+  TORCH_CHECK(qs.has_value() && qs->defined(), "scale update: su_amax needs su_qs");
+  TORCH_CHECK(amax->scalar_type() == at::kFloat && qs->scalar_type() == at::kFloat && amax->is_contiguous() &&
+                  qs->is_contiguous() && qs->numel() >= 2 * amax->numel() && amax->numel() <= 64,
+              "scale update: fp32 amax[n <= 64], qs[2n]");
+  su.amax = amax->data_ptr<float>();
+  su.qs = qs->data_ptr<float>();
+  su.n = static_cast<int>(amax->numel());
+  su.headroom = static_cast<float>(headroom);
+  su.maxval = static_cast<float>(maxval);
+  return su;
+}
+
 void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, const optional<Tensor>& bias,
              const optional<Tensor>& aux, const optional<Tensor>& colsum, int64_t epi_mode, at::IntArrayRef epi_i,
              at::ArrayRef<double> epi_f, double alpha, bool accumulate, int64_t M, int64_t N, int64_t K, int64_t idx_ld,
              bool force_generic, const optional<Tensor>& mask, const optional<Tensor>& scale_a,
              const optional<Tensor>& scale_b, const optional<Tensor>& out8, const optional<Tensor>& out8_qscale,
-             const optional<Tensor>& amax, int64_t max_split) {
+             const optional<Tensor>& amax, int64_t flags) {
   check_dev(A, "A");
   auto p = gemm_args(A, a_kc, B, b_kc, C, bias, aux, colsum, epi_mode, epi_i, epi_f, alpha, accumulate, M, N, K, idx_ld,
                      force_generic, mask);
@@ -228,10 +244,18 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
   }
   TORCH_CHECK((p.out8 == nullptr && p.in_dtype != pz::DT_FP8) || pz::gemm_path(p) == 1,
               "pz::gemm: fp8 operands / outputs need an MFMA-eligible shape");
+  // flags bit 1: C is not stored — only the epilogue's side outputs (fp8 copy, ReLU bitmask, bias-
+  // gradient column sums) are; the MFMA path's bf16 epilogue implements it
+  if (flags & 2) {
+    TORCH_CHECK(p.out_dtype == pz::DT_BF16 && pz::gemm_path(p) == 1 && (p.out8 != nullptr || p.mask != nullptr ||
+                                                                         p.colsum != nullptr),
+                "pz::gemm: store_c=False needs the MFMA path with a bf16 C and a side output");
+    p.C = nullptr;
+  }
   at::Tensor ws;  // split-K slabs: from the caching allocator, stream-ordered reuse is safe
-  // max_split == 1: no split-K (a GEMM that runs concurrently with others: its tile count need
-  // not fill the CUs on its own, and it skips the in-launch reduction)
-  const int64_t ws_floats = max_split == 1 ? 0 : pz::gemm_split_ws_floats(p);
+  // flags bit 0: no split-K (a GEMM that runs concurrently with others: its tile count need not
+  // fill the CUs on its own, and it skips the in-launch reduction)
+  const int64_t ws_floats = (flags & 1) ? 0 : pz::gemm_split_ws_floats(p);
   if (ws_floats > 0) {
     ws = at::empty({ws_floats}, A.options().dtype(at::kFloat));
     p.split_k = pz::gemm_split(p);
@@ -340,7 +364,10 @@ void stage_bwd_op(const Tensor& g, const Tensor& y, const Tensor& dx, at::IntArr
 
 void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid, const optional<Tensor>& loss,
                   double loss_scale, const optional<Tensor>& dh, double grad_scale, const optional<Tensor>& colsum,
-                  const optional<Tensor>& probs, at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld) {
+                  const optional<Tensor>& probs, at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld,
+                  const optional<Tensor>& out8, const optional<Tensor>& out8_qscale, const optional<Tensor>& amax,
+                  bool store_dh, const optional<Tensor>& su_amax, const optional<Tensor>& su_qs, double su_headroom,
+                  double su_maxval) {
   check_dev(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "pz::xent_head: 2-D logits");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "pz::xent_head: int64 labels");
@@ -367,6 +394,23 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
   }
   a.epi = make_epi(ei, ef);
   a.idx_ld = idx_ld > 0 ? idx_ld : a.cols;
+  if (out8.has_value() && out8->defined()) {
+    TORCH_CHECK(out8->scalar_type() == at::kFloat8_e5m2 && out8->dim() == 2 && out8->stride(1) == 1 &&
+                    out8->size(0) >= a.rows && out8->size(1) >= a.cols,
+                "pz::xent_head: out8 must be float8_e5m2 [rows, cols]");
+    a.out8 = static_cast<uint8_t*>(out8->data_ptr());
+    a.ld_out8 = out8->stride(0);
+    a.out8_qscale = f32_scalar_ptr(out8_qscale, "out8_qscale");
+    TORCH_CHECK(a.out8_qscale != nullptr, "pz::xent_head: out8 needs out8_qscale");
+    if (amax.has_value() && amax->defined()) {
+      TORCH_CHECK(amax->scalar_type() == at::kFloat, "pz::xent_head: amax must be fp32");
+      a.amax = amax->data_ptr<float>();
+    }
+  }
+  a.skip_dh = store_dh ? 0 : 1;
+  a.su = scale_upd(su_amax, su_qs, su_headroom, su_maxval);
+  TORCH_CHECK((a.out8 == nullptr && !a.skip_dh) || pz::xent_head_out8_ok(a),
+              "pz::xent_head: out8 / store_dh=False need the bf16 fast path (bf16, cols % 8 == 0, <= 2048, aligned)");
   PZ_HIP_CHECK(pz::xent_head(a, cur_stream(logits)));
 }
 
@@ -425,7 +469,9 @@ void colsum_op(const Tensor& x, const Tensor& out) {
 void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t seed_lo, int64_t seed_hi,
                     const Tensor& out, int64_t rows_valid, const optional<Tensor>& labels_in,
                     const optional<Tensor>& labels_out, const optional<Tensor>& picked,
-                    const optional<Tensor>& epoch, const optional<Tensor>& data8, const optional<Tensor>& out8) {
+                    const optional<Tensor>& epoch, const optional<Tensor>& data8, const optional<Tensor>& out8,
+                    const optional<Tensor>& su_amax, const optional<Tensor>& su_qs, double su_headroom,
+                    double su_maxval) {
   check_dev(data, "data");
   TORCH_CHECK(data.dim() == 2 && out.dim() == 2 && data.stride(1) == 1 && out.stride(1) == 1, "pz::gather_rows: 2-D");
   TORCH_CHECK(out.size(1) == data.size(1), "pz::gather_rows: width mismatch");
@@ -460,6 +506,8 @@ void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t
     a.out8 = static_cast<uint8_t*>(o8.data_ptr());
     a.ld_out8 = o8.stride(0);
   }
+  a.su = scale_upd(su_amax, su_qs, su_headroom, su_maxval);
+  TORCH_CHECK(a.su.n == 0 || a.rows > 0, "pz::gather_rows: a folded scale update needs a launch");
   PZ_HIP_CHECK(pz::gather_rows(a, cur_stream(data)));
 }
 
@@ -704,7 +752,8 @@ void quant_transpose_op(const Tensor& w, const Tensor& out, const Tensor& qs, co
                                    fused ? amax_clear->data_ptr<float>() : nullptr, cur_stream(w)));
 }
 
-void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, const optional<Tensor>& amax) {
+void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, const optional<Tensor>& amax,
+                      const optional<Tensor>& amax_in, const optional<Tensor>& amax_clear) {
   check_dev(x, "x");
   const bool e5m2 = out.scalar_type() == at::kFloat8_e5m2;
   TORCH_CHECK(x.dim() == 2 && x.stride(1) == 1 && out.dim() == 2 && out.stride(1) == 1 &&
@@ -714,7 +763,8 @@ void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, cons
   PZ_HIP_CHECK(pz::quantize_rows(x.data_ptr(), dt_of(x), x.stride(0), static_cast<int>(x.size(0)),
                                  static_cast<int>(x.size(1)), static_cast<uint8_t*>(out.data_ptr()), out.stride(0),
                                  qs.data_ptr<float>(), amax.has_value() ? amax->data_ptr<float>() : nullptr,
-                                 cur_stream(x), e5m2 ? 1 : 0));
+                                 cur_stream(x), e5m2 ? 1 : 0, f32_scalar_ptr(amax_in, "amax_in"),
+                                 amax_clear.has_value() ? amax_clear->data_ptr<float>() : nullptr));
 }
 
 void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tensor& stats_prev, const Tensor& stats_cur,
@@ -828,7 +878,7 @@ TORCH_LIBRARY(pz, m) {
   m.def("gemm(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor(a!) C, Tensor? bias, Tensor? aux, Tensor(b!)? colsum, "
         "int epi_mode, int[] epi_i, float[] epi_f, float alpha, bool accumulate, int M, int N, int K, int idx_ld, "
         "bool force_generic, Tensor(c!)? mask=None, Tensor? scale_a=None, Tensor? scale_b=None, "
-        "Tensor(d!)? out8=None, Tensor? out8_qscale=None, Tensor(e!)? amax=None, int max_split=0) -> ()");
+        "Tensor(d!)? out8=None, Tensor? out8_qscale=None, Tensor(e!)? amax=None, int flags=0) -> ()");
   m.def("gemm_update(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor grad, int M, int N, int K, float alpha, "
         "Tensor(a!) params, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor(d!)? shadow, Tensor(e!)? stats, "
         "Tensor(f!)? amax, bool adam, float lr, float beta1, float beta2, float eps, float bias_c1, "
@@ -837,7 +887,9 @@ TORCH_LIBRARY(pz, m) {
   m.def("stage_fwd(Tensor x, Tensor(a!) y, int[] epi_i, float[] epi_f) -> ()");
   m.def("stage_bwd(Tensor g, Tensor y, Tensor(a!) dx, int[] epi_i, float[] epi_f) -> ()");
   m.def("xent_head(Tensor logits, Tensor labels, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "
-        "float grad_scale, Tensor(c!)? colsum, Tensor(d!)? probs, int[] epi_i, float[] epi_f, int idx_ld) -> ()");
+        "float grad_scale, Tensor(c!)? colsum, Tensor(d!)? probs, int[] epi_i, float[] epi_f, int idx_ld, "
+        "Tensor(e!)? out8=None, Tensor? out8_qscale=None, Tensor(f!)? amax=None, bool store_dh=True, "
+        "Tensor(s!)? su_amax=None, Tensor(t!)? su_qs=None, float su_headroom=1.0, float su_maxval=448.0) -> ()");
   m.def("mse_head(Tensor y, Tensor target, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "
         "float grad_scale, Tensor(c!)? colsum, int[] epi_i, float[] epi_f, int idx_ld) -> ()");
   m.def("softmax_rows(Tensor x, Tensor(a!) y) -> ()");
@@ -845,7 +897,8 @@ TORCH_LIBRARY(pz, m) {
   m.def("colsum(Tensor x, Tensor(a!) out) -> ()");
   m.def("gather_rows(Tensor data, Tensor? indices, int seed_lo, int seed_hi, Tensor(a!) out, int rows_valid, "
         "Tensor? labels_in, Tensor(b!)? labels_out, Tensor(c!)? picked, Tensor? epoch=None, Tensor? data8=None, "
-        "Tensor(d!)? out8=None) -> ()");
+        "Tensor(d!)? out8=None, Tensor(s!)? su_amax=None, Tensor(t!)? su_qs=None, float su_headroom=1.0, "
+        "float su_maxval=448.0) -> ()");
   m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows, "
         "Tensor?[] grads16, int[] zero_grad, Tensor?[] amax) -> Tensor");
   m.def("optimizer_step(Tensor(a!) params, Tensor(e!) grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
@@ -870,7 +923,8 @@ TORCH_LIBRARY(pz, m) {
   m.def("amax_abs(Tensor x, Tensor(a!) amax) -> ()");
   m.def("scale_update(Tensor(a!) amax, Tensor(b!) qs, float headroom, bool reset, float maxval=448.0) -> ()");
   m.def("quant_transpose(Tensor w, Tensor(a!) out, Tensor(b!) qs, Tensor? amax=None, Tensor(c!)? amax_clear=None) -> ()");
-  m.def("quantize_rows(Tensor x, Tensor(a!) out, Tensor qs, Tensor(b!)? amax) -> ()");
+  m.def("quantize_rows(Tensor x, Tensor(a!) out, Tensor(c!) qs, Tensor(b!)? amax, Tensor? amax_in=None, "
+        "Tensor(d!)? amax_clear=None) -> ()");
   m.def("format_json_array(Tensor t, int level) -> str");
   m.def("repr_double(float x) -> str");
   m.def("scan_json_arrays(str path, str key) -> (str, Tensor, Tensor)");

@@ -90,6 +90,7 @@ template <> PZ_DEV double* head_loss<double>(void*, void* f64) { return static_c
 
 template <typename T, typename F>
 __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
+  apply_scale_update(a.su);
   a.epi = epi_resolve(a.epi);
   extern __shared__ __attribute__((aligned(16))) char cs_raw[];
   F* cs_lds = reinterpret_cast<F*>(cs_raw);  // [cols] when a.colsum (LDS column partials)
@@ -156,6 +157,7 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
 // kBf16HeadRows rows, which keeps the bias-gradient atomics at one per column per 32 rows.
 template <int NCH, int WAVES>
 __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) {
+  apply_scale_update(a.su);
   a.epi = epi_resolve(a.epi);
   extern __shared__ float cs_lds[];  // [WAVES][cols] wave partials (when colsum)
   __shared__ float red[WAVES];
@@ -189,6 +191,8 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
                        : make_uint4(0, 0, 0, 0);
   }
   float loss_acc = 0.f;
+  float amax8 = 0.f;
+  const float qs8 = a.out8 != nullptr ? *a.out8_qscale : 1.f;
 #pragma unroll
   for (int rr = 0; rr < RPW; ++rr) {
     const int row = row0 + rr;
@@ -242,8 +246,19 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
           const float zero4[4] = {0.f, 0.f, 0.f, 0.f};
           epi_bwd4(g, zero4, idx, a.epi);
           epi_bwd4(g + 4, zero4, idx + 4, a.epi);
-          *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + c0) =
-              make_uint4(pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7]));
+          const uint4 gb = make_uint4(pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7]));
+          if (!a.skip_dh) *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + c0) = gb;
+          if (a.out8 != nullptr) {  // e5m2 copy of the stored bf16 values (as quantize_rows would)
+            const uint32_t w[4] = {gb.x, gb.y, gb.z, gb.w};
+            float x[8];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              x[2 * e] = bf2f(w[e] & 0xFFFFu);
+              x[2 * e + 1] = bf2f(w[e] >> 16);
+              amax8 = fmaxf(amax8, fmaxf(fabsf(x[2 * e]), fabsf(x[2 * e + 1])));
+            }
+            *reinterpret_cast<u32x2_t*>(a.out8 + static_cast<int64_t>(row) * a.ld_out8 + c0) = to_e5m2x8(x, qs8);
+          }
 #pragma unroll
           for (int e = 0; e < 8; ++e) cs[j][e] += g[e];
         }
@@ -251,9 +266,26 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
     } else if (dh != nullptr) {
 #pragma unroll
       for (int j = 0; j < NCH; ++j)
-        if (ok[j])
-          *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + (lane + 64 * j) * 8) =
-              make_uint4(0, 0, 0, 0);
+        if (ok[j]) {
+          if (!a.skip_dh)
+            *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + (lane + 64 * j) * 8) =
+                make_uint4(0, 0, 0, 0);
+          if (a.out8 != nullptr)
+            *reinterpret_cast<u32x2_t*>(a.out8 + static_cast<int64_t>(row) * a.ld_out8 + (lane + 64 * j) * 8) =
+                u32x2_t{0u, 0u};
+        }
+    }
+  }
+  if (a.out8 != nullptr && a.amax != nullptr) {  // one atomic per block
+    __shared__ float red8[WAVES];
+    const float m = wave_max(amax8);
+    if (lane == 0) red8[wave] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t = red8[0];
+#pragma unroll
+      for (int w = 1; w < WAVES; ++w) t = fmaxf(t, red8[w]);
+      atomicMax(reinterpret_cast<unsigned int*>(a.amax), __float_as_uint(t));
     }
   }
   if (a.loss != nullptr) {
@@ -389,6 +421,7 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, A*
 // ---------------------------------------------------------------------------------------------
 template <typename Tin, typename Tout>
 __global__ void __launch_bounds__(256) gather_rows_kernel(GatherArgs a) {
+  apply_scale_update(a.su);
   if (a.epoch_ptr != nullptr) gather_seed(a.seed_lo, a.seed_hi, static_cast<uint32_t>(*a.epoch_ptr));
   const Tin* __restrict__ src = static_cast<const Tin*>(a.data);
   Tout* __restrict__ dst = static_cast<Tout*>(a.out);
@@ -423,6 +456,7 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(GatherArgs a) {
 // store) per lane-iteration; the sampled index is hashed once per row by lane 0
 template <typename Tin>
 __global__ void __launch_bounds__(256) gather_rows_vec_kernel(GatherArgs a) {
+  apply_scale_update(a.su);
   if (a.epoch_ptr != nullptr) gather_seed(a.seed_lo, a.seed_hi, static_cast<uint32_t>(*a.epoch_ptr));
   const Tin* __restrict__ src = static_cast<const Tin*>(a.data);
   uint16_t* __restrict__ dst = static_cast<uint16_t*>(a.out);
@@ -514,9 +548,19 @@ hipError_t launch_xent_bf16(const XentArgs& a, dim3 grid, size_t lds, hipStream_
 
 constexpr int kMaxLdsCols = 16384;  // 64 KiB of fp32 column partials
 
+// the bf16 fast path (the only one with the e5m2 copy / skip_dh)
+bool xent_head_out8_ok(const XentArgs& a) {
+  return a.dtype == DT_BF16 && a.cols % 8 == 0 && a.cols <= 2048 && a.ld % 8 == 0 && a.dh != nullptr &&
+         a.ld_dh % 8 == 0 && (a.probs == nullptr || a.ld_probs % 8 == 0) && a.idx_ld % 2 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.logits) & 15) == 0 && (reinterpret_cast<uintptr_t>(a.dh) & 15) == 0 &&
+         (reinterpret_cast<uintptr_t>(a.probs) & 15) == 0 && (a.out8 == nullptr || (a.ld_out8 % 8 == 0 &&
+         (reinterpret_cast<uintptr_t>(a.out8) & 7) == 0 && a.out8_qscale != nullptr));
+}
+
 hipError_t xent_head(const XentArgs& in, hipStream_t s) {
   if (in.rows <= 0) return hipSuccess;
   XentArgs a = in;
+  if ((a.out8 != nullptr || a.skip_dh) && !xent_head_out8_ok(a)) return hipErrorInvalidValue;
   void* colsum_direct = nullptr;
   const bool acc64 = a.dtype == DT_F64;
   if ((a.colsum != nullptr || a.colsum64 != nullptr) && a.cols > kMaxLdsCols / (acc64 ? 2 : 1)) {

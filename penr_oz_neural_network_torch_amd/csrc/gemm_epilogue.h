@@ -105,21 +105,26 @@ PZ_DEV void relu_dropout_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, uint32_t p
 #pragma unroll
   for (int j = 0; j < L::COLS; ++j) {
     const uint32_t pr = pr_row + static_cast<uint32_t>(L::n_off(j) / 2);
-    uint32_t keep = e.drop_all ? 0u : 0xFu;
+    // keep decisions as lane masks (compares -> SGPR pairs, ANDed on the scalar unit)
+    bool k[4] = {!e.drop_all, !e.drop_all, !e.drop_all, !e.drop_all};
     if (e.drop_pre) {
       const uint32_t a0 = mix32(pr ^ e.key_pre), a1 = mix32((pr + 1u) ^ e.key_pre);
-      keep &= ((a0 & 0xFFFFu) >= th ? 1u : 0u) | ((a0 >> 16) >= th ? 2u : 0u) | ((a1 & 0xFFFFu) >= th ? 4u : 0u) |
-              ((a1 >> 16) >= th ? 8u : 0u);
+      k[0] = k[0] && (a0 & 0xFFFFu) >= th;
+      k[1] = k[1] && (a0 >> 16) >= th;
+      k[2] = k[2] && (a1 & 0xFFFFu) >= th;
+      k[3] = k[3] && (a1 >> 16) >= th;
     }
     if (e.drop_post) {
       const uint32_t c0 = mix32(pr ^ e.key_post), c1 = mix32((pr + 1u) ^ e.key_post);
-      keep &= ((c0 & 0xFFFFu) >= th ? 1u : 0u) | ((c0 >> 16) >= th ? 2u : 0u) | ((c1 & 0xFFFFu) >= th ? 4u : 0u) |
-              ((c1 >> 16) >= th ? 8u : 0u);
+      k[0] = k[0] && (c0 & 0xFFFFu) >= th;
+      k[1] = k[1] && (c0 >> 16) >= th;
+      k[2] = k[2] && (c1 & 0xFFFFu) >= th;
+      k[3] = k[3] && (c1 >> 16) >= th;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const float x = relu ? fmaxf(v[j][r], 0.f) : v[j][r];
-      v[j][r] = ((keep >> r) & 1u) ? (x * m1) * m2 : 0.f;
+      v[j][r] = k[r] ? (x * m1) * m2 : 0.f;
     }
   }
 }
@@ -163,36 +168,6 @@ PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], u32x2_t bits, int nlane) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[j][r] = ((w >> r) & 1u) ? v[j][r] : 0.f;
   }
-}
-
-// 8 fp32 -> 8 e5m2 bytes (OCP bf8, saturating at +-57344): the backward's dZ copy
-PZ_DEV u32x2_t to_e5m2x8(const float (&x)[8], float qs) {
-  u32x2_t out;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float c[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = fminf(fmaxf(x[4 * h + q] * qs, -57344.f), 57344.f);
-    int w = __builtin_amdgcn_cvt_pk_bf8_f32(c[0], c[1], 0, false);
-    w = __builtin_amdgcn_cvt_pk_bf8_f32(c[2], c[3], w, true);
-    out[h] = static_cast<uint32_t>(w);
-  }
-  return out;
-}
-
-// 8 fp32 -> 8 e4m3 bytes (OCP, saturating at +-448)
-PZ_DEV u32x2_t to_e4m3x8(const float (&x)[8], float qs) {
-  u32x2_t out;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    float c[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) c[q] = fminf(fmaxf(x[4 * h + q] * qs, -448.f), 448.f);
-    int w = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
-    w = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w, true);
-    out[h] = static_cast<uint32_t>(w);
-  }
-  return out;
 }
 
 // Compile-time epilogue kinds. The generic epilogue (EK_ANY) carries every transform — sigmoid /
@@ -286,7 +261,8 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     for (int j = 0; j < COLS; ++j) v[j] = L::get(acc, i, j) * alpha + bias4[j];
     if constexpr (EK == EK_STORE) {
     } else if constexpr (EK == EK_RELU) {  // (dispatcher: EPI_FWD, act NONE or RELU)
-      relu_dropout_row<L>(v, e, pr_row, relu_on, rd_m1, rd_m2);
+      if (relu_on && both && !e.drop_all) dropout_relu_dropout_row<L>(v, e, pr_row);  // hidden ReLU stages
+      else relu_dropout_row<L>(v, e, pr_row, relu_on, rd_m1, rd_m2);
     } else if (!bwd) {
       if (p.epi_mode == EPI_FWD) {
         if (e.drop_pre && e.drop_post && e.act == ACT_RELU && !e.drop_all) {
@@ -343,7 +319,8 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     const bool in_range = gm < p.M && gn < p.N;
     uint32_t byte = 0;  // ReLU bitmask of this 8-column chunk: bit b = element gn+b > 0
     if (in_range) {
-      *reinterpret_cast<u32x4_t*>(Cp + static_cast<int64_t>(gm) * p.ldc + gn) = v;
+      if (Cp != nullptr)  // (fp8 policy: a bf16 output nobody reads is not written — only its copies)
+        *reinterpret_cast<u32x4_t*>(Cp + static_cast<int64_t>(gm) * p.ldc + gn) = v;
       if (!bwd && use_mask) {  // bf16 > 0: sign clear, magnitude nonzero
 #pragma unroll
         for (int q = 0; q < 4; ++q) {

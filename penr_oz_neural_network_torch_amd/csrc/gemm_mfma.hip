@@ -547,11 +547,16 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // gradients (B), BOTH M/N-contiguous ([K][M] / [K][N] bytes, K = batch rows), staged as k-row
   // images and read with the transposing ds_read_b64_tr_b8 (no transposed copies), bf16 output
   constexpr bool F8_MN = VAR == 14;
-  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11 || VAR == 12 || VAR == 13 || F8_MN;
+  // VAR 15: the fp8 forward X8 · W8 with the e4m3 weights in their natural [in, out] layout
+  // (B N-contiguous, transposing 8-bit reads) — the same copy the backward dX GEMM reads as its
+  // K-contiguous B, so one e4m3 weight copy serves both and no transposed copy is made
+  constexpr bool F8_MNB = VAR == 15;
+  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11 || VAR == 12 || VAR == 13 || F8_MN || F8_MNB;
   constexpr bool F8_BWD = VAR == 9 || VAR == 11 || VAR == 13;
   constexpr int F8_FMT_A = F8_BWD ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
   constexpr int F8_FMT_B = F8_MN ? 1 : 0;
-  static_assert(!F8 || ((F8_MN ? (!A_KC && !B_KC) : (A_KC && B_KC)) && std::is_same<OutT, uint16_t>::value),
+  static_assert(!F8 || ((F8_MN ? (!A_KC && !B_KC) : F8_MNB ? (A_KC && !B_KC) : (A_KC && B_KC)) &&
+                         std::is_same<OutT, uint16_t>::value),
                 "fp8: K-contiguous in (M/N-contiguous for VAR 14), bf16 out");
   // VAR 41 (lab A/B): bf16 on v_mfma_f32_32x32x16_bf16 (32x32 accumulator tiles, the fp8 layout)
   constexpr bool M32 = VAR == 41;
@@ -619,6 +624,15 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
         for (int j = 0; j < TN8; ++j) f.b[ks][j] = frag_kc(tb, wn * C::WTN + j * 32 + (lane & 31), (lane >> 5) + 2 * ks);
 #pragma unroll
         for (int i = 0; i < TM8; ++i) f.a[ks][i] = frag_kc(ta, wm * C::WTM + i * 32 + (lane & 31), (lane >> 5) + 2 * ks);
+      }
+    } else if constexpr (F8_MNB) {  // A: 16-B chunks of K-contiguous rows; B: transposing 8-bit reads
+      const int h2 = 2 * (lane >> 5);
+#pragma unroll
+      for (int j = 0; j < TN8; ++j) f.b[0][j] = frag_mn8<BN>(tb, wn * C::WTN + j * 32, lane);
+#pragma unroll
+      for (int i = 0; i < TM8; ++i) {
+        const int row = wm * C::WTM + i * 32 + (lane & 31);
+        f.a[0][i] = cat_frag(frag_kc<BK>(ta, row, h2), frag_kc<BK>(ta, row, h2 + 1));
       }
     } else if constexpr (F8_MN) {  // transposing 8-bit reads of the [64 k][256 B] images (KB == 1)
 #pragma unroll
@@ -693,7 +707,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   auto stage_b_t = [&](int kt, auto team, int tw) {
     constexpr int TEAM = decltype(team)::value;
     PZ_LDS char* base = smem + (kt % C::NS) * C::SLOT_BYTES + C::A_BYTES;
-    if constexpr (F8_MN) stage_mn8<BN, TEAM, 64>(ldb, n0, (kt0 + kt) * 64, base, tw, lane, rs_b);
+    if constexpr (F8_MN || F8_MNB) stage_mn8<BN, TEAM, 64>(ldb, n0, (kt0 + kt) * 64, base, tw, lane, rs_b);
     else if constexpr (B_KC) stage_kc<BN, TEAM, BK, BUF_B, POL, FULL_KC>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
     else stage_mn<BN, TEAM, BK, BUF_B, POL>(B, ldb, n0, p.N, (kt0 + kt) * BK, base, tw, lane, rs_b);
   };
@@ -1131,6 +1145,12 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
                           // plain store)
     return launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14, EK_STORE>(p, s);
   const int ek = epi_kind(p);
+  if (p.a_kc && !p.b_kc) {  // e4m3 X x e4m3 W[in, out] (fp8_eligible: N % 256 — B's transposed image
+                           // rows are whole 256-B tiles, swz_mn8 — buffer-addressable B; split-K
+                           // when the tiles do not fill the CUs, gemm_split)
+    if (ek == EK_RELU) return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, EK_RELU>(p, s);
+    return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15>(p, s);
+  }
   // PZ_GEMM_F8BUF=1: buffer-addressed staging DMA (VAR 10 / 11), A/B
   static const bool f8buf = [] {
     const char* e = getenv("PZ_GEMM_F8BUF");
@@ -1191,7 +1211,12 @@ bool fp8_eligible(const GemmArgs& p) {
   if (p.bias64 != nullptr || p.colsum64 != nullptr) return false;
   if (!p.a_kc && !p.b_kc) return fp8_dw_eligible(p);
   if (p.b_fmt != 0) return false;
-  if (!p.a_kc || !p.b_kc || p.accumulate) return false;
+  if (p.a_kc && !p.b_kc) {  // VAR 15: forward on the [in, out] e4m3 weights
+    if (p.a_fmt != 0 || p.epi_mode == EPI_BWD || p.accumulate || p.N % 256 != 0) return false;
+    if (static_cast<int64_t>(p.K) * p.ldb >= (int64_t(1) << 32)) return false;  // buffer-addressed B
+  } else if (!p.a_kc || p.accumulate) {
+    return false;
+  }
   if (p.M < 64 || p.N < 64 || p.K < 64 || p.K % 64 != 0) return false;
   if (p.N % 8 != 0 || p.ldc % 8 != 0 || p.lda % 16 != 0 || p.ldb % 16 != 0) return false;
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
@@ -1260,7 +1285,8 @@ int gemm_split(const GemmArgs& p) {
   static const bool forced_tile = getenv("PZ_GEMM_TILE") != nullptr;
   // fp8 skinny shapes run better as 128x128 tiles (measured: split-K 256x256 -4%); the fp8
   // weight-gradient GEMM (both operands M/N-contiguous, 256-tiles only) splits like bf16
-  const bool f8_dw = p.in_dtype == DT_FP8 && !p.a_kc && !p.b_kc;
+  // (and the N-contiguous-weight fp8 forward, VAR 15: 256x256 tiles only)
+  const bool f8_dw = p.in_dtype == DT_FP8 && !p.b_kc;
   if (mode == 0 || forced_tile || (p.in_dtype == DT_FP8 && !f8_dw) || !mfma_eligible(p)) return 1;
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   constexpr int kFill = 240;

@@ -47,6 +47,48 @@ template <> PZ_DEV float to_f<uint16_t>(uint16_t v) { return bf2f(v); }
 template <typename T> PZ_DEV T from_f(float v) { return static_cast<T>(v); }
 template <> PZ_DEV uint16_t from_f<uint16_t>(float v) { return f2bf(v); }
 
+// 8 fp32 -> 8 e5m2 bytes (OCP bf8, saturating at +-57344): the backward's dZ copy
+PZ_DEV u32x2_t to_e5m2x8(const float (&x)[8], float qs) {
+  u32x2_t out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = fminf(fmaxf(x[4 * h + q] * qs, -57344.f), 57344.f);
+    int w = __builtin_amdgcn_cvt_pk_bf8_f32(c[0], c[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_bf8_f32(c[2], c[3], w, true);
+    out[h] = static_cast<uint32_t>(w);
+  }
+  return out;
+}
+
+// 8 fp32 -> 8 e4m3 bytes (OCP, saturating at +-448)
+PZ_DEV u32x2_t to_e4m3x8(const float (&x)[8], float qs) {
+  u32x2_t out;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float c[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) c[q] = fminf(fmaxf(x[4 * h + q] * qs, -448.f), 448.f);
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w, true);
+    out[h] = static_cast<uint32_t>(w);
+  }
+  return out;
+}
+
+// a folded scale update (pz_kernels.h ScaleUpd): call from every thread; block 0 applies it
+template <class SU>
+PZ_DEV void apply_scale_update(const SU& su) {
+  if (su.n <= 0 || blockIdx.x != 0 || blockIdx.y != 0 || static_cast<int>(threadIdx.x) >= su.n) return;
+  const int i = threadIdx.x;
+  const float a = su.amax[i];
+  const float q = a > 0.f ? su.maxval / (a * su.headroom) : 1.f;
+  su.qs[2 * i] = q;
+  su.qs[2 * i + 1] = 1.f / q;
+  su.amax[i] = 0.f;
+}
+
 // ------------------------------------------------------------------------------------------
 // counter-based dropout RNG
 // ------------------------------------------------------------------------------------------

@@ -7,6 +7,16 @@
 namespace pz {
 
 // ------------------------------------------------------------------ elementwise / heads
+// A folded fp8 delayed-scale update (the scale_update op inside another launch): block 0 turns
+// amax[i] into qs[2i] = q = maxval / (amax[i] * headroom), qs[2i+1] = 1/q and clears amax[i]
+// (i < n). Only for launches in which nothing reads qs or writes amax.
+struct ScaleUpd {
+  float* amax;
+  float* qs;
+  int n;
+  float headroom, maxval;
+};
+
 struct XentArgs {
   const void* logits;   // [rows][ld]
   int64_t ld;
@@ -26,7 +36,17 @@ struct XentArgs {
   int64_t ld_probs;
   EpiSpec epi;          // logits' dropout (drop_pre); act must be NONE
   int64_t idx_ld;
+  // fp8 policy (bf16 fast path only): e5m2 copy sat(bf16(dh) * *out8_qscale) of the gradient for
+  // the stage's fp8 dX / dW GEMMs, its running max |bf16(dh)| into *amax (delayed scaling), and
+  // skip_dh: the bf16 dh itself is not stored (nobody reads it; colsum is still reduced)
+  uint8_t* out8;
+  int64_t ld_out8;
+  const float* out8_qscale;
+  float* amax;
+  int skip_dh;
+  ScaleUpd su;  // e.g. this step's activation amax -> the next step's scales (fp8 policy)
 };
+bool xent_head_out8_ok(const XentArgs& a);
 
 struct MseArgs {
   const void* y;        // final stage output [rows][ld_y]
@@ -69,6 +89,7 @@ struct GatherArgs {
   int64_t ld_data8;
   uint8_t* out8;             // [rows][ld_out8]
   int64_t ld_out8;
+  ScaleUpd su;               // e.g. the previous step's gradient amax -> this step's e5m2 scales
 };
 
 
@@ -234,8 +255,10 @@ hipError_t scale_update(float* amax, float* qs, int n, float headroom, bool rese
 hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* out, int64_t ldo, float* qs,
                            const float* amax, float* amax_clear,
                            hipStream_t s);
-// fmt 0: e4m3 (sat 448), 1: e5m2 (sat 57344)
+// fmt 0: e4m3 (sat 448), 1: e5m2 (sat 57344). amax_in != nullptr (e4m3 only): q = 448 / *amax_in is
+// derived in-kernel and {q, 1/q} written to qs, *amax_clear reset (weights: the optimizer's amax)
 hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
-                         const float* qs, float* amax, hipStream_t s, int fmt = 0);
+                         float* qs, float* amax, hipStream_t s, int fmt = 0, const float* amax_in = nullptr,
+                         float* amax_clear = nullptr);
 
 }  // namespace pz

@@ -176,11 +176,25 @@ __global__ void __launch_bounds__(256) quantize_rows_kernel(const T* __restrict_
 // 8-B store, one 32-bit row division per 8 elements (the scalar kernel above spends a 64-bit
 // division and four 2-B loads per 4 elements: 18 us for the [8192, 1024] dX operand of mlp8192).
 // Same clamp + conversion per value as to_e4m3 / to_e5m2, so the bytes are identical.
+// amax_in != nullptr (weights, current scaling): q = 448 / *amax_in — the max the optimizer reduced
+// while writing x — derived by every block, block 0 publishes {q, 1/q} into qs and clears
+// *amax_clear (the other shadow parity's accumulator), as the transpose-quantise does
 template <typename T, bool E5M2>
 __global__ void __launch_bounds__(256) quantize_rows8_kernel(const T* __restrict__ x, int64_t ldx, int rows, int cols,
-                                                             uint8_t* __restrict__ out, int64_t ldo,
-                                                             const float* __restrict__ qs, float* amax) {
-  const float q = qs[0];
+                                                             uint8_t* __restrict__ out, int64_t ldo, float* qs,
+                                                             float* amax, const float* amax_in, float* amax_clear) {
+  float q;
+  if (amax_in != nullptr) {
+    const float am = *amax_in;
+    q = am > 0.f ? kE4m3Max / am : 1.f;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      qs[0] = q;
+      qs[1] = 1.f / q;
+      *amax_clear = 0.f;
+    }
+  } else {
+    q = qs[0];
+  }
   const float lim = E5M2 ? kE5m2Max : kE4m3Max;
   float m = 0.f;
   const uint32_t per_row = static_cast<uint32_t>(cols / 8);
@@ -265,7 +279,7 @@ hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* o
 
 template <bool E5M2>
 hipError_t quantize_rows_fmt(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
-                             const float* qs, float* amax, hipStream_t s) {
+                             float* qs, float* amax, hipStream_t s, const float* amax_in, float* amax_clear) {
   const int esz = dtype == DT_BF16 ? 2 : 4;
   const bool vec8 = (dtype == DT_BF16 || dtype == DT_F32) && cols % 8 == 0 && ldx % 8 == 0 && ldo % 8 == 0 &&
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0 &&
@@ -277,15 +291,18 @@ hipError_t quantize_rows_fmt(const void* x, int dtype, int64_t ldx, int rows, in
       const char* e = getenv("PZ_QUANT_GRID");
       return e != nullptr ? atoi(e) : 256;
     }();
-    const int g8 = grid_for(static_cast<int64_t>(rows) * (cols / 8), 256 * 4, cap > 0 ? cap : 256);
+    // (no amax output: no serialising atomics, 4 blocks per CU)
+    const int g8 = grid_for(static_cast<int64_t>(rows) * (cols / 8), 256 * 4,
+                            amax == nullptr ? 1024 : (cap > 0 ? cap : 256));
     if (dtype == DT_BF16)
       hipLaunchKernelGGL((quantize_rows8_kernel<uint16_t, E5M2>), dim3(g8), dim3(256), 0, s,
-                         static_cast<const uint16_t*>(x), ldx, rows, cols, out, ldo, qs, amax);
+                         static_cast<const uint16_t*>(x), ldx, rows, cols, out, ldo, qs, amax, amax_in, amax_clear);
     else
       hipLaunchKernelGGL((quantize_rows8_kernel<float, E5M2>), dim3(g8), dim3(256), 0, s, static_cast<const float*>(x),
-                         ldx, rows, cols, out, ldo, qs, amax);
+                         ldx, rows, cols, out, ldo, qs, amax, amax_in, amax_clear);
     return hipGetLastError();
   }
+  if (amax_in != nullptr) return hipErrorInvalidValue;  // (the derived scale: 8-wide path only)
   const int g = grid_for(static_cast<int64_t>(rows) * (cols / 4), 256 * 8, 1024);
   if (dtype == DT_BF16)
     hipLaunchKernelGGL((quantize_rows_kernel<uint16_t, E5M2>), dim3(g), dim3(256), 0, s,
@@ -298,11 +315,11 @@ hipError_t quantize_rows_fmt(const void* x, int dtype, int64_t ldx, int rows, in
 }
 
 hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
-                         const float* qs, float* amax, hipStream_t s, int fmt) {
+                         float* qs, float* amax, hipStream_t s, int fmt, const float* amax_in, float* amax_clear) {
   if (rows <= 0 || cols <= 0) return hipSuccess;
-  if (cols % 4 != 0) return hipErrorInvalidValue;
-  if (fmt == 1) return quantize_rows_fmt<true>(x, dtype, ldx, rows, cols, out, ldo, qs, amax, s);
-  return quantize_rows_fmt<false>(x, dtype, ldx, rows, cols, out, ldo, qs, amax, s);
+  if (cols % 4 != 0 || (amax_in != nullptr && (amax_clear == nullptr || fmt != 0))) return hipErrorInvalidValue;
+  if (fmt == 1) return quantize_rows_fmt<true>(x, dtype, ldx, rows, cols, out, ldo, qs, amax, s, amax_in, amax_clear);
+  return quantize_rows_fmt<false>(x, dtype, ldx, rows, cols, out, ldo, qs, amax, s, amax_in, amax_clear);
 }
 
 }  // namespace pz

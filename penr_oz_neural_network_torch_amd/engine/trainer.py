@@ -223,8 +223,16 @@ class FusedTrainer:
                 seg = next(s for s in self.store.segments if s.offset == sh_off)
                 sh.copy_(self.store.view(seg))
         self.opt.init_stats()
-        # fp8 policy: e4m3 copies [out, in] of every GEMM weight + per-tensor {q, s} records
+        # fp8 policy: ONE e4m3 copy per GEMM weight in its natural [in, out] layout — the forward
+        # reads it N-contiguous (transposing 8-bit LDS reads), the backward dX GEMM K-contiguous —
+        # + per-tensor {q, s} records. PZ_FP8_WT=1: the former [out, in] transposed forward copy
+        # (a transpose-quantise pass per update; A/B)
         self.fp8 = model.precision.name == "fp8"
+        # (the natural-layout forward GEMM stages B as whole 256-byte rows: every width % 256)
+        self._w8_nat = os.environ.get("PZ_FP8_WT", "0") != "1" and all(
+            st.seg_w.shape[1] % 256 == 0 for st in self.stages if st.kind == "gemm")
+        self.w8_kc = not self._w8_nat  # the forward operand's layout (K-contiguous = transposed copy)
+        self._fp8_bwd_env = os.environ.get("PZ_FP8_BWD", "1") != "0"
         self.w8: dict[int, torch.Tensor] = {}
         if self.fp8:
             gemms = [st for st in self.stages if st.kind == "gemm"]
@@ -247,9 +255,13 @@ class FusedTrainer:
             self.wamax2 = torch.zeros(2, len(gemms), device=self.dev)
             for k, st in enumerate(gemms):
                 st.w8_index = k
+                if self._w8_nat:  # one copy: the forward's B and (layers 2..n) the dX GEMM's B
+                    self.w8[st.seg_w.offset] = self.w8n[st.seg_w.offset] = torch.empty(
+                        st.seg_w.shape, device=self.dev, dtype=torch.float8_e4m3fn)
+                    continue
                 self.w8[st.seg_w.offset] = torch.empty(st.seg_w.shape[1], st.seg_w.shape[0], device=self.dev,
                                                        dtype=torch.float8_e4m3fn)
-                if k > 0 and os.environ.get("PZ_FP8_BWD", "1") != "0":  # dX operand of layers 2..n
+                if k > 0 and self._fp8_bwd_env:  # dX operand of layers 2..n
                     self.w8n[st.seg_w.offset] = torch.empty(st.seg_w.shape, device=self.dev,
                                                             dtype=torch.float8_e4m3fn)
             self._refresh_fp8_weights()
@@ -265,6 +277,9 @@ class FusedTrainer:
         self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
         self._g8_done: dict = {}  # stage index -> the dZ tensor whose e5m2 copy is current this step
         self._g8_epi_ready: set = set()  # stages whose epilogue-written e5m2 dZ scale is calibrated
+        self._y_dead_cache: dict = {}  # fp8 policy: which bf16 GEMM outputs go unwritten (_y_dead)
+        self._grad_su_pending = False  # fp8: a gradient scale update waits for the next step's gather
+        self._act_su = None            # fp8: this step's activation scale update (folded into the head)
         self._run_epoch = None
         # PZ_FP8_DW=0: bf16 weight-gradient GEMMs under the fp8 policy
         self._fp8_dw_on = os.environ.get("PZ_FP8_DW", "1") != "0"
@@ -467,6 +482,16 @@ class FusedTrainer:
                 continue
             k = st.w8_index
             w = self.store.view(st.seg_w)
+            if self._w8_nat:
+                w8 = self.w8[st.seg_w.offset]
+                if parity is not None:  # q from the amax the update reduced; clear the other parity's
+                    p = parity % 2
+                    ops.quantize_rows(w, w8, self.wqs[k], None, self.wamax2[p, k:k + 1], self.wamax2[1 - p, k:k + 1])
+                else:
+                    ops.amax_abs(w, self.wamax[k:k + 1])
+                    ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
+                    ops.quantize_rows(w, w8, self.wqs[k], None)
+                continue
             if parity is not None:
                 p = parity % 2
                 ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k], self.wamax2[p, k:k + 1],
@@ -536,10 +561,10 @@ class FusedTrainer:
                     self.stages[prev.index - 1].buffers.get("y8") if prev.fp8 else
                     (self.stages[prev.index - 1].buffers["y"] if prev.index > 0 else self.x_in))
                 pw = self.w8[prev.seg_w.offset] if prev.fp8 else self._w(prev)
-                if px is None or PF.gemm_path(px, True, pw, prev.fp8, prev.buffers["y"]) != "mfma":
+                if px is None or PF.gemm_path(px, True, pw, prev.fp8 and self.w8_kc, prev.buffers["y"]) != "mfma":
                     continue
                 x8 = torch.empty(prev.buffers["y"].shape, device=self.dev, dtype=torch.float8_e4m3fn)
-            if PF.gemm_path(x8, True, self.w8[st.seg_w.offset], True, st.buffers["y"]) != "mfma":
+            if PF.gemm_path(x8, True, self.w8[st.seg_w.offset], self.w8_kc, st.buffers["y"]) != "mfma":
                 continue
             st.fp8 = True
             if prev is None:
@@ -553,7 +578,7 @@ class FusedTrainer:
             # (the [in, out] e4m3 copy is single-buffered: the update of W must not run before this
             # step's dX GEMM has read it — true with the updates queued after the dX GEMMs)
             if (st.kind != "gemm" or not st.fp8 or prev is None or prev.kind != "gemm" or not prev.has_epi
-                    or st.seg_w.offset not in self.w8n or not self._after_dx):
+                    or st.seg_w.offset not in self.w8n or not self._fp8_bwd_env or not self._after_dx):
                 continue
             if st.out_width % 64 or prev.out_width % 8 or rows_b < 64:
                 continue
@@ -572,6 +597,7 @@ class FusedTrainer:
             st.g8_from_epi = True
             st.buffers["g8"] = torch.empty(st.buffers["g"].shape, device=self.dev, dtype=torch.float8_e5m2)
         self._g8_epi_ready = set()
+        self._y_dead_cache = {}
         self.data8 = None
         if self.x8 is not None:
             # first-layer input: the device-resident dataset is quantised to e4m3 ONCE with a static
@@ -787,9 +813,16 @@ class FusedTrainer:
             main.wait_event(pf[1])  # gathered by the previous step's side stream (_prefetch)
             self.prefetched_steps += 1
         else:
+            # the previous step's gradient amax -> this step's e5m2 scales rides on the gather
+            # (delayed scaling: nothing reads them before this step's backward)
+            su = (self.gamax, self.gqs, 2.0, 57344.0) if self._grad_su_pending else (None, None, 1.0, 448.0)
             ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
                             self.epoch_ctr if capture else None, self.data8,
-                            self.x8 if self.data8 is not None else None)
+                            self.x8 if self.data8 is not None else None, *su)
+            self._grad_su_pending = False
+        if self._grad_su_pending:  # (prefetched sample: no gather launch to ride on)
+            ops.scale_update(self.gamax, self.gqs, 2.0, True, 57344.0)
+            self._grad_su_pending = False
         # PZ_PREFETCH=1: the next step's sample rides on this step's side stream, beside the dW GEMM
         # of the first layer, instead of opening the next step between HBM-bound updates. Off: the
         # gather starves beside a one-tile-per-CU GEMM (82 us instead of 10) and slows it (dW_L1 90
@@ -816,21 +849,25 @@ class FusedTrainer:
             x = self._forward_stage(st, x, batch, dropout, keys, rec)
             prev = st
         last = prev
-        if self.fp8 and not record:  # this step's activation amax -> next step's scales
-            ops.scale_update(self.aamax, self.aqs, 1.25, True)
+        # this step's activation amax -> next step's scales: folded into the softmax head's launch
+        # (nothing reads them there), else its own launch
+        self._act_su = (self.aamax, self.aqs, 1.25, 448.0) if (self.fp8 and not record) else None
 
         # ---------------- head
         if self._opt_done is not None:
             main.wait_event(self._opt_done)
             self._opt_done = None
         self._early_done = None
+        self._g8_done = {}  # this step's e5m2 dZ copies are produced anew (the head's included)
         self._phase("pz.head")
         g_pre = self._head(last, x, batch, dropout, keys, rec)
+        if self._act_su is not None:
+            ops.scale_update(self._act_su[0], self._act_su[1], self._act_su[2], True)
+            self._act_su = None
 
         # ---------------- backward
         self._phase("pz.backward")
         handles = []
-        self._g8_done = {}  # this step's e5m2 dZ copies are produced anew
         g = last.buffers["g"]
         for si in range(len(self.stages) - 1, -1, -1):
             st = self.stages[si]
@@ -838,8 +875,9 @@ class FusedTrainer:
             x_in = before.buffers["y"] if before is not None else self.x_in
             g, g_pre = self._backward_stage(st, before, x_in, g, g_pre, batch, dropout, keys, rec, handles)
         if self.fp8 and any(getattr(st, "fp8_bwd", False) for st in self.stages):
-            # this step's gradient amax -> next step's e5m2 scales (delayed scaling)
-            torch.ops.pz.scale_update(self.gamax, self.gqs, 2.0, True, 57344.0)
+            # this step's gradient amax -> next step's e5m2 scales (delayed scaling): applied by the
+            # next step's first launch (the sample gather)
+            self._grad_su_pending = True
             self._g8_calibrated = True
 
         # ---------------- reduce + update
@@ -946,13 +984,15 @@ class FusedTrainer:
                     i = st.index
                     xa, sa = (self.x8, self.xqs[1:2]) if i == 0 else \
                         (self.stages[i - 1].buffers["y8"], self.aqs[i - 1, 1:2])
-                    wa, wkc = self.w8[st.seg_w.offset], True
+                    wa, wkc = self.w8[st.seg_w.offset], self.w8_kc
                     kw.update(scale_a=sa, scale_b=self.wqs[st.w8_index, 1:2])
                 else:
                     xa, wa, wkc = x, self._w(st), False
                 if "y8" in st.buffers:  # the next stage consumes an e4m3 copy (delayed scaling)
                     kw.update(out8=st.buffers["y8"], out8_qscale=self.aqs[st.index, 0:1],
                               amax=self.aamax[st.index:st.index + 1])
+                    if self._y_dead(st):
+                        kw["store_c"] = False
                 PF.gemm(xa, True, wa, wkc, y, bias=bias, mode=PF.EPI_FWD, epi=(ei, ef),
                         mask=st.buffers.get("mask"), **kw)
             else:
@@ -1015,8 +1055,20 @@ class FusedTrainer:
         if self.head == "softmax":
             probs = self._scratch(("probs",), y) if rec is not None else None
             gb = self._gbatch  # loss and gradient of the GLOBAL mean (this rank's share of it)
+            kw8 = {}
+            if fuse and self._head_g8_ok(last, y, g):
+                # fp8 policy: the head writes dZ's e5m2 copy itself (no quantisation pass), and
+                # not the bf16 dZ when the stage's dX and dW GEMMs both take the copy
+                k = last.index
+                kw8 = dict(out8=last.buffers["g8"], out8_qscale=self.gqs[k, 0:1], amax=self.gamax[k:k + 1],
+                           store_dh=not self._fp8_dw_ready_cached(last))
+                self._g8_done[k] = g
+            if self._act_su is not None:
+                kw8.update(su_amax=self._act_su[0], su_qs=self._act_su[1], su_headroom=self._act_su[2],
+                           su_maxval=self._act_su[3])
+                self._act_su = None
             ops.xent_head(y, self.lab, batch, self.loss_slot, 1.0 / gb, g, 1.0 / gb,
-                          bias_grad if fuse else None, probs, ei, ef, 0)
+                          bias_grad if fuse else None, probs, ei, ef, 0, **kw8)
             if rec is not None:
                 rec[len(n) - 1] = probs[:batch]
                 rec[("grad", len(n) - 2)] = g[:batch]
@@ -1127,6 +1179,46 @@ class FusedTrainer:
         self._g8_done[st.index] = g
         return g8
 
+    def _head_g8_ok(self, last: Stage, y, g) -> bool:
+        """The softmax head can write the last stage's e5m2 dZ (fp8 dX stage, delayed scale
+        calibrated, the head kernel's bf16 fast path)."""
+        if not (self.fp8 and getattr(last, "fp8_bwd", False) and self._g8_calibrated and "g8" in last.buffers):
+            return False
+        key = ("head", last.index)
+        if key not in self._y_dead_cache:
+            cols = y.shape[1]
+            self._y_dead_cache[key] = (y.dtype == torch.bfloat16 and g.dtype == torch.bfloat16 and cols % 8 == 0
+                                       and cols <= 2048 and y.stride(0) % 8 == 0 and g.stride(0) % 8 == 0)
+        return self._y_dead_cache[key]
+
+    def _fp8_dw_ready(self, st: Stage) -> bool:
+        """This step's dW GEMM of ``st`` will run on fp8 operands (``_fp8_dw`` returns them)."""
+        if not (self.fp8 and st.fp8 and self._fp8_dw_on and st.kind == "gemm"):
+            return False
+        if getattr(st, "g8_from_epi", False):
+            if st.index not in self._g8_epi_ready:
+                return False
+        elif not getattr(st, "fp8_bwd", False):
+            return False
+        x8 = self.x8 if st.index == 0 else self.stages[st.index - 1].buffers.get("y8")
+        w_grad = self._w_grad(st.seg_w)
+        return (x8 is not None and w_grad.dtype == torch.bfloat16
+                and PF.gemm_path(x8, False, st.buffers["g8"], False, w_grad) == "mfma")
+
+    def _fp8_dw_ready_cached(self, st: Stage) -> bool:
+        key = ("dw", st.index, st.index in self._g8_epi_ready)
+        if key not in self._y_dead_cache:
+            self._y_dead_cache[key] = self._fp8_dw_ready(st)
+        return self._y_dead_cache[key]
+
+    def _y_dead(self, st: Stage) -> bool:
+        """fp8 policy: nobody reads the bf16 output of ``st`` this step — the next stage's forward
+        and weight-gradient GEMMs take its e4m3 copy, the next dX GEMM's ReLU derivative its
+        bitmask — so the forward epilogue writes only those (mlp8192: 128 MB of writes a step)."""
+        if "y8" not in st.buffers or st.buffers.get("mask") is None or st.index + 1 >= len(self.stages):
+            return False
+        return self._fp8_dw_ready_cached(self.stages[st.index + 1])
+
     def _fp8_dw(self, st: Stage, g, w_grad):
         """fp8 weight-gradient operands (BASELINE config 5): the stage input's e4m3 copy (written by
         the previous GEMM's epilogue, or the gathered e4m3 dataset rows) and dZ's e5m2 copy, both
@@ -1180,6 +1272,10 @@ class FusedTrainer:
             kw8 = {}
             if getattr(before, "g8_from_epi", False) and b in self._g8_epi_ready:
                 kw8 = dict(out8=before.buffers["g8"], out8_qscale=self.gqs[b, 0:1], amax=self.gamax[b:b + 1])
+                if b == 0 and self._fp8_dw_ready_cached(before):
+                    # the first stage has no dX GEMM and its dW reads the e5m2 copy: the bf16 dZ
+                    # is not written (mlp8192: 128 MB a step)
+                    kw8["store_c"] = False
             if getattr(st, "fp8_bwd", False):  # e5m2 dZ x e4m3 W on the scaled fp8 MFMA
                 k, g8 = st.index, self._quantize_g8(st, g)
                 PF.gemm(g8, True, self.w8n[st.seg_w.offset], True, dx,

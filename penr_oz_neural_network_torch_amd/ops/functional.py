@@ -99,7 +99,8 @@ def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Ten
          epi: tuple[list[int], list[float]] = NO_EPI, alpha: float = 1.0, accumulate: bool = False,
          idx_ld: int = 0, force_generic: bool = False, mask: Tensor | None = None,
          scale_a: Tensor | None = None, scale_b: Tensor | None = None, out8: Tensor | None = None,
-         out8_qscale: Tensor | None = None, amax: Tensor | None = None, max_split: int = 0) -> Tensor:
+         out8_qscale: Tensor | None = None, amax: Tensor | None = None, no_split: bool = False,
+         store_c: bool = True) -> Tensor:
     """``out[M,N] = op(a) @ op(b)`` with a fused epilogue.
 
     ``a_kc``: ``a`` is stored ``[M,K]`` (else ``[K,M]``); ``b_kc``: ``b`` is stored ``[N,K]`` (else ``[K,N]``).
@@ -107,13 +108,16 @@ def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Ten
     ``y > 0`` of the final output; EPI_BWD with a ReLU stage reads it instead of ``aux``.
     fp8: ``a``/``b`` may be ``float8_e4m3fn`` (both K-contiguous); products are multiplied by the
     device scalars ``scale_a * scale_b``. ``out8`` (e4m3, EPI_FWD) receives ``sat(y * out8_qscale)``
-    and ``amax`` (fp32 scalar, caller-zeroed) the running ``max |y|``. ``max_split=1`` turns the
+    and ``amax`` (fp32 scalar, caller-zeroed) the running ``max |y|``. ``no_split`` turns the
     split-K plan of a skinny shape off (a GEMM running beside others on its own stream).
+    ``store_c=False`` (MFMA path, bf16 ``out``): only the side outputs — ``out8``, ``mask``,
+    ``colsum`` — are written, ``out`` is not (the fp8 policy's bf16 tensors nobody reads).
     """
     M, N = out.shape
     K = a.shape[1] if a_kc else a.shape[0]
     _ops().gemm(a, a_kc, b, b_kc, out, bias, aux, colsum, mode, epi[0], epi[1], alpha, accumulate,
-                M, N, K, idx_ld, force_generic, mask, scale_a, scale_b, out8, out8_qscale, amax, max_split)
+                M, N, K, idx_ld, force_generic, mask, scale_a, scale_b, out8, out8_qscale, amax,
+                (1 if no_split else 0) | (0 if store_c else 2))
     return out
 
 

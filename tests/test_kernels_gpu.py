@@ -243,6 +243,73 @@ def test_gemm_fp8_forward(native_lib, M, N, K):
     assert (y8.view(torch.uint8) != exp8.view(torch.uint8)).float().mean().item() < 1e-4
     bits = torch.stack([(mask[:, :N // 8].int() >> b) & 1 for b in range(8)], dim=2).reshape(M, N)
     assert torch.equal(bits.bool(), yf > 0)
+    # store_c=False (the fp8 policy's unread bf16 outputs): C untouched, side outputs identical
+    y_skip = torch.full_like(y, 7.0)
+    y8_skip, mask_skip, amax_skip = torch.empty_like(y8), torch.empty_like(mask), torch.zeros(1, device=DEV)
+    PF.gemm(x8, True, w8, True, y_skip, bias=bias, mode=PF.EPI_FWD, epi=epi, scale_a=sa, scale_b=sb, out8=y8_skip,
+            out8_qscale=qs, amax=amax_skip, mask=mask_skip, store_c=False)
+    assert (y_skip == 7.0).all()
+    assert torch.equal(y8_skip.view(torch.uint8), y8.view(torch.uint8)) and torch.equal(mask_skip, mask)
+    assert amax_skip.item() == amax.item()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 256, 128), (4096 + 64, 1024, 512), (8192, 8192, 1024), (8192, 1024, 8192)])
+def test_gemm_fp8_forward_natural_weights(native_lib, M, N, K):
+    """fp8 forward on the [in, out] e4m3 weights (B N-contiguous, transposing 8-bit LDS reads;
+    256x256 tiles, ragged M, split-K on the skinny shape) with the fused stage epilogue == the same
+    GEMM on the transposed [out, in] copy."""
+    f8 = torch.float8_e4m3fn
+    p, seed = 0.1, (3, 4)
+    x8 = (torch.randn(M, K, device=DEV) * 4).to(f8)
+    w8n = (torch.randn(K, N, device=DEV) * 2).to(f8)            # [in, out]
+    w8t = w8n.t().contiguous()                                   # [out, in]
+    sa, sb = torch.tensor([0.125], device=DEV), torch.tensor([1.0 / 64], device=DEV)
+    bias = torch.randn(N, device=DEV)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=p, seed=seed)
+    outs = []
+    for w, kc in ((w8n, False), (w8t, True)):
+        y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        y8 = torch.empty(M, N, device=DEV, dtype=f8)
+        mask = torch.empty(M, PF.relu_mask_cols(N), device=DEV, dtype=torch.uint8)
+        amax = torch.zeros(1, device=DEV)
+        assert PF.gemm_path(x8, True, w, kc, y) == "mfma"
+        PF.gemm(x8, True, w, kc, y, bias=bias, mode=PF.EPI_FWD, epi=epi, scale_a=sa, scale_b=sb, out8=y8,
+                out8_qscale=torch.tensor([8.0], device=DEV), amax=amax, mask=mask)
+        outs.append((y, y8, mask, amax))
+    (y, y8, mask, amax), (yt, y8t, maskt, amaxt) = outs
+    h = (x8.double() @ w8n.double()) * (0.125 / 64) + bias.double()
+    m1 = torch.from_numpy(keep_mask(M * N, *seed, 1, p).reshape(M, N)).to(DEV)
+    m2 = torch.from_numpy(keep_mask(M * N, *seed, 2, p).reshape(M, N)).to(DEV)
+    ref = torch.relu(h * m1 / (1 - p)) * m2 / (1 - p)
+    assert (y.double() - ref).abs().max().item() < 0.01 * ref.abs().max().item()
+    torch.testing.assert_close(y.float(), yt.float(), rtol=2 ** -7, atol=1e-3 * ref.abs().max().item())
+    assert (y8.view(torch.uint8) != y8t.view(torch.uint8)).float().mean().item() < 1e-3
+    assert (mask != maskt).float().mean().item() < 1e-3
+    assert abs(amax.item() - amaxt.item()) <= 2 ** -7 * amaxt.item()
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 768, 1024), (8192, 8192, 1024)])
+def test_gemm_fp8_backward_store_c_false(native_lib, M, N, K):
+    """e5m2 x e4m3 dX GEMM with store_c=False: only the e5m2 dZ copy, its amax and the bias-gradient
+    column sums are written — equal to the ones of the storing launch."""
+    g8 = (torch.randn(M, K, device=DEV) * 100).to(torch.float8_e5m2)
+    w8 = (torch.randn(N, K, device=DEV) * 8).to(torch.float8_e4m3fn)
+    sa, sb = torch.tensor([1e-3], device=DEV), torch.tensor([1.0 / 16], device=DEV)
+    mask = torch.randint(0, 256, (M, PF.relu_mask_cols(N)), device=DEV, dtype=torch.uint8)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=0.2, seed=(5, 6))
+    qs = torch.tensor([4.0], device=DEV)
+    outs = []
+    for store in (True, False):
+        out = torch.full((M, N), 3.0, device=DEV, dtype=torch.bfloat16)
+        o8 = torch.empty(M, N, device=DEV, dtype=torch.float8_e5m2)
+        cs, am = torch.zeros(N, device=DEV), torch.zeros(1, device=DEV)
+        PF.gemm(g8, True, w8, True, out, colsum=cs, mode=PF.EPI_BWD, epi=epi, mask=mask, scale_a=sa, scale_b=sb,
+                out8=o8, out8_qscale=qs, amax=am, store_c=store)
+        outs.append((out, o8, cs, am))
+    (y, y8, cs, am), (y_s, y8_s, cs_s, am_s) = outs
+    assert (y_s == 3.0).all() and not (y == 3.0).all()
+    assert torch.equal(y8_s.view(torch.uint8), y8.view(torch.uint8)) and am_s.item() == am.item()
+    torch.testing.assert_close(cs_s, cs, rtol=1e-5, atol=1e-5 * cs.abs().max().item())
 
 
 def test_stage_kernels_match_torch(native_lib):
@@ -294,6 +361,37 @@ def test_xent_head_fused_dropout_colsum(native_lib):
     dref = (torch.softmax(logits.double(), 1) - F.one_hot(labels, C)) / B * m / (1 - p)
     assert (dh.double() - dref).abs().max().item() < 1e-6
     assert (colsum.double() - dref.sum(0)).abs().max().item() < 1e-5
+
+
+@pytest.mark.parametrize("B,C", [(8192, 1024), (300, 520)])
+def test_xent_head_e5m2_copy(native_lib, B, C):
+    """fp8 policy head: the bf16 kernel's e5m2 dZ copy equals quantize_rows of its bf16 dZ (same
+    bytes, same amax), rows past rows_valid are zero in both, and store_dh=False leaves dh untouched
+    while the loss and the bias-gradient column sums are unchanged."""
+    rows_valid = B - 44
+    logits = (torch.randn(B, C, device=DEV) * 3).to(torch.bfloat16)
+    labels = torch.randint(0, C, (B,), device=DEV)
+    ei, ef = PF.epi_spec(drop_pre=3, p=0.2, seed=(7, 8))
+    qs = torch.tensor([2.0 ** 20, 2.0 ** -20], device=DEV)
+    res = []
+    for store in (True, False):
+        loss, colsum, amax = torch.zeros(1, device=DEV), torch.zeros(C, device=DEV), torch.zeros(1, device=DEV)
+        dh = torch.full((B, C), 5.0, device=DEV, dtype=torch.bfloat16)
+        g8 = torch.empty(B, C, device=DEV, dtype=torch.float8_e5m2)
+        torch.ops.pz.xent_head(logits, labels, rows_valid, loss, 1.0 / rows_valid, dh, 1.0 / rows_valid, colsum, None,
+                               ei, ef, 0, g8, qs[0:1], amax, store)
+        res.append((dh, g8, loss, colsum, amax))
+    (dh, g8, loss, colsum, amax), (dh_s, g8_s, loss_s, colsum_s, amax_s) = res
+    ref8 = torch.empty_like(g8)
+    ref_amax = torch.zeros(1, device=DEV)
+    torch.ops.pz.quantize_rows(dh, ref8, qs, ref_amax)
+    assert torch.equal(g8.view(torch.uint8), ref8.view(torch.uint8)) and amax.item() == ref_amax.item()
+    assert (g8[rows_valid:].view(torch.uint8) == 0).all()
+    assert (dh_s == 5.0).all()
+    assert torch.equal(g8_s.view(torch.uint8), g8.view(torch.uint8)) and amax_s.item() == amax.item()
+    # (float atomics across blocks: equal up to summation order)
+    assert abs(loss_s.item() - loss.item()) <= 1e-6 * abs(loss.item())
+    torch.testing.assert_close(colsum_s, colsum, rtol=1e-5, atol=1e-6 * colsum.abs().max().item())
 
 
 def test_mse_and_softmax(native_lib):
@@ -471,6 +569,21 @@ def test_gemm_fp8_split_k(native_lib):
     PF.gemm(x8, True, w8, True, y, mode=PF.EPI_FWD, epi=PF.epi_spec(), scale_a=one, scale_b=one)
     ref = x8.double() @ w8.double().t()
     assert (y.double() - ref).abs().max().item() < 0.01 * ref.abs().max().item()
+
+
+def test_quantize_rows_derived_weight_scale(native_lib):
+    """Weights under the fp8 policy: q = 448 / amax (the optimizer's reduced max |w|) derived in the
+    kernel, {q, 1/q} published, the other parity's accumulator cleared, bytes == torch's cast."""
+    w = torch.randn(1024, 8192, device=DEV) * 0.02
+    amax_in = w.abs().max().reshape(1)
+    clear = torch.full((1,), 3.0, device=DEV)
+    qs = torch.zeros(2, device=DEV)
+    out = torch.empty(1024, 8192, device=DEV, dtype=torch.float8_e4m3fn)
+    torch.ops.pz.quantize_rows(w, out, qs, None, amax_in, clear)
+    q = 448.0 / amax_in.item()
+    assert abs(qs[0].item() - q) <= 1e-6 * q and abs(qs[1].item() * q - 1) < 1e-6 and clear.item() == 0.0
+    ref = (w * qs[0]).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert (out.view(torch.uint8) != ref.view(torch.uint8)).float().mean().item() < 1e-4
 
 
 @pytest.mark.parametrize("dtype,fmt,cols", [(torch.bfloat16, torch.float8_e4m3fn, 1024),
