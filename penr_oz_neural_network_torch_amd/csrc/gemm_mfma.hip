@@ -49,7 +49,13 @@ constexpr int kBK = 32;  // K depth of one ring slot (BK64 variants: two of thes
 template <int VAR> constexpr int var_bk() {
   return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31 || VAR == 32 || VAR == 12 || VAR == 13) ? 64 : 32;
 }
-template <int VAR> constexpr int var_ns() { return VAR == 5 ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4); }
+template <int VAR> constexpr int var_ns() {
+  return (VAR == 5 || VAR == 7) ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4);
+}
+// VAR 7: buffer DMA on a 3-slot 32-deep ring, for 4-wave 256x128 tiles that run TWO workgroups
+// per CU (72 KiB of LDS and <= 256 VGPRs each): one workgroup's epilogue overlaps the other's
+// main loop (the hardware interleaves the two instead of a barrier-phased ping-pong)
+template <int VAR> constexpr int var_waves_per_eu() { return VAR == 7 ? 2 : 1; }
 
 // K-contiguous slot [rows][BK]. BK 32: 64-B rows = 4 chunks; chunk XOR for conflict-free
 // ds_read_b128 under the gfx950 b128 lane grouping (row groups of 4 rows map to permutation
@@ -516,7 +522,8 @@ PZ_DEV void epilogue_opt(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR, int EK = EK_ANY>
-__global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs p) {
+__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(var_waves_per_eu<VAR>())))
+gemm_mfma_kernel(const GemmArgs p) {
   static_assert(EK == EK_ANY || std::is_same<OutT, uint16_t>::value, "specialised epilogues: bf16 output");
   PZ_STAMP(0);
   constexpr int BK = var_bk<VAR>();
@@ -683,8 +690,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_mfma_kernel(const GemmArgs 
   // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
   // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
   // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
-  constexpr bool BUF_A = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 32);
-  constexpr bool BUF_B = VAR == 6 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 32);
+  constexpr bool BUF_A = VAR == 6 || VAR == 7 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 32);
+  constexpr bool BUF_B = VAR == 6 || VAR == 7 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 32);
   constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
   // VAR 30/31: full row tiles of the K-contiguous operands (use_bk64 checks M % BM, N % BN)
   constexpr bool FULL_KC = VAR == 30 || VAR == 31 || VAR == 32 || VAR == 12 || VAR == 13;

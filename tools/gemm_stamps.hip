@@ -46,6 +46,7 @@ struct Case {
   int split;
   LaunchFn fn;
   int f8 = 0;  // 0 bf16, 1 e4m3 x e4m3 (forward), 2 e5m2 x e4m3 (backward dX), 3 e4m3 x e5m2 (dW)
+  int tile_m = 0, tile_n = 0;  // 0: 256x256 (128x128 for the small fp8 config)
 };
 
 static double med(std::vector<double> v) {
@@ -61,6 +62,16 @@ int main(int argc, char** argv) {
   constexpr int R = EK_RELU, S = EK_STORE, M = EK_BWD_MASK, G = EK_ANY;
   std::vector<Case> cases = {
       {"fwd_L1", B, 4096, 1024, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwd_L1_s0", B, 4096, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      // two co-resident 4-wave workgroups per CU on 256x128 tiles (VAR 7: 3-slot 32-deep buffer ring)
+      {"fwd_L1_s0_2wg", B, 4096, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 7, R>, 0, 256, 128},
+      {"fwd_L2_2wg", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 7, R>, 0, 256, 128},
+      {"fwd_L3_2wg", B, 1024, 4096, true, false, false, 11, 1, (F)launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 7, R>, 0, 256, 128},
+      {"dX_L3_2wg", B, 4096, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 128, 2, 2, true, true, uint16_t, uint16_t, 7, M>, 0, 256, 128},
+      {"dX_L2_2wg", B, 4096, 4096, true, true, false, 3, 1, (F)launch_cfg<256, 128, 2, 2, true, true, uint16_t, uint16_t, 7, M>, 0, 256, 128},
+      {"dW_L3_2wg", 4096, 1024, B, false, false, false, 0, 1, (F)launch_cfg<256, 128, 2, 2, false, false, uint16_t, uint16_t, 7, S>, 0, 256, 128},
+      {"dW_L1_2wg", 1024, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 128, 2, 2, false, false, uint16_t, uint16_t, 7, S>, 0, 256, 128},
+      {"dW_L2_2wg", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 128, 2, 2, false, false, uint16_t, uint16_t, 7, S>, 0, 256, 128},
       {"fwd_L1_gen", B, 4096, 1024, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, G>},
       {"fwd_L2", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
       {"fwd_L3", B, 1024, 4096, true, false, false, 11, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
@@ -150,8 +161,9 @@ int main(int argc, char** argv) {
       p.colsum = colsum;
     }
     p.epi = e;
-    const int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, R> ? 128 : 256;
-    const int tiles = ((c.M + bm - 1) / bm) * ((c.N + bm - 1) / bm);
+    int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, R> ? 128 : 256, bn = bm;
+    if (c.tile_m) bm = c.tile_m, bn = c.tile_n;
+    const int tiles = ((c.M + bm - 1) / bm) * ((c.N + bn - 1) / bn);
     const int nwg = tiles * c.split;
     p.split_k = c.split;
     float* ws = nullptr;
