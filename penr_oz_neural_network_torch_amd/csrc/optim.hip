@@ -131,7 +131,7 @@ PZ_DEV void vst(R* p, const R (&x)[Vec<R>::N]) {
 // Grid: min(total_blocks, kOptMaxResident) workgroups loop over the 4096-element work blocks, so
 // a launch that overlaps the MFMA-bound GEMMs (side stream) gets all its workgroups resident
 // beside the GEMM's instead of queueing behind the GEMM's pending ones.
-template <bool ADAM, typename R>
+template <bool ADAM, typename R, int PRE>
 PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block, bool full) {
   constexpr int VN = Vec<R>::N;
   const int seg_id = find_segment(args.block_seg, args.num_segments, block);
@@ -145,36 +145,60 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
   float am = 0.f;  // max |w_new| (fp8 weight scaling, seg.amax)
 
   if (((seg.offset | seg.numel) & 3) == 0) {
+    // the loads of PRE consecutive vectors of the thread are issued before their first store (the
+    // streams are distinct buffers, __restrict__): PRE x 4 x 16 B in flight per lane instead of one
+    // vector's worth behind each store — the update is HBM-bound
+    constexpr int UN = kPerThread / VN;
+    static_assert(UN % PRE == 0, "preload groups");
 #pragma unroll
-    for (int u = 0; u < kPerThread / VN; ++u) {
-      const int64_t li = local0 + (static_cast<int64_t>(u) * kThreads + threadIdx.x) * VN;
-      if (li >= seg.numel) break;
-      const int64_t gi = seg.offset + li;
-      R p0[VN], g[VN], m[VN] = {}, v[VN] = {}, p1[VN];
-      vld<R>(a.params + gi, p0);
+    for (int u0 = 0; u0 < UN; u0 += PRE) {
+    const R* __restrict__ P = a.params;
+    const R* __restrict__ Gr = a.grads;
+    const R* __restrict__ Mm = a.exp_avg;
+    const R* __restrict__ Vv = a.exp_avg_sq;
+    const uint16_t* __restrict__ G16 = seg.grad16;
+    R p0[PRE][VN], g[PRE][VN], m[PRE][VN], v[PRE][VN];
+    bool ok[PRE];
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) {
+      const int64_t li = local0 + (static_cast<int64_t>(u0 + u) * kThreads + threadIdx.x) * VN;
+      ok[u] = li < seg.numel;
+      const int64_t gi = seg.offset + (ok[u] ? li : 0);
+      const int64_t lc = ok[u] ? li : 0;
+#pragma unroll
+      for (int k = 0; k < VN; ++k) m[u][k] = v[u][k] = R(0);
+      if (!ok[u]) continue;
+      vld<R>(P + gi, p0[u]);
       if constexpr (VN == 4) {
-        if (seg.grad16 != nullptr) {
-          const uint2 q = *reinterpret_cast<const uint2*>(seg.grad16 + li);
-          g[0] = bf2f(q.x & 0xFFFF); g[1] = bf2f(q.x >> 16); g[2] = bf2f(q.y & 0xFFFF); g[3] = bf2f(q.y >> 16);
+        if (G16 != nullptr) {
+          const uint2 q = *reinterpret_cast<const uint2*>(G16 + lc);
+          g[u][0] = bf2f(q.x & 0xFFFF); g[u][1] = bf2f(q.x >> 16); g[u][2] = bf2f(q.y & 0xFFFF); g[u][3] = bf2f(q.y >> 16);
         } else {
-          vld<R>(a.grads + gi, g);
+          vld<R>(Gr + gi, g[u]);
         }
       } else {
-        vld<R>(a.grads + gi, g);
+        vld<R>(Gr + gi, g[u]);
       }
+      if constexpr (ADAM) {
+        vld<R>(Mm + gi, m[u]);
+        vld<R>(Vv + gi, v[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < PRE; ++u) {
+      if (!ok[u]) continue;
+      const int64_t li = local0 + (static_cast<int64_t>(u0 + u) * kThreads + threadIdx.x) * VN;
+      const int64_t gi = seg.offset + li;
       if (seg.zero_grad && seg.grad16 == nullptr) {
         const R z[VN] = {};
         vst<R>(a.grads + gi, z);
       }
-      if constexpr (ADAM) {
-        vld<R>(a.exp_avg + gi, m);
-        vld<R>(a.exp_avg_sq + gi, v);
-      }
+      R p1[VN];
 #pragma unroll
-      for (int k = 0; k < VN; ++k) p1[k] = update_one<ADAM, R>(a, p0[k], g[k], l2x2, step_size, m[k], v[k]);
+      for (int k = 0; k < VN; ++k) p1[k] = update_one<ADAM, R>(a, p0[u][k], g[u][k], l2x2, step_size, m[u][k], v[u][k]);
       if constexpr (ADAM) {
-        vst<R>(a.exp_avg + gi, m);
-        vst<R>(a.exp_avg_sq + gi, v);
+        vst<R>(a.exp_avg + gi, m[u]);
+        vst<R>(a.exp_avg_sq + gi, v[u]);
       }
       vst<R>(a.params + gi, p1);
       if constexpr (VN == 4) {
@@ -188,9 +212,10 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
       }
 #pragma unroll
       for (int k = 0; k < VN; ++k) {
-        if (stats) add_stats<R>(st, p0[k], p1[k], full);
+        if (stats) add_stats<R>(st, p0[u][k], p1[k], full);
         am = fmaxf(am, fabsf(static_cast<float>(p1[k])));
       }
+    }
     }
   } else {
 #pragma unroll
@@ -226,7 +251,7 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
   if (seg.amax != nullptr) block_amax_commit(am, seg.amax);
 }
 
-template <bool ADAM, typename R>
+template <bool ADAM, typename R, int PRE>
 __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   int epoch = -1;
   if (a.epoch_ptr != nullptr) epoch = *a.epoch_ptr;
@@ -239,7 +264,7 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   const OptView<R> view(a);
   const bool full = a.stats_every == 1 || (a.stats_every > 1 && (epoch < 0 || epoch % a.stats_every == 0));
   for (int b = blockIdx.x; b < a.total_blocks; b += gridDim.x) {
-    optimizer_block<ADAM, R>(a, view, b, full);
+    optimizer_block<ADAM, R, PRE>(a, view, b, full);
     __syncthreads();  // the block reductions reuse their LDS slots
   }
 }
@@ -327,12 +352,15 @@ hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
   }();
   const int cap = a.max_grid > 0 ? a.max_grid : max_grid;
   const int grid = cap > 0 && cap < a.total_blocks ? cap : a.total_blocks;
+  // one 16-B vector of each stream per load group (PRE = 1): measured 5.7 TB/s for the whole-model
+  // Adam update in isolation vs 5.2 with all four of a thread's vectors loaded up front (PRE = 4:
+  // more VGPRs, fewer resident waves), tools/opt_bw.py, profiles/r3_opt_preload.txt
   if (a.real == DT_F64) {
-    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, double>), dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((optimizer_kernel<false, double>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((optimizer_kernel<false, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   } else {
-    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float>), dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((optimizer_kernel<false, float>), dim3(grid), dim3(kThreads), 0, s, a);
+    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((optimizer_kernel<false, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   }
   return hipGetLastError();
 }
