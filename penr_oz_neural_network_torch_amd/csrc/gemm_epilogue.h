@@ -180,6 +180,46 @@ PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], u32x2_t bits, int nlane) {
 //   EK_RELU     EPI_FWD with act NONE / RELU: bias, dropout pre / post, ReLU bitmask, fp8 copy
 //   EK_BWD_MASK EPI_BWD through a ReLU stage from its bitmask: dropout scales, column sums, e5m2 copy
 constexpr int EK_ANY = 0, EK_STORE = 1, EK_RELU = 2, EK_BWD_MASK = 3;
+// Fixed forward stages (EPI_FWD, no colsum, not drop_all): the activation and both dropout flags
+// are compile-time, so a row is ONE straight-line pass — no per-row flag branches, no untaken hash
+// copies. EK_RELU with every transform switched off still ran ~1,400 more VALU instructions per
+// wave and tile than the plain store (its 6.3k-instruction stage-math section: 3.6k I-cache
+// misses per launch vs 0.6k; profiles/r3_epilogue_fixed_kinds.txt). The MLP's three stage
+// shapes: linear -> ReLU -> dropout (first hidden stage), linear -> dropout -> ReLU -> dropout
+// (later hidden stages), linear -> dropout (the logits).
+constexpr int EK_F_RELU_POST = 4, EK_F_RELU_PREPOST = 5, EK_F_PRE = 6;
+constexpr bool ek_fixed(int ek) { return ek >= EK_F_RELU_POST && ek <= EK_F_PRE; }
+constexpr bool ek_relu(int ek) { return ek == EK_F_RELU_POST || ek == EK_F_RELU_PREPOST; }
+constexpr bool ek_pre(int ek) { return ek == EK_F_RELU_PREPOST || ek == EK_F_PRE; }
+constexpr bool ek_post(int ek) { return ek == EK_F_RELU_POST || ek == EK_F_RELU_PREPOST; }
+
+// one row of a fixed forward stage: y = keep ? act(z) * sc : 0 with keep = pre bit & post bit and
+// sc = the product of the enabled dropouts' scales (both: act(z * m1 * s) * m2 * s with s > 0 and
+// act in {identity, ReLU} equals (m1 & m2) ? act(z) * s^2 : 0 — the EK_RELU forms bit for bit)
+template <class L, int EK>
+PZ_DEV void fixed_fwd_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, uint32_t pr_row, float sc) {
+  const uint32_t th = e.thresh16;
+#pragma unroll
+  for (int j = 0; j < L::COLS; ++j) {
+    const uint32_t pr = pr_row + static_cast<uint32_t>(L::n_off(j) / 2);
+    bool k0 = true, k1 = true, k2 = true, k3 = true;
+    if constexpr (ek_pre(EK)) {
+      const uint32_t a0 = mix32(pr ^ e.key_pre), a1 = mix32((pr + 1u) ^ e.key_pre);
+      k0 = (a0 & 0xFFFFu) >= th; k1 = (a0 >> 16) >= th; k2 = (a1 & 0xFFFFu) >= th; k3 = (a1 >> 16) >= th;
+    }
+    if constexpr (ek_post(EK)) {
+      const uint32_t c0 = mix32(pr ^ e.key_post), c1 = mix32((pr + 1u) ^ e.key_post);
+      k0 = k0 && (c0 & 0xFFFFu) >= th; k1 = k1 && (c0 >> 16) >= th;
+      k2 = k2 && (c1 & 0xFFFFu) >= th; k3 = k3 && (c1 >> 16) >= th;
+    }
+    const bool k[4] = {k0, k1, k2, k3};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float x = ek_relu(EK) ? fmaxf(v[j][r], 0.f) : v[j][r];
+      v[j][r] = k[r] ? x * sc : 0.f;
+    }
+  }
+}
 
 template <int BM, int BN, int WM, int WN, class L, bool FWD_ONLY = false, int EK = EK_ANY, class Acc>
 PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0, int n0, int wm, int wn, int lane,
@@ -238,7 +278,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 #pragma unroll
   for (int j = 0; j < COLS; ++j) {
     const int n = n0 + nl0 + L::n_off(j);
-    bias4[j] = ((EK == EK_ANY || EK == EK_RELU) && !bwd && p.bias != nullptr && n < p.N)
+    bias4[j] = ((EK == EK_ANY || EK == EK_RELU || ek_fixed(EK)) && !bwd && p.bias != nullptr && n < p.N)
                    ? *reinterpret_cast<const f32x4_t*>(p.bias + n)
                    : f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
@@ -251,6 +291,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   const bool both = e.drop_pre && e.drop_post;
   const float rd_m1 = relu_on && both ? e.scale * e.scale : (e.drop_pre ? e.scale : 1.f);
   const float rd_m2 = relu_on && both ? 1.f : (e.drop_post ? e.scale : 1.f);
+  const float fixed_sc = (ek_pre(EK) ? e.scale : 1.f) * (ek_post(EK) ? e.scale : 1.f);
   static_for<ROWS>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
     const int ml = ml0 + L::MSTEP * i;
@@ -260,6 +301,8 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 #pragma unroll
     for (int j = 0; j < COLS; ++j) v[j] = L::get(acc, i, j) * alpha + bias4[j];
     if constexpr (EK == EK_STORE) {
+    } else if constexpr (ek_fixed(EK)) {
+      fixed_fwd_row<L, EK>(v, e, pr_row, fixed_sc);
     } else if constexpr (EK == EK_RELU) {  // (dispatcher: EPI_FWD, act NONE or RELU)
       if (relu_on && both && !e.drop_all) dropout_relu_dropout_row<L>(v, e, pr_row);  // hidden ReLU stages
       else relu_dropout_row<L>(v, e, pr_row, relu_on, rd_m1, rd_m2);
@@ -311,7 +354,10 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   const bool want8 = EK != EK_STORE && p.out8 != nullptr && (bwd ? p.out8_fmt == 1 : p.out8_fmt == 0);
   const float qs = want8 ? *p.out8_qscale : 1.f;
   float amax = 0.f;
-#pragma unroll
+  // fixed forward kinds: the pass loop rolled by 4 (it indexes no accumulator; the unrolled
+  // 16-pass form is ~2.3k instructions of the kernel's I-cache footprint)
+  constexpr int kStoreUnroll = ek_fixed(EK) ? 4 : PASSES;
+#pragma unroll kStoreUnroll
   for (int s = 0; s < PASSES; ++s) {
     const int r = s * ROWS_PER_PASS + my_row;
     const int gm = m0 + r, gn = n0 + my_chunk * 8;

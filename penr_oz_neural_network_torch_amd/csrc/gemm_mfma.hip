@@ -1089,8 +1089,20 @@ int epi_kind(const GemmArgs& p) {
   if (off || p.out_dtype != DT_BF16 || p.accumulate) return EK_ANY;
   if (p.epi_mode == EPI_STORE && p.bias == nullptr && p.colsum == nullptr && p.mask == nullptr && p.out8 == nullptr)
     return EK_STORE;
-  if (p.epi_mode == EPI_FWD && (p.epi.act == ACT_NONE || p.epi.act == ACT_RELU) && p.colsum == nullptr)
+  if (p.epi_mode == EPI_FWD && (p.epi.act == ACT_NONE || p.epi.act == ACT_RELU) && p.colsum == nullptr) {
+    static const bool fixed_off = [] {  // PZ_GEMM_EKF=0: EK_RELU for every forward stage (A/B)
+      const char* e = getenv("PZ_GEMM_EKF");
+      return e != nullptr && atoi(e) == 0;
+    }();
+    const EpiSpec& e = p.epi;
+    const bool relu = e.act == ACT_RELU;
+    if (!fixed_off && !e.drop_all) {
+      if (relu && !e.drop_pre && e.drop_post) return EK_F_RELU_POST;
+      if (relu && e.drop_pre && e.drop_post) return EK_F_RELU_PREPOST;
+      if (!relu && e.drop_pre && !e.drop_post) return EK_F_PRE;
+    }
     return EK_RELU;
+  }
   if (p.epi_mode == EPI_BWD && p.mask != nullptr && p.epi.act == ACT_RELU) return EK_BWD_MASK;
   return EK_ANY;
 }
@@ -1102,7 +1114,13 @@ template <typename OutT, typename AuxT, int VAR>
 hipError_t launch_bk64_256(const GemmArgs& p, hipStream_t s) {
   if constexpr (std::is_same<OutT, uint16_t>::value) {
     const int ek = epi_kind(p);
-    if (p.a_kc && !p.b_kc && ek == EK_RELU) return launch_cfg<256, 256, 2, 4, true, false, OutT, AuxT, VAR, EK_RELU>(p, s);
+    if (p.a_kc && !p.b_kc) {
+      if (ek == EK_RELU) return launch_cfg<256, 256, 2, 4, true, false, OutT, AuxT, VAR, EK_RELU>(p, s);
+      if (ek == EK_F_RELU_POST) return launch_cfg<256, 256, 2, 4, true, false, OutT, AuxT, VAR, EK_F_RELU_POST>(p, s);
+      if (ek == EK_F_RELU_PREPOST)
+        return launch_cfg<256, 256, 2, 4, true, false, OutT, AuxT, VAR, EK_F_RELU_PREPOST>(p, s);
+      if (ek == EK_F_PRE) return launch_cfg<256, 256, 2, 4, true, false, OutT, AuxT, VAR, EK_F_PRE>(p, s);
+    }
     if (p.a_kc && p.b_kc && ek == EK_BWD_MASK)
       return launch_cfg<256, 256, 2, 4, true, true, OutT, AuxT, VAR, EK_BWD_MASK>(p, s);
     if (!p.a_kc && !p.b_kc && ek == EK_STORE) return launch_cfg<256, 256, 2, 4, false, false, OutT, AuxT, VAR, EK_STORE>(p, s);
@@ -1151,11 +1169,15 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   if (!p.a_kc && !p.b_kc)  // e4m3 x e5m2 weight gradient (fp8_eligible: full 256-tiles, buffer-addressable,
                           // plain store)
     return launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14, EK_STORE>(p, s);
-  const int ek = epi_kind(p);
+  int ek = epi_kind(p);
   if (p.a_kc && !p.b_kc) {  // e4m3 X x e4m3 W[in, out] (fp8_eligible: N % 256 — B's transposed image
                            // rows are whole 256-B tiles, swz_mn8 — buffer-addressable B; split-K
                            // when the tiles do not fill the CUs, gemm_split)
     if (ek == EK_RELU) return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, EK_RELU>(p, s);
+    if (ek == EK_F_RELU_POST) return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, EK_F_RELU_POST>(p, s);
+    if (ek == EK_F_RELU_PREPOST)
+      return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, EK_F_RELU_PREPOST>(p, s);
+    if (ek == EK_F_PRE) return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, EK_F_PRE>(p, s);
     return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15>(p, s);
   }
   // PZ_GEMM_F8BUF=1: buffer-addressed staging DMA (VAR 10 / 11), A/B
@@ -1171,6 +1193,7 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
     const char* e = getenv("PZ_GEMM_F8BK64");
     return e != nullptr && atoi(e) == 1;
   }();
+  if (ek_fixed(ek)) ek = EK_RELU;  // (VAR 8 / 10 / 12 forms: the generic ReLU-stage kind)
   const int split = p.split_k > 1 ? p.split_k : 1;
   const bool bk64 = bk64_on && buffer_ok(p) && p.M % 256 == 0 && p.N % 256 == 0 && p.K % 128 == 0 &&
                     (p.K / 128) % split == 0 && (tiles >= 240 || p.split_k > 1);

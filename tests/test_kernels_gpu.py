@@ -113,6 +113,38 @@ def test_gemm_backward_epilogue_and_colsum(native_lib, act):
     assert (out16.double() - ref).abs().max().item() < 0.03 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 128), (8192, 1024, 2048)])
+@pytest.mark.parametrize("act,pre,post", [("relu", False, True), ("relu", True, True), ("none", True, False)])
+def test_gemm_fixed_forward_kinds(native_lib, M, N, K, act, pre, post):
+    """The compile-time forward epilogues (EK_F_*: the trainer's stage-0, hidden and logits stages)
+    on shapes that take the 256x256 64-deep-ring kernel (the second one split-K) == fp64 torch with
+    the kernels' keep masks; ReLU stages also write the bitmask of y > 0."""
+    p, seed = 0.2, (21, 4)
+    x = torch.randn(M, K, device=DEV).to(torch.bfloat16)
+    w = (torch.randn(K, N, device=DEV) / 8).to(torch.bfloat16)
+    bias = torch.randn(N, device=DEV)
+    y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    relu = act == "relu"
+    mask = torch.zeros((M, PF.relu_mask_cols(N)), device=DEV, dtype=torch.uint8) if relu else None
+    epi = PF.epi_spec(act=PF.ACT_RELU if relu else PF.ACT_NONE, drop_pre=3 if pre else -1,
+                      drop_post=4 if post else -1, p=p, seed=seed)
+    assert PF.gemm_path(x, True, w, False, y) == "mfma"
+    PF.gemm(x, True, w, False, y, bias=bias, mode=PF.EPI_FWD, epi=epi, mask=mask)
+    ref = x.double() @ w.double() + bias.double()
+    if pre:
+        ref = ref * torch.from_numpy(keep_mask(M * N, *seed, 3, p).reshape(M, N)).to(DEV) / (1 - p)
+    if relu:
+        ref = torch.relu(ref)
+    if post:
+        ref = ref * torch.from_numpy(keep_mask(M * N, *seed, 4, p).reshape(M, N)).to(DEV) / (1 - p)
+    err = (y.double() - ref).abs()
+    assert err.max().item() < 1e-2 * ref.abs().max().item(), err.max().item()
+    assert torch.equal(y == 0, ref == 0) or (y == 0).ne(ref == 0).double().mean().item() < 1e-5
+    if relu:
+        bits = torch.stack([(mask[:, :N // 8].int() >> b) & 1 for b in range(8)], dim=2).reshape(M, N)
+        assert torch.equal(bits.bool(), y.float() > 0)
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (8192 + 64, 1024 + 64, 256), (256, 4096, 64)])
 def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
     """EPI_FWD writes bit(y > 0); EPI_BWD reading those bits == EPI_BWD reading y."""

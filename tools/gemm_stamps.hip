@@ -60,8 +60,24 @@ int main(int argc, char** argv) {
   // the library's dispatch (gemm_mfma.hip: launch_bk64_256 / launch_fp8): each stage's GEMM with its
   // specialised epilogue (EK_*); *_gen = the same GEMM on the generic epilogue (A/B)
   constexpr int R = EK_RELU, S = EK_STORE, M = EK_BWD_MASK, G = EK_ANY;
+  constexpr int F1 = EK_F_RELU_POST, F2 = EK_F_RELU_PREPOST, F3 = EK_F_PRE;  // fixed forward kinds
   std::vector<Case> cases = {
       {"fwd_L1", B, 4096, 1024, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      // stage-0 epilogue decomposition (EK_RELU kernel): 9 nothing, 8 bias, 7 ReLU, 4 bias+ReLU+bitmask, 5 bias+ReLU+dropout (no bitmask)
+      {"fwdL1_m9", B, 4096, 1024, true, false, false, 9, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwdL1_m8", B, 4096, 1024, true, false, false, 8, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwdL1_m7", B, 4096, 1024, true, false, false, 7, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwdL1_m4", B, 4096, 1024, true, false, false, 4, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwdL1_m5", B, 4096, 1024, true, false, false, 5, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
+      {"fwdL1_st", B, 4096, 1024, true, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, S>},
+      // the trainer's three forward stages on EK_RELU vs their fixed kinds (same arguments)
+      {"fwd_L1_s0_fx", B, 4096, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, F1>},
+      {"fwd_L2_fx", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, F2>},
+      {"fwd_L3_fx", B, 1024, 4096, true, false, false, 11, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, F3>},
+      {"f8n_fwd_L1", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, R>, 1},
+      {"f8n_fwd_L1_fx", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, F1>, 1},
+      {"f8n_fwd_L2", B, 1024, 8192, true, false, false, 11, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, R>, 1},
+      {"f8n_fwd_L2_fx", B, 1024, 8192, true, false, false, 11, 2, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, F3>, 1},
       {"fwd_L1_s0", B, 4096, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, R>},
       // two co-resident 4-wave workgroups per CU on 256x128 tiles (VAR 7: 3-slot 32-deep buffer ring)
       {"fwd_L1_s0_2wg", B, 4096, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 7, R>, 0, 256, 128},
