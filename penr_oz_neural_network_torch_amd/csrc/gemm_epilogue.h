@@ -165,8 +165,12 @@ PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], u32x2_t bits, int nlane) {
 #pragma unroll
   for (int j = 0; j < L::COLS; ++j) {
     const uint32_t w = bits[L::n_off(j) >> 5] >> ((L::n_off(j) & 31) + nlane);
+    // bit r -> an all-ones / all-zeros word (v_bfe_i32) ANDed onto the float: 2 VALU per element
+    // instead of and + compare + select
 #pragma unroll
-    for (int r = 0; r < 4; ++r) v[j][r] = ((w >> r) & 1u) ? v[j][r] : 0.f;
+    for (int r = 0; r < 4; ++r)
+      v[j][r] = __uint_as_float(__float_as_uint(v[j][r]) &
+                                static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(w), r, 1)));
   }
 }
 

@@ -38,8 +38,12 @@ PZ_DEV uint16_t f2bf(float f) {  // RNE; hipcc lowers the cast to v_cvt_pk_bf16_
   __bf16 b = static_cast<__bf16>(f);
   return __builtin_bit_cast(uint16_t, b);
 }
+// two floats -> one packed bf16 pair as ONE v_cvt_pk_bf16_f32 (RNE, NaN-safe): the scalar form
+// (two casts + shift + or) cost 4 VALU instructions per pair in every epilogue
+typedef float pz_f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 pz_bf16x2_t __attribute__((ext_vector_type(2)));
 PZ_DEV uint32_t pack_bf2(float lo, float hi) {
-  return static_cast<uint32_t>(f2bf(lo)) | (static_cast<uint32_t>(f2bf(hi)) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(pz_f32x2_t{lo, hi}, pz_bf16x2_t));
 }
 
 template <typename T> PZ_DEV float to_f(T v) { return static_cast<float>(v); }

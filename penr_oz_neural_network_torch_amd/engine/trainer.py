@@ -864,6 +864,18 @@ class FusedTrainer:
         if self._act_su is not None:
             ops.scale_update(self._act_su[0], self._act_su[1], self._act_su[2], True)
             self._act_su = None
+        # PZ_PREFETCH_MAIN=1: the NEXT step's minibatch is gathered into the other sample set
+        # right here, on this stream between the head and the first backward GEMM, where it has the
+        # HBM to itself, instead of at the head of the next step (26 us there, behind the
+        # first-layer update and beside the side stream's largest one). Measured SLOWER in the step
+        # (mlp4 1.130-1.134 vs 1.115-1.119 ms, profiles/r3_ab_prefetch_main.txt): off by default.
+        # The other set was last read by the previous step's kernels, all earlier on this stream.
+        # Not for the fp8 policy (one e4m3 input copy) or regression targets.
+        if (overlap and not capture and indices is None and self.data8 is None and self.tgt is None
+                and self._pf_args is None and os.environ.get("PZ_PREFETCH_MAIN", "0") == "1"
+                and epoch + 1 < self.costs.numel()):
+            self._pf_args = (epoch + 1, 1 - self.parity, batch)
+            self._prefetch()
 
         # ---------------- backward
         self._phase("pz.backward")
