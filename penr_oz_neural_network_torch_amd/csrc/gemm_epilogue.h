@@ -348,8 +348,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     for (int j = 0; j < COLS; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-#pragma unroll
-        for (int o = 1; o < L::RED; o <<= 1) cs[j][r] += __shfl_xor(cs[j][r], o, 64);
+        cs[j][r] = group_sum<L::RED>(cs[j][r]);
   }
   PZ_STAMP(5);  // (diagnostic builds: stage math + LDS image writes done, wave 0)
   __syncthreads();

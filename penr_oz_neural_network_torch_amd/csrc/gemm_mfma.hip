@@ -992,11 +992,7 @@ gemm_mfma_kernel(const GemmArgs p) {
     if (p.colsum != nullptr) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float s = cs[r];
-        s += __shfl_xor(s, 1, 64);
-        s += __shfl_xor(s, 2, 64);
-        s += __shfl_xor(s, 4, 64);
-        s += __shfl_xor(s, 8, 64);
+        const float s = group_sum<16>(cs[r]);
         if ((lane & 15) == 0 && n + r < p.N) atomicAdd(p.colsum + n + r, s);
       }
     }

@@ -248,19 +248,40 @@ PZ_DEV void epi_bwd4(float g[4], const float y_in[4], uint64_t idx, const EpiSpe
 // ------------------------------------------------------------------------------------------
 // wave / block reductions (wave64)
 // ------------------------------------------------------------------------------------------
-PZ_DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// Reductions over DPP rows (16 lanes) with in-row DPP moves — quad_perm xor 1, xor 2, then
+// row_half_mirror and row_mirror (each lane then holds its row's total) — instead of ds_bpermute
+// shuffles (an LDS round trip of ~100 cycles per step on a serial chain); the four row totals are
+// combined through v_readlane. Every lane returns the same value.
+template <typename Op>
+PZ_DEV float row16_reduce(float v, Op op) {
+  // (the dpp control must be a literal: one builtin call per pattern)
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xF, 0xF, false)));   // xor 1
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xF, 0xF, false)));   // xor 2
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xF, 0xF, false)));  // half mirror
+  v = op(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xF, 0xF, false)));  // mirror
   return v;
 }
-PZ_DEV float wave_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-  return v;
+template <typename Op>
+PZ_DEV float wave_reduce(float v, Op op) {
+  v = row16_reduce(v, op);
+  const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+  const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+  const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+  return op(op(r0, r1), op(r2, r3));
 }
-PZ_DEV float wave_min(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+struct OpAdd { PZ_DEV float operator()(float a, float b) const { return a + b; } };
+struct OpMax { PZ_DEV float operator()(float a, float b) const { return fmaxf(a, b); } };
+struct OpMin { PZ_DEV float operator()(float a, float b) const { return fminf(a, b); } };
+PZ_DEV float wave_sum(float v) { return wave_reduce(v, OpAdd{}); }
+PZ_DEV float wave_max(float v) { return wave_reduce(v, OpMax{}); }
+PZ_DEV float wave_min(float v) { return wave_reduce(v, OpMin{}); }
+// sum over the RED consecutive lanes sharing a 16- or 32-lane group (GEMM epilogue column sums)
+template <int RED>
+PZ_DEV float group_sum(float v) {
+  static_assert(RED == 16 || RED == 32, "16- or 32-lane groups");
+  v = row16_reduce(v, OpAdd{});
+  if constexpr (RED == 32) v += __shfl_xor(v, 16, 64);
   return v;
 }
 PZ_DEV double wave_sum_d(double v) {
