@@ -155,14 +155,14 @@ __global__ void __launch_bounds__(256) xent_head_kernel(XentArgs a) {
 // WAVES = 16 (one row per wave, 1024-thread blocks): the row's reductions are serial shuffle
 // chains, so the kernel is latency-bound and wants many resident waves; the block still owns
 // kBf16HeadRows rows, which keeps the bias-gradient atomics at one per column per 32 rows.
-template <int NCH, int WAVES>
+template <int NCH, int WAVES, int RPB = kBf16HeadRows>
 __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) {
   apply_scale_update(a.su);
   a.epi = epi_resolve(a.epi);
   extern __shared__ float cs_lds[];  // [WAVES][cols] wave partials (when colsum)
   __shared__ float red[WAVES];
-  constexpr int RPW = kBf16HeadRows / WAVES;
-  static_assert(RPW * WAVES == kBf16HeadRows, "rows per block split over the waves");
+  constexpr int RPW = RPB / WAVES;
+  static_assert(RPW * WAVES == RPB, "rows per block split over the waves");
   const uint16_t* __restrict__ logits = static_cast<const uint16_t*>(a.logits);
   uint16_t* __restrict__ dh = static_cast<uint16_t*>(a.dh);
   uint16_t* __restrict__ probs = static_cast<uint16_t*>(a.probs);
@@ -177,7 +177,7 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
   bool ok[NCH];
 #pragma unroll
   for (int j = 0; j < NCH; ++j) ok[j] = (lane + 64 * j) * 8 < a.cols;
-  const int row0 = blockIdx.x * kBf16HeadRows + wave * RPW;
+  const int row0 = blockIdx.x * RPB + wave * RPW;
   uint4 raw[RPW][NCH];
   int64_t labels[RPW];  // fetched with the logits: no dependent load inside the row loop
 #pragma unroll
@@ -416,6 +416,153 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, A*
   if (threadIdx.x < 64 && c < cols) atomicAdd(out + c, part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
+// Lean bf16 CE head for the trainer's logits stage: no probabilities, dZ always stored, the
+// logits' dropout (if any) applied BEFORE the head only (the reference's linear -> dropout ->
+// softmax), and the optional bias-gradient sums / e5m2 copy selected at COMPILE time. The general
+// kernel above carries every option as runtime branches: ~4.4k instructions, 13.4 us for the
+// [8192, 1024] head with no dropout and no column sums against a 4.1 us copy of the same bytes
+// (tools/head_bench.py). One row per wave-iteration, every load issued up front.
+template <int NCH, int WAVES, bool COLSUM, bool OUT8, bool DROP>
+__global__ void __launch_bounds__(WAVES * 64) xent_head_lean_kernel(XentArgs a) {
+  apply_scale_update(a.su);
+  const EpiSpec e = epi_resolve(a.epi);
+  extern __shared__ float cs_lds[];  // [WAVES][cols] wave partials (COLSUM)
+  __shared__ float red[WAVES];
+  constexpr int RPW = kBf16HeadRows / WAVES;
+  const uint16_t* __restrict__ logits = static_cast<const uint16_t*>(a.logits);
+  uint16_t* __restrict__ dh = static_cast<uint16_t*>(a.dh);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  float cs[NCH][8];
+#pragma unroll
+  for (int j = 0; j < NCH; ++j)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) cs[j][q] = 0.f;
+  const int row0 = blockIdx.x * kBf16HeadRows + wave * RPW;
+  uint4 raw[RPW][NCH];
+  int labels[RPW];
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = row0 + rr;
+    labels[rr] = row < a.rows_valid ? static_cast<int>(a.labels[row]) : -1;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+      raw[rr][j] = row < a.rows ? *reinterpret_cast<const uint4*>(logits + static_cast<int64_t>(row) * a.ld + (lane + 64 * j) * 8)
+                                : make_uint4(0, 0, 0, 0);
+  }
+  const float gs = static_cast<float>(a.grad_scale);
+  const float qs8 = OUT8 ? *a.out8_qscale : 1.f;
+  float loss_acc = 0.f, amax8 = 0.f;
+#pragma unroll
+  for (int rr = 0; rr < RPW; ++rr) {
+    const int row = row0 + rr;
+    if (row >= a.rows) break;
+    const bool valid = row < a.rows_valid;  // (wave-uniform) padding rows: zero gradient
+    const int label = labels[rr];
+    float v[NCH][8];
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const uint32_t w[4] = {raw[rr][j].x, raw[rr][j].y, raw[rr][j].z, raw[rr][j].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { v[j][2 * q] = bf2f(w[q] & 0xFFFF); v[j][2 * q + 1] = bf2f(w[q] >> 16); }
+    }
+    float mx = -INFINITY, xl = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        mx = fmaxf(mx, v[j][q]);
+        xl += (lane + 64 * j) * 8 + q == label ? v[j][q] : 0.f;
+      }
+    mx = wave_max(mx);
+    float se = 0.f;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        v[j][q] = __expf(v[j][q] - mx);
+        se += v[j][q];
+      }
+    se = wave_sum(se);
+    xl = wave_sum(xl);
+    if (valid && lane == 0) loss_acc += (mx + __logf(se) - xl) * static_cast<float>(a.loss_scale);
+    const float inv = valid ? gs / se : 0.f;  // padding rows: every gradient 0
+    const uint64_t row_idx = static_cast<uint64_t>(row) * static_cast<uint64_t>(a.idx_ld);
+#pragma unroll
+    for (int j = 0; j < NCH; ++j) {
+      const int c0 = (lane + 64 * j) * 8;
+      float g[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) g[q] = v[j][q] * inv - (c0 + q == label && valid ? gs : 0.f);
+      if constexpr (DROP) {  // d(dropout_pre): keep ? g * scale : 0 (pairs 2p, 2p+1 share a hash)
+        const uint32_t p0 = static_cast<uint32_t>((row_idx + c0) >> 1);
+#pragma unroll
+        for (int h = 0; h < 4; ++h) {
+          const uint32_t b = mix32((p0 + h) ^ e.key_pre);
+          g[2 * h] = (b & 0xFFFFu) >= e.thresh16 ? g[2 * h] * e.scale : 0.f;
+          g[2 * h + 1] = (b >> 16) >= e.thresh16 ? g[2 * h + 1] * e.scale : 0.f;
+        }
+      }
+      const uint4 gb = make_uint4(pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7]));
+      if (!a.skip_dh) *reinterpret_cast<uint4*>(dh + static_cast<int64_t>(row) * a.ld_dh + c0) = gb;
+      if constexpr (OUT8) {  // e5m2 copy of the stored bf16 values (as quantize_rows would)
+        const uint32_t w[4] = {gb.x, gb.y, gb.z, gb.w};
+        float x[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          x[2 * q] = bf2f(w[q] & 0xFFFFu);
+          x[2 * q + 1] = bf2f(w[q] >> 16);
+          amax8 = fmaxf(amax8, fmaxf(fabsf(x[2 * q]), fabsf(x[2 * q + 1])));
+        }
+        *reinterpret_cast<u32x2_t*>(a.out8 + static_cast<int64_t>(row) * a.ld_out8 + c0) = to_e5m2x8(x, qs8);
+      }
+      if constexpr (COLSUM) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cs[j][q] += g[q];
+      }
+    }
+  }
+  if constexpr (OUT8) {
+    if (a.amax != nullptr) {  // one atomic per block
+      __shared__ float red8[WAVES];
+      const float m = wave_max(amax8);
+      if (lane == 0) red8[wave] = m;
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        float t = red8[0];
+#pragma unroll
+        for (int w = 1; w < WAVES; ++w) t = fmaxf(t, red8[w]);
+        atomicMax(reinterpret_cast<unsigned int*>(a.amax), __float_as_uint(t));
+      }
+    }
+  }
+  if (a.loss != nullptr) {
+    const float t = wave_sum(loss_acc);
+    if (lane == 0) red[wave] = t;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) s += red[w];
+      atomicAdd(a.loss + (a.loss_slots > 1 ? blockIdx.x % a.loss_slots : 0), s);
+    }
+  }
+  if constexpr (COLSUM) {
+    float* mine = cs_lds + wave * a.cols;
+#pragma unroll
+    for (int j = 0; j < NCH; ++j)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) mine[(lane + 64 * j) * 8 + q] = cs[j][q];
+    __syncthreads();
+    for (int c = threadIdx.x; c < a.cols; c += WAVES * 64) {
+      float t = 0.f;
+#pragma unroll
+      for (int w = 0; w < WAVES; ++w) t += cs_lds[w * a.cols + c];
+      atomicAdd(a.colsum + c, t);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // minibatch gather: out[i] = cast(data[idx_i]), idx_i = hash(seed, i) mod n_data (or given)
 // ---------------------------------------------------------------------------------------------
@@ -533,17 +680,45 @@ hipError_t stage_bwd(const void* g, const void* y, void* dx, int dtype, int64_t 
   return hipGetLastError();
 }
 
-template <int NCH, int W>
+template <int NCH, int W, int RPB = kBf16HeadRows>
 hipError_t launch_xent_bf16(const XentArgs& a, dim3 grid, size_t lds, hipStream_t s) {
   static bool attr = false;  // > 64 KiB of dynamic LDS (W partial rows of up to 2048 columns)
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(xent_head_bf16_kernel<NCH, W>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(xent_head_bf16_kernel<NCH, W, RPB>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, W * 512 * NCH * 4);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL((xent_head_bf16_kernel<NCH, W>), grid, dim3(W * 64), lds, s, a);
+  hipLaunchKernelGGL((xent_head_bf16_kernel<NCH, W, RPB>), grid, dim3(W * 64), lds, s, a);
   return hipGetLastError();
+}
+
+template <int NCH, bool CS, bool O8, bool DR>
+hipError_t launch_xent_lean1(const XentArgs& a, dim3 grid, size_t lds, hipStream_t s) {
+  constexpr int W = 16;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(xent_head_lean_kernel<NCH, W, CS, O8, DR>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, W * 512 * NCH * 4);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((xent_head_lean_kernel<NCH, W, CS, O8, DR>), grid, dim3(W * 64), lds, s, a);
+  return hipGetLastError();
+}
+template <int NCH>
+hipError_t launch_xent_lean_n(const XentArgs& a, bool cs, bool o8, bool dr, dim3 grid, size_t lds, hipStream_t s) {
+  if (cs) {
+    if (o8) return dr ? launch_xent_lean1<NCH, true, true, true>(a, grid, lds, s) : launch_xent_lean1<NCH, true, true, false>(a, grid, lds, s);
+    return dr ? launch_xent_lean1<NCH, true, false, true>(a, grid, lds, s) : launch_xent_lean1<NCH, true, false, false>(a, grid, lds, s);
+  }
+  if (o8) return dr ? launch_xent_lean1<NCH, false, true, true>(a, grid, lds, s) : launch_xent_lean1<NCH, false, true, false>(a, grid, lds, s);
+  return dr ? launch_xent_lean1<NCH, false, false, true>(a, grid, lds, s) : launch_xent_lean1<NCH, false, false, false>(a, grid, lds, s);
+}
+hipError_t launch_xent_lean(const XentArgs& a, int nch, bool cs, bool o8, bool dr, dim3 grid, size_t lds, hipStream_t s) {
+  if (nch == 1) return launch_xent_lean_n<1>(a, cs, o8, dr, grid, lds, s);
+  if (nch == 2) return launch_xent_lean_n<2>(a, cs, o8, dr, grid, lds, s);
+  return launch_xent_lean_n<4>(a, cs, o8, dr, grid, lds, s);
 }
 
 constexpr int kMaxLdsCols = 16384;  // 64 KiB of fp32 column partials
@@ -578,7 +753,28 @@ hipError_t xent_head(const XentArgs& in, hipStream_t s) {
   constexpr int kW = 16;         // waves per bf16 block: one row each
   const size_t ldsw = kW * lds;  // the bf16 kernel keeps one partial row per wave (up to 128 KiB)
   hipError_t le = hipSuccess;
+  // the lean kernel: the trainer's logits stage (no probabilities, dZ stored, at most the logits'
+  // pre-head dropout), row width a multiple of 512 (PZ_HEAD_LEAN=0: the general kernel, A/B)
+  static const bool lean_off = [] {
+    const char* e = getenv("PZ_HEAD_LEAN");
+    return e != nullptr && atoi(e) == 0;
+  }();
+  const EpiSpec& ep = a.epi;
+  const int nch = a.cols / 512;
+  if (!lean_off && vec && a.probs == nullptr && a.dh != nullptr && a.cols % 512 == 0 && nch >= 1 && nch <= 4 &&
+      nch != 3 && ep.act == ACT_NONE && !ep.drop_post && !ep.drop_all && a.labels != nullptr &&
+      (a.out8 == nullptr || xent_head_out8_ok(a))) {
+    const bool cs = a.colsum != nullptr, o8 = a.out8 != nullptr, dr = ep.drop_pre != 0;
+    return launch_xent_lean(a, nch, cs, o8, dr, grid16, cs ? ldsw : 0, s);
+  }
+  // PZ_HEAD_RPB=16 (A/B): 16-row blocks, one row per wave (twice the blocks and resident waves)
+  static const int rpb = [] {
+    const char* e = getenv("PZ_HEAD_RPB");
+    return e != nullptr ? atoi(e) : kBf16HeadRows;
+  }();
   if (vec && a.cols <= 512) le = launch_xent_bf16<1, kW>(a, grid16, ldsw, s);
+  else if (vec && a.cols <= 1024 && rpb == 16)
+    le = launch_xent_bf16<2, kW, 16>(a, dim3((a.rows + 15) / 16), ldsw, s);
   else if (vec && a.cols <= 1024) le = launch_xent_bf16<2, kW>(a, grid16, ldsw, s);
   else if (vec && a.cols <= 2048) le = launch_xent_bf16<4, kW>(a, grid16, ldsw, s);
   else {

@@ -395,6 +395,33 @@ def test_xent_head_fused_dropout_colsum(native_lib):
     assert (colsum.double() - dref.sum(0)).abs().max().item() < 1e-5
 
 
+@pytest.mark.parametrize("B,C,p", [(8192, 1024, 0.2), (1000, 512, 0.0), (64, 2048, 0.3)])
+def test_xent_head_bf16_lean_matches_fp64(native_lib, B, C, p):
+    """The lean bf16 head (the trainer's logits stage: widths of 512 / 1024 / 2048, dropout before
+    the head only, dZ + bias-gradient sums) == fp64 torch: loss, dZ = (softmax - onehot) / B
+    through the logits' keep mask, and the column sums; rows past rows_valid get a zero gradient."""
+    seed = (13, 2)
+    rows_valid = B - 8
+    logits = (torch.randn(B, C, device=DEV) * 2).to(torch.bfloat16)
+    labels = torch.randint(0, C, (B,), device=DEV)
+    loss = torch.zeros(4, device=DEV)
+    dh = torch.full((B, C), 7.0, device=DEV, dtype=torch.bfloat16)
+    colsum = torch.zeros(C, device=DEV)
+    ei, ef = PF.epi_spec(drop_pre=6 if p > 0 else -1, p=p, seed=seed)
+    torch.ops.pz.xent_head(logits, labels, rows_valid, loss, 1.0 / rows_valid, dh, 1.0 / rows_valid, colsum, None,
+                           ei, ef, C)
+    lg = logits[:rows_valid].double()
+    lref = F.cross_entropy(lg, labels[:rows_valid])
+    assert abs(loss.sum().item() - lref.item()) < 1e-4 * max(1.0, lref.item())
+    dref = (torch.softmax(lg, 1) - F.one_hot(labels[:rows_valid], C)) / rows_valid
+    if p > 0:
+        dref = dref * torch.from_numpy(keep_mask(B * C, *seed, 6, p).reshape(B, C))[:rows_valid].to(DEV) / (1 - p)
+    scale = dref.abs().max().item()
+    assert (dh[:rows_valid].double() - dref).abs().max().item() < 1e-2 * scale
+    assert (dh[rows_valid:] == 0).all()
+    assert (colsum.double() - dref.sum(0)).abs().max().item() < 1e-3 * scale * math.sqrt(B)
+
+
 @pytest.mark.parametrize("B,C", [(8192, 1024), (300, 520)])
 def test_xent_head_e5m2_copy(native_lib, B, C):
     """fp8 policy head: the bf16 kernel's e5m2 dZ copy equals quantize_rows of its bf16 dZ (same

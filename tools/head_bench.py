@@ -32,10 +32,15 @@ def main() -> None:
     dh = torch.empty(R, C, device=dev, dtype=torch.bfloat16)
     colsum = torch.zeros(C, device=dev)
     epi_i, epi_f = PF.epi_spec(drop_pre=4, p=0.2, seed=(1, 2), epoch=0)
+    no_i, no_f = PF.epi_spec()
     out = {}
-    for name, cs in (("colsum", colsum), ("no_colsum", None)):
+    for name, cs, ei, ef in (("colsum", colsum, epi_i, epi_f), ("no_colsum", None, epi_i, epi_f),
+                             ("no_colsum_no_dropout", None, no_i, no_f), ("copy_floor", None, None, None)):
         def run():
-            torch.ops.pz.xent_head(logits, labels, R, loss, 1.0 / R, dh, 1.0 / R, cs, None, epi_i, epi_f, C)
+            if ei is None:  # the same bytes through a plain device copy (read 16 MB, write 16 MB)
+                dh.copy_(logits)
+                return
+            torch.ops.pz.xent_head(logits, labels, R, loss, 1.0 / R, dh, 1.0 / R, cs, None, ei, ef, C)
         for _ in range(10):
             run()
         torch.cuda.synchronize()
