@@ -357,9 +357,63 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   const bool want8 = EK != EK_STORE && p.out8 != nullptr && (bwd ? p.out8_fmt == 1 : p.out8_fmt == 0);
   const float qs = want8 ? *p.out8_qscale : 1.f;
   float amax = 0.f;
-  // fixed forward kinds: the pass loop rolled by 4 (it indexes no accumulator; the unrolled
-  // 16-pass form is ~2.3k instructions of the kernel's I-cache footprint)
+  // Full tiles of the specialised kinds: every pass's image chunk is read up front (the
+  // accumulators are dead: 64 VGPRs of 16-B chunks fit), then the stores go out back to back
+  // from one base address advanced by a constant stride. The generic per-pass loop below waited
+  // on each ds_read before its store and recomputed a 64-bit row address (two quarter-rate
+  // multiplies) per pass behind per-pass range branches.
+  const bool full_tile = EK != EK_ANY && m0 + BM <= p.M && n0 + BN <= p.N;
+  if (full_tile) {
+    u32x4_t vv[PASSES];
+#pragma unroll
+    for (int s = 0; s < PASSES; ++s)
+      vv[s] = *reinterpret_cast<const PZ_LDS u32x4_t*>(smem + cimg_off<BN>(s * ROWS_PER_PASS + my_row, my_chunk * 8));
+    const int gn = n0 + my_chunk * 8;
+    const int64_t row0 = static_cast<int64_t>(m0 + my_row);
+    if (Cp != nullptr) {  // (fp8 policy: a bf16 output nobody reads is not written — only its copies)
+      uint16_t* dst = Cp + row0 * p.ldc + gn;
+      const int64_t step = static_cast<int64_t>(ROWS_PER_PASS) * p.ldc;
+#pragma unroll
+      for (int s = 0; s < PASSES; ++s) *reinterpret_cast<u32x4_t*>(dst + s * step) = vv[s];
+    }
+    if (!bwd && use_mask) {
+      uint8_t* mdst = p.mask + row0 * p.ldmask + gn / 8;
+      const int64_t mstep = static_cast<int64_t>(ROWS_PER_PASS) * p.ldmask;
+#pragma unroll
+      for (int s = 0; s < PASSES; ++s) {
+        uint32_t byte = 0;  // bit b = element gn+b > 0 (bf16: sign clear, magnitude nonzero)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint32_t lo = vv[s][q] & 0xFFFFu, hi = vv[s][q] >> 16;
+          byte |= ((lo - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q);
+          byte |= ((hi - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q + 1);
+        }
+        const uint32_t b1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0x55, 0xF, 0xF, false));
+        const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xAA, 0xF, 0xF, false));
+        const uint32_t b3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xFF, 0xF, 0xF, false));
+        if ((my_chunk & 3) == 0) *reinterpret_cast<uint32_t*>(mdst + s * mstep) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+      }
+    }
+    if (want8) {  // fp8 copy of the stored bf16 values + running |y| max
+      uint8_t* d8 = p.out8 + row0 * p.ldout8 + gn;
+      const int64_t step8 = static_cast<int64_t>(ROWS_PER_PASS) * p.ldout8;
+#pragma unroll
+      for (int s = 0; s < PASSES; ++s) {
+        float x[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          x[2 * q] = bf2f(vv[s][q] & 0xFFFFu);
+          x[2 * q + 1] = bf2f(vv[s][q] >> 16);
+          amax = fmaxf(amax, fmaxf(fabsf(x[2 * q]), fabsf(x[2 * q + 1])));
+        }
+        *reinterpret_cast<u32x2_t*>(d8 + s * step8) = bwd ? to_e5m2x8(x, qs) : to_e4m3x8(x, qs);
+      }
+    }
+  }
+  // ragged tiles (and the generic kind): one pass at a time with range checks; the fixed forward
+  // kinds keep it rolled by 4 (it indexes no accumulator)
   constexpr int kStoreUnroll = ek_fixed(EK) ? 4 : PASSES;
+  if (!full_tile) {
 #pragma unroll kStoreUnroll
   for (int s = 0; s < PASSES; ++s) {
     const int r = s * ROWS_PER_PASS + my_row;
@@ -401,6 +455,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
             byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
     }
   }
+  }  // !full_tile
   PZ_STAMP(6);  // (stores issued)
   if (want8 && p.amax != nullptr) {  // one atomic per workgroup (same-address atomics serialise)
     amax = wave_max(amax);
