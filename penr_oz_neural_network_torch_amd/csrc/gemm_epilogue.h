@@ -174,6 +174,21 @@ PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], u32x2_t bits, int nlane) {
   }
 }
 
+// ReLU bitmask byte of 8 packed bf16 (bit b = element b > 0). A bf16 is > 0 iff its sign is clear
+// and it is nonzero: per packed pair, ((w & 0x7FFF7FFF) + 0x7FFF7FFF) carries into bit 15 / 31
+// exactly for a nonzero magnitude (no carry crosses the halves) and ~w clears the negative ones —
+// 3 VALU per pair instead of 6 (positive NaN payloads count as > 0, as the compare form did)
+PZ_DEV uint32_t relu_bits8(const u32x4_t& v) {
+  uint32_t byte = 0;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t pos = ((v[q] & 0x7FFF7FFFu) + 0x7FFF7FFFu) & ~v[q] & 0x80008000u;
+    byte |= ((pos >> 15) & 1u) << (2 * q);
+    byte |= (pos >> 31) << (2 * q + 1);
+  }
+  return byte;
+}
+
 // Compile-time epilogue kinds. The generic epilogue (EK_ANY) carries every transform — sigmoid /
 // tanh with IEEE reciprocals, both dropout forms, aux-tile derivatives — unrolled over the tile's
 // rows: ~20k instructions, and it measured ~5 us per tile of instruction-fetch stalls with EVERY
@@ -381,13 +396,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       const int64_t mstep = static_cast<int64_t>(ROWS_PER_PASS) * p.ldmask;
 #pragma unroll
       for (int s = 0; s < PASSES; ++s) {
-        uint32_t byte = 0;  // bit b = element gn+b > 0 (bf16: sign clear, magnitude nonzero)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t lo = vv[s][q] & 0xFFFFu, hi = vv[s][q] >> 16;
-          byte |= ((lo - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q);
-          byte |= ((hi - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q + 1);
-        }
+        const uint32_t byte = relu_bits8(vv[s]);  // bit b = element gn+b > 0
         const uint32_t b1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0x55, 0xF, 0xF, false));
         const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xAA, 0xF, 0xF, false));
         const uint32_t b3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xFF, 0xF, 0xF, false));
@@ -424,14 +433,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     if (in_range) {
       if (Cp != nullptr)  // (fp8 policy: a bf16 output nobody reads is not written — only its copies)
         *reinterpret_cast<u32x4_t*>(Cp + static_cast<int64_t>(gm) * p.ldc + gn) = v;
-      if (!bwd && use_mask) {  // bf16 > 0: sign clear, magnitude nonzero
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const uint32_t lo = v[q] & 0xFFFFu, hi = v[q] >> 16;
-          byte |= ((lo - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q);
-          byte |= ((hi - 1u) < 0x7FFFu ? 1u : 0u) << (2 * q + 1);
-        }
-      }
+      if (!bwd && use_mask) byte = relu_bits8(v);
       if (want8) {  // e4m3 copy of the bf16 values + running |y| max
         float x[8];
 #pragma unroll
