@@ -75,6 +75,17 @@ CONFIGS = {
 DTYPE_LABEL = {"bfloat16": "bf16", "fp8": "fp8", "float32": "fp32", "float64": "fp64"}
 
 
+HEADLINE_METRIC = "training samples/sec (whole node), 4x8192 MLP bf16 at 1/2/4/8 MI355X"  # BASELINE.json
+
+
+def _metric_label(key: str, cfg: dict) -> str:
+    """BASELINE.json's metric string for the headline config; every other config names its own
+    model and precision (same unit, same whole-node aggregation)."""
+    if key == "mlp4":
+        return HEADLINE_METRIC
+    return f"training samples/sec (whole node), {cfg['name']}, {DTYPE_LABEL[cfg['dtype']]} on MI355X"
+
+
 def log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -127,7 +138,7 @@ def _emit(args, cfg, world, elapsed, costs, batch, ctx) -> None:
         return
     log(f"cost first/last = {costs[0]:.4f} / {costs[-1]:.4f}, finite={finite}")
     print(json.dumps({
-        "metric": "training samples/sec (whole node), 4x8192 MLP bf16 at 1/2/4/8 MI355X",
+        "metric": _metric_label(args.config, cfg),
         "value": round(value, 1),
         "unit": "samples/s",
         "n_gpus": world,
@@ -144,7 +155,11 @@ def _emit(args, cfg, world, elapsed, costs, batch, ctx) -> None:
                    "dist_backend": ctx.backend or "none", "dist_world_size": world,
                    "launcher": os.environ.get("PZ_BENCH_LAUNCHER", "torchrun" if world > 1 else "none"),
                    "dropout": args.dropout, "l2": args.l2, "config_key": args.config,
-                   "engine": cfg.get("engine", "fused")},
+                   "engine": cfg.get("engine", "fused"),
+                   # dense weight-gradient storage of the fused engine (PZ_GRAD_DTYPE: bf16 default,
+                   # fp32 = exact fp32 gradients into the fp32-master Adam)
+                   "grad_dtype": os.environ.get("PZ_GRAD_DTYPE", "bf16") if cfg["dtype"] in ("bfloat16", "fp8")
+                   else DTYPE_LABEL[cfg["dtype"]]},
     }), flush=True)
 
 

@@ -87,9 +87,11 @@ PZ_DEV void apply_scale_update(const SU& su) {
   if (su.n <= 0 || blockIdx.x != 0 || blockIdx.y != 0 || static_cast<int>(threadIdx.x) >= su.n) return;
   const int i = threadIdx.x;
   const float a = su.amax[i];
-  const float q = a > 0.f ? su.maxval / (a * su.headroom) : 1.f;
-  su.qs[2 * i] = q;
-  su.qs[2 * i + 1] = 1.f / q;
+  if (a > 0.f) {  // no amax this step (nothing quantised that tensor): keep the previous scale
+    const float q = su.maxval / (a * su.headroom);
+    su.qs[2 * i] = q;
+    su.qs[2 * i + 1] = 1.f / q;
+  }
   su.amax[i] = 0.f;
 }
 

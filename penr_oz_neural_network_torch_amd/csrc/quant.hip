@@ -67,9 +67,13 @@ __global__ void scale_update_kernel(float* amax, float* qs, int n, float headroo
   const int i = threadIdx.x + blockIdx.x * blockDim.x;
   if (i >= n) return;
   const float a = amax[i];
-  const float q = a > 0.f ? maxval / (a * headroom) : 1.f;
-  qs[2 * i] = q;
-  qs[2 * i + 1] = 1.f / q;
+  // no amax recorded (a tensor nothing quantised this step: a record-mode step, a stage with no
+  // e5m2 copy) carries no information: keep the previous scale instead of resetting it to 1
+  if (a > 0.f) {
+    const float q = maxval / (a * headroom);
+    qs[2 * i] = q;
+    qs[2 * i + 1] = 1.f / q;
+  }
   if (reset) amax[i] = 0.f;
 }
 

@@ -328,6 +328,23 @@ class FusedTrainer:
         sizes = {st.seg_w.offset: st.seg_w.numel for st in self.stages if st.kind == "gemm"}
         self._defer_key = max(gemm_w[1:], key=lambda k: sizes[k]) if self._defer else None
         self._deferred: list = []
+        # Backward ORDER (one process, side-stream updates): the weight-gradient GEMM of the
+        # LARGEST GEMM weight after the first layer is issued LAST, behind the dX chain and the
+        # first layer's dW. Every other update — the first-layer weight and the biases included —
+        # then runs on the side stream beside that long GEMM instead of after it, and the largest
+        # update runs beside the next step's first forward GEMM (which does not read that weight).
+        # The step's tail shrinks to the launch that queues it. PZ_BWD_ORDER=0: the reference
+        # order (dW then dX per layer, first-layer + bias update on the critical path). Not under
+        # data parallelism: there the last bucket's all-reduce is exposed, so the backward ends
+        # on the smallest dW (the first layer's, chunked).
+        self._late_idx = None
+        if (os.environ.get("PZ_BWD_ORDER", "1") == "1" and not self.ctx.enabled and not self.fuse_opt
+                and self.overlap and len(gemm_w) > 1):
+            cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
+            if cands:
+                self._late_idx = max(cands, key=lambda st: (st.seg_w.numel, st.index)).index
+        self._late_dw = None       # (stage, x_in, dZ) of the deferred weight-gradient GEMM
+        self._fwd_waits: dict = {}  # stage index -> event the next step's forward waits for
         self._pf_args = None       # (epoch, parity, batch) of the sample _prefetch gathers next
         self._pf_ready = None      # ((epoch, parity, batch, data id), event) of a gathered sample
         self.prefetched_steps = 0  # steps that consumed a prefetched sample
@@ -715,7 +732,7 @@ class FusedTrainer:
         if sample_size < world:
             raise ValueError(f"sample size {sample_size} is smaller than the {world} data-parallel ranks")
         # the global sample is split exactly (reference :441, 460 draw sample_size rows): rank r
-        # draws rows [r*S/W, (r+1)*S/W), the first S % W ranks one more. Every rank scales its
+        # draws rows [r*S//W, (r+1)*S//W): S % W ranks (the LAST ones) draw one row more. Every rank scales its
         # loss and gradients by 1/S (the GLOBAL sample), so the all-reduced sum is the global mean
         # with no 1/world factor — unequal shards weigh exactly by their share
         batch = (rank + 1) * sample_size // world - rank * sample_size // world
@@ -752,6 +769,9 @@ class FusedTrainer:
         if self._opt_done is not None:
             main.wait_event(self._opt_done)
             self._opt_done = None
+        for ev in self._fwd_waits.values():
+            main.wait_event(ev)
+        self._fwd_waits = {}
         self._early_done = None
         if self._ctr_epoch != epoch:
             self.epoch_ctr.fill_(epoch)
@@ -846,6 +866,9 @@ class FusedTrainer:
             if self._early_done is not None and st.kind == "gemm" and st.seg_w.offset in self._early_keys:
                 main.wait_event(self._early_done)
                 self._early_done = self._opt_done = None
+            ev = self._fwd_waits.pop(st.index, None)
+            if ev is not None:  # reordered backward: this stage's weights were updated on the side stream
+                main.wait_event(ev)
             x = self._forward_stage(st, x, batch, dropout, keys, rec)
             prev = st
         last = prev
@@ -854,6 +877,9 @@ class FusedTrainer:
         self._act_su = (self.aamax, self.aqs, 1.25, 448.0) if (self.fp8 and not record) else None
 
         # ---------------- head
+        for ev in self._fwd_waits.values():  # (stages skipped above: record mode, no GEMM)
+            main.wait_event(ev)
+        self._fwd_waits = {}
         if self._opt_done is not None:
             main.wait_event(self._opt_done)
             self._opt_done = None
@@ -886,7 +912,8 @@ class FusedTrainer:
             before = self.stages[si - 1] if si > 0 else None
             x_in = before.buffers["y"] if before is not None else self.x_in
             g, g_pre = self._backward_stage(st, before, x_in, g, g_pre, batch, dropout, keys, rec, handles)
-        if self.fp8 and any(getattr(st, "fp8_bwd", False) for st in self.stages):
+        if self.fp8 and any(getattr(st, "fp8_bwd", False) or getattr(st, "g8_from_epi", False)
+                            for st in self.stages):
             # this step's gradient amax -> next step's e5m2 scales (delayed scaling): applied by the
             # next step's first launch (the sample gather)
             self._grad_su_pending = True
@@ -896,6 +923,9 @@ class FusedTrainer:
         self._phase("pz.update")
         handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:], exact=True))
         fin = dict(epoch_ctr=self.epoch_ctr, every=self._plan["every"] if self._plan else 1)
+        if overlap and self._late_dw is not None:
+            self._finish_reordered(main, l2, capture, epoch, row, fin, handles)
+            return
         if overlap:
             # the last update (first-layer weights, biases, batchnorm, embeddings) runs on THIS
             # stream right behind the last dW: the next step's first GEMM follows it in order (no
@@ -1135,27 +1165,35 @@ class FusedTrainer:
         if self.fuse_opt and self._ov is not None:
             self._dw_update(st, x_in, g)
             return self._backward_dx(st, before, g, batch, p, keys, rec)
+        if st.index == self._late_idx and rec is None and self._ov is not None:
+            # reordered backward: this weight's gradient GEMM is issued after the whole dX chain
+            # (its operands — the stage input and dZ — stay untouched until then)
+            out = self._backward_dx(st, before, g, batch, p, keys, rec)
+            self._late_dw = (st, x_in, g)
+            return out
         w_grad = self._w_grad(st.seg_w)
         # Data parallel: the first layer's gradient is the last bucket of the backward and nothing
         # is left to hide its all-reduce behind, so its dW GEMM runs in row chunks and chunk c's
         # all-reduce travels while chunk c+1 is computed (only the last chunk's is exposed)
-        chunks = self._dw_chunks if (before is None and self.ctx.enabled) else 1
-        if chunks < 2 or w_grad.shape[0] % (8 * chunks):
-            chunks = 1
+        chunks = self._dw_chunk_count(st)
         mine = []
         rows = w_grad.shape[0] // chunks
-        f8 = self._fp8_dw(st, g, w_grad) if chunks == 1 else None
+        # fp8 policy: the chunks run on the e4m3 x e5m2 operands too (column slices of the stage
+        # input's e4m3 copy) — _fp8_dw_ready checked the chunk shapes, so when the bf16 dZ went
+        # unwritten (store_c=False) the e5m2 copy is always what the dW GEMM reads
+        f8 = self._fp8_dw(st, g, w_grad)
         # (measured, not kept: these dW GEMMs on a stream of their own beside the dX chain, without
         # split-K: the concurrent GEMMs stretch each other, mlp4 1.26 vs 1.23 ms —
         # profiles/r3_ab_dw_stream.txt)
         for c in range(chunks):
             sl = slice(c * rows, (c + 1) * rows)
+            out = w_grad[sl] if chunks > 1 else w_grad
             if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
                 x8, sx, g8, sg = f8
-                PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
+                PF.gemm(x8[:, sl] if chunks > 1 else x8, False, g8, False, out, scale_a=sx, scale_b=sg)
             else:
-                PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False, w_grad[sl] if chunks > 1 else w_grad)
-            mine.append(self.ctx.all_reduce_async(w_grad[sl] if chunks > 1 else w_grad))
+                PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False, out)
+            mine.append(self.ctx.all_reduce_async(out))
         handles.extend(mine)
         # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
         # unless the GEMMs read the fp32 master itself (float32 policy)
@@ -1176,6 +1214,55 @@ class FusedTrainer:
                 self._opt_async(self._side_pending)
                 self._side_pending = []
         return out
+
+    def _finish_reordered(self, main, l2, capture, epoch, row, fin, handles) -> None:
+        """End of a reordered step (``PZ_BWD_ORDER``, one process). Main stream: the deferred
+        weight-gradient GEMM of the largest weight. Side stream, in order: every other pending
+        update (the other side-updated weights, then the first-layer weight + biases / batchnorm /
+        embedding), all beside that GEMM; then the deferred weight's own update and
+        ``step_finalize``, beside the next step's first forward GEMMs. The next step waits for the
+        first group before its first GEMM stage and for the rest before the deferred weight's
+        forward stage (``_fwd_waits``)."""
+        st, x_in, g = self._late_dw
+        self._late_dw = None
+        if self._side_pending:
+            self._opt_async(self._side_pending)
+            self._side_pending = []
+        for h in list(self._late_handles) + [handles[-1]]:
+            self.ctx.wait_one(h)
+        ready = torch.cuda.Event()
+        ready.record(main)  # the dX chain (bias column sums) and the first layer's dW are done
+        with torch.cuda.stream(self.opt_stream):
+            self.opt_stream.wait_event(ready)
+            self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
+            if self.fp8:
+                for s0 in self._late_stages:
+                    self._refresh_fp8_weights(s0, 1 - self.parity)
+            rest_ev = torch.cuda.Event()
+            rest_ev.record(self.opt_stream)
+        w_grad = self._w_grad(st.seg_w)
+        f8 = self._fp8_dw(st, g, w_grad)
+        if f8 is not None:
+            x8, sx, g8, sg = f8
+            PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
+        else:
+            PF.gemm(x_in, False, g, False, w_grad)
+        self._opt_async([(st.seg_w.offset, [self.ctx.all_reduce_async(w_grad)], [st])])
+        self._ov = None
+        with torch.cuda.stream(self.opt_stream):
+            self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row, **fin)
+            ev = torch.cuda.Event(enable_timing=not capture)
+            ev.record(self.opt_stream)
+        if capture:  # join the side stream into the capture stream
+            main.wait_event(ev)
+        else:
+            # stage 0 reads first-layer / embedding / batchnorm parameters of the rest group
+            self._fwd_waits = {0: rest_ev, st.index: ev}
+            self._opt_done = ev  # (the head: loss-slot reset by step_finalize)
+            self._early_done = None
+            self._last_event = ev
+        self.parity = 1 - self.parity
+        self._phase(None)
 
     def _quantize_g8(self, st: Stage, g):
         """dZ of an fp8 stage -> its e5m2 copy (delayed scaling; the first step calibrates on its
@@ -1214,8 +1301,27 @@ class FusedTrainer:
             return False
         x8 = self.x8 if st.index == 0 else self.stages[st.index - 1].buffers.get("y8")
         w_grad = self._w_grad(st.seg_w)
-        return (x8 is not None and w_grad.dtype == torch.bfloat16
-                and PF.gemm_path(x8, False, st.buffers["g8"], False, w_grad) == "mfma")
+        return x8 is not None and w_grad.dtype == torch.bfloat16 and self._fp8_dw_shape_ok(st, x8, w_grad)
+
+    def _dw_chunk_count(self, st: Stage) -> int:
+        """Row chunks of the stage's dW GEMM: the first layer's under data parallelism (its
+        all-reduce then travels chunk by chunk), else 1."""
+        if st.index != 0 or not self.ctx.enabled or self._dw_chunks < 2 or st.kind != "gemm":
+            return 1
+        rows = st.seg_w.shape[0]
+        return 1 if rows % (8 * self._dw_chunks) else self._dw_chunks
+
+    def _fp8_dw_shape_ok(self, st: Stage, x8, w_grad) -> bool:
+        """Every chunk of the fp8 dW GEMM (x8 column slice x e5m2 dZ) takes the MFMA path."""
+        key = ("dwshape", st.index)
+        ok = self._y_dead_cache.get(key)
+        if ok is None:
+            chunks = self._dw_chunk_count(st)
+            rows = w_grad.shape[0] // chunks
+            ok = self._y_dead_cache[key] = all(
+                PF.gemm_path(x8[:, c * rows:(c + 1) * rows], False, st.buffers["g8"], False,
+                             w_grad[c * rows:(c + 1) * rows]) == "mfma" for c in range(chunks))
+        return ok
 
     def _fp8_dw_ready_cached(self, st: Stage) -> bool:
         key = ("dw", st.index, st.index in self._g8_epi_ready)
@@ -1246,8 +1352,7 @@ class FusedTrainer:
         x8, sx = (self.x8, self.xqs[1:2]) if i == 0 else (self.stages[i - 1].buffers.get("y8"), self.aqs[i - 1, 1:2])
         if x8 is None or w_grad.dtype != torch.bfloat16:
             return None
-        g8 = st.buffers["g8"]
-        if PF.gemm_path(x8, False, g8, False, w_grad) != "mfma":
+        if not self._fp8_dw_shape_ok(st, x8, w_grad):
             return None
         return x8, sx, self._quantize_g8(st, g), self.gqs[i, 1:2]
 

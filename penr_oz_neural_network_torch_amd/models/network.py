@@ -382,7 +382,7 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                 sampler = torch.Generator().manual_seed(int(seed.item()))
         if sample_size < world:
             raise ValueError(f"sample size {sample_size} is smaller than the {world} data-parallel ranks")
-        # contiguous shards of the global sample; the first sample_size % world ranks take one more
+        # contiguous shards of the global sample; sample_size % world ranks (the LAST ones) take one more
         lo, hi = rank * sample_size // world, (rank + 1) * sample_size // world
         weight = (hi - lo) / sample_size  # this rank's share of the global mean loss
         activations = None

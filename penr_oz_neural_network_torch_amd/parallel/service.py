@@ -191,9 +191,13 @@ class TrainGroup:
     def wait_ready(self, timeout: float | None = None) -> bool:
         return self._ready.wait(timeout) and self._error is None
 
-    def _collect(self, timeout: float | None) -> list:
+    def _collect(self, timeout: float | None, straggler_s: float | None = None) -> list:
         """One reply per rank; ``None`` for a rank that did not answer (closed, or ``timeout`` s
-        passed). Stops early once the watchdog marks the group lost."""
+        passed). Stops early once the watchdog marks the group lost. ``straggler_s``: once ANY
+        rank has answered, the others must answer within that many seconds — a training may run
+        for hours, but its ranks finish together (every step ends in a collective), so a rank
+        still silent long after a peer reported is hung (a kernel that never returns, a deadlock
+        outside a collective) and must not hold the group lock forever."""
         out: list = [None] * len(self.conns)
         waiting = set(range(len(self.conns)))
         deadline = None if timeout is None else time.monotonic() + timeout
@@ -206,18 +210,28 @@ class TrainGroup:
                         waiting.discard(r)
                 except (EOFError, OSError):
                     waiting.discard(r)
+                if straggler_s is not None and len(waiting) < len(self.conns):
+                    late = time.monotonic() + straggler_s
+                    deadline = late if deadline is None else min(deadline, late)
+                    straggler_s = None  # armed once, at the first reply
             if deadline is not None and time.monotonic() > deadline:
                 break
         return out
 
-    def _lose(self, why: str, model_id: str | None = None) -> None:
+    def _lose(self, why: str, model_id: str | None = None, rank0_done: bool = False) -> None:
         self._lost = self._lost or why
         log.error("data-parallel training lost its group: %s", self._lost)
         self._teardown()
-        if model_id is not None:  # rank 0 owned the files and may have died with the group
+        # rank 0 owned the files and may have died with the group: mark the model Failed, unless
+        # rank 0 reported a completed training (its "Trained" checkpoint is final: a peer that
+        # died afterwards does not undo it) or the persisted status is no longer "Training"
+        if model_id is not None and not rank0_done:
             try:
                 from ..utils import checkpoint as ckpt
-                ckpt.set_status(model_id, "Failed")
+                if ckpt.load_meta(model_id).get("status") == "Training":
+                    ckpt.set_status(model_id, "Failed")
+            except FileNotFoundError:  # no checkpoint at all: nothing to mark
+                pass
             except Exception:  # pragma: no cover - keep the original failure
                 log.exception(f"could not mark model {model_id} failed")
 
@@ -244,11 +258,14 @@ class TrainGroup:
                 raise RuntimeError("data-parallel ranks could not load the model: " + "; ".join(failed))
             self._in_flight = True
             try:
-                results = self._collect(None)  # until every rank reported, or the group is lost
+                # until every rank reported, or the group is lost; once one rank reported, the
+                # rest get the process-group timeout plus a margin
+                results = self._collect(None, straggler_s=self.timeout_s + 60.0)
             finally:
                 self._in_flight = False
             if self._lost is not None or any(m is None for m in results):
-                self._lose("a rank did not report the end of the training", model.model_id)
+                self._lose("a rank did not report the end of the training", model.model_id,
+                           rank0_done=bool(results) and results[0] == "done")
                 raise RuntimeError(f"data-parallel training lost its group: {self._lost}")
             self._refresh(model)
             bad = [f"rank {r}: {m}" for r, m in enumerate(results) if m != "done"]

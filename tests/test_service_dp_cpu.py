@@ -124,3 +124,40 @@ def test_group_recovers_from_lost_workers(models_tmpdir, monkeypatch):
         g = _health_group(client)
         assert g["healthy"] and g["restarts"] == 2 and g["trainings"] == 2
         assert group.procs[0] is not victim and all(p.poll() is None for p in group.procs)
+
+
+def test_collect_straggler_deadline_and_lose_keeps_a_finished_model(models_tmpdir):
+    """a rank still silent long after a peer reported the end of the training is hung
+    and must not hold the group lock forever (straggler deadline); and losing the group after
+    rank 0 persisted a finished ("Trained") checkpoint must not rewrite it as "Failed"."""
+    from multiprocessing import Pipe
+
+    from neural_net_model import NeuralNetworkModel
+    from penr_oz_neural_network_torch_amd.parallel.service import TrainGroup
+    from penr_oz_neural_network_torch_amd.utils import checkpoint as ckpt
+
+    class _Listener:
+        def close(self):
+            pass
+
+    g = TrainGroup.__new__(TrainGroup)
+    (a0, b0), (a1, b1) = Pipe(), Pipe()
+    g.conns, g.procs, g._lost, g._listener, g._rdv_dir = [a0, a1], [], None, _Listener(), None
+    b0.send("done")  # rank 0 finished, rank 1 never answers
+    t0 = time.time()
+    assert g._collect(None, straggler_s=0.5) == ["done", None]
+    assert time.time() - t0 < 10
+    b1.send("done")
+    g2 = TrainGroup.__new__(TrainGroup)
+    g2.conns, g2._lost = [a1], None
+    assert g2._collect(None, straggler_s=0.5) == ["done"]  # nobody late: no deadline hit
+
+    for status, rank0_done, want in (("Trained", False, "Trained"), ("Training", True, "Training"),
+                                     ("Training", False, "Failed")):
+        m = NeuralNetworkModel("lose", [4, 8, 2], activation_algos=["tanh", "softmax"])
+        m.status = status
+        m.serialize()
+        g._lost = None
+        g._lose("test", "lose", rank0_done=rank0_done)
+        assert ckpt.load_meta("lose")["status"] == want, (status, rank0_done)
+    g._lose("test", "no_such_model")  # nothing persisted: nothing to mark, no error
