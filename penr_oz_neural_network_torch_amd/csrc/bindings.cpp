@@ -515,11 +515,13 @@ void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t
 Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::IntArrayRef is_weight,
                         at::IntArrayRef stat_slot, at::ArrayRef<optional<Tensor>> shadows,
                         at::ArrayRef<optional<Tensor>> grads16, at::IntArrayRef zero_grad,
-                        at::ArrayRef<optional<Tensor>> amax) {
+                        at::ArrayRef<optional<Tensor>> amax, at::ArrayRef<optional<Tensor>> w8,
+                        at::ArrayRef<optional<Tensor>> w8_amax_prev, at::ArrayRef<optional<Tensor>> w8_qs) {
   const size_t n = offsets.size();
   TORCH_CHECK(numels.size() == n && is_weight.size() == n && stat_slot.size() == n && shadows.size() == n &&
                   (grads16.empty() || grads16.size() == n) && (zero_grad.empty() || zero_grad.size() == n) &&
-                  (amax.empty() || amax.size() == n),
+                  (amax.empty() || amax.size() == n) && (w8.empty() || w8.size() == n) &&
+                  w8_amax_prev.size() == w8.size() && w8_qs.size() == w8.size(),
               "pz::pack_segments: length mismatch");
   Tensor out = at::empty({static_cast<int64_t>(n * sizeof(pz::OptSegment))}, at::TensorOptions().dtype(at::kByte));
   auto* segs = reinterpret_cast<pz::OptSegment*>(out.data_ptr<uint8_t>());
@@ -545,6 +547,18 @@ Tensor pack_segments_op(at::IntArrayRef offsets, at::IntArrayRef numels, at::Int
     if (!amax.empty() && amax[i].has_value() && amax[i]->defined()) {
       TORCH_CHECK(amax[i]->scalar_type() == at::kFloat && amax[i]->numel() >= 1, "pz::pack_segments: fp32 amax");
       s.amax = amax[i]->data_ptr<float>();
+    }
+    if (!w8.empty() && w8[i].has_value() && w8[i]->defined()) {
+      const Tensor& q = *w8[i];
+      TORCH_CHECK(q.is_contiguous() && q.numel() == numels[i] && q.element_size() == 1 &&
+                      q.scalar_type() == at::kFloat8_e4m3fn,
+                  "pz::pack_segments: e4m3 weight copy shape");
+      TORCH_CHECK(w8_amax_prev[i].has_value() && w8_amax_prev[i]->scalar_type() == at::kFloat &&
+                      w8_qs[i].has_value() && w8_qs[i]->scalar_type() == at::kFloat && w8_qs[i]->numel() >= 2,
+                  "pz::pack_segments: e4m3 copy needs fp32 amax_prev and {q, 1/q}");
+      s.w8 = reinterpret_cast<uint8_t*>(q.data_ptr());
+      s.w8_amax_prev = w8_amax_prev[i]->data_ptr<float>();
+      s.w8_qs = w8_qs[i]->data_ptr<float>();
     }
     std::memcpy(segs + i, &s, sizeof(s));
   }
@@ -769,7 +783,8 @@ void quantize_rows_op(const Tensor& x, const Tensor& out, const Tensor& qs, cons
 
 void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tensor& stats_prev, const Tensor& stats_cur,
                       const Tensor& slot_numel, int64_t nslots, double l2, const Tensor& costs, int64_t epoch,
-                      const Tensor& ratios, int64_t ratio_row, const optional<Tensor>& epoch_ctr, int64_t every) {
+                      const Tensor& ratios, int64_t ratio_row, const optional<Tensor>& epoch_ctr, int64_t every,
+                      const optional<Tensor>& clear) {
   check_dev(costs, "costs");
   const bool dev_epoch = epoch < 0;  // read from the counter (graph-replayed step)
   TORCH_CHECK(!dev_epoch || epoch_ctr.has_value(), "pz::step_finalize: epoch < 0 needs the epoch counter");
@@ -800,6 +815,11 @@ void step_finalize_op(const optional<Tensor>& loss, double loss_div, const Tenso
   a.n_costs = static_cast<int>(costs.numel());
   a.n_ratio_rows = static_cast<int>(ratios.numel() / (nslots > 0 ? nslots : 1));
   a.epoch_ptr = const_cast<int*>(epoch_counter(epoch_ctr));
+  if (clear.has_value() && clear->defined()) {
+    TORCH_CHECK(clear->scalar_type() == at::kFloat && clear->is_contiguous(), "pz::step_finalize: fp32 clear");
+    a.clear = clear->data_ptr<float>();
+    a.nclear = static_cast<int>(clear->numel());
+  }
   PZ_HIP_CHECK(pz::step_finalize(a, cur_stream(costs)));
 }
 
@@ -900,7 +920,8 @@ TORCH_LIBRARY(pz, m) {
         "Tensor(d!)? out8=None, Tensor(s!)? su_amax=None, Tensor(t!)? su_qs=None, float su_headroom=1.0, "
         "float su_maxval=448.0) -> ()");
   m.def("pack_segments(int[] offsets, int[] numels, int[] is_weight, int[] stat_slot, Tensor?[] shadows, "
-        "Tensor?[] grads16, int[] zero_grad, Tensor?[] amax) -> Tensor");
+        "Tensor?[] grads16, int[] zero_grad, Tensor?[] amax, Tensor?[] w8, Tensor?[] w8_amax_prev, "
+        "Tensor?[] w8_qs) -> Tensor");
   m.def("optimizer_step(Tensor(a!) params, Tensor(e!) grads, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor segments, "
         "Tensor block_seg, int num_segments, int total_blocks, bool adam, float lr, float beta1, float beta2, float eps, "
         "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor(d!)? stats, Tensor? hp=None, "
@@ -919,7 +940,7 @@ TORCH_LIBRARY(pz, m) {
   m.def("embedding_bwd(Tensor dout, Tensor idx, Tensor(a!) dtable) -> ()");
   m.def("step_finalize(Tensor(e!)? loss, float loss_div, Tensor(a!) stats_prev, Tensor stats_cur, Tensor slot_numel, "
         "int nslots, float l2, Tensor(b!) costs, int epoch, Tensor(c!) ratios, int ratio_row, "
-        "Tensor(d!)? epoch_ctr=None, int every=1) -> ()");
+        "Tensor(d!)? epoch_ctr=None, int every=1, Tensor(f!)? clear=None) -> ()");
   m.def("amax_abs(Tensor x, Tensor(a!) amax) -> ()");
   m.def("scale_update(Tensor(a!) amax, Tensor(b!) qs, float headroom, bool reset, float maxval=448.0) -> ()");
   m.def("quant_transpose(Tensor w, Tensor(a!) out, Tensor(b!) qs, Tensor? amax=None, Tensor(c!)? amax_clear=None) -> ()");

@@ -21,6 +21,15 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kPerThread = kOptElemsPerBlock / kThreads;  // 16
+constexpr float kE4m3Max = 448.f;
+
+// four floats -> four OCP e4m3 bytes (saturated to +-448, round to nearest even)
+PZ_DEV uint32_t e4m3x4(float a, float b, float c, float d) {
+  auto sat = [](float x) { return fminf(fmaxf(x, -kE4m3Max), kE4m3Max); };
+  uint32_t w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(a), sat(b), 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(sat(c), sat(d), w, true);
+  return w;
+}
 
 PZ_DEV int find_segment(const int64_t* block_seg, int nseg, int block) {
   int lo = 0, hi = nseg - 1;
@@ -143,6 +152,15 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
   const bool stats = seg.stat_slot >= 0;
   double st[4] = {0.0, 0.0, 0.0, 0.0};
   float am = 0.f;  // max |w_new| (fp8 weight scaling, seg.amax)
+  float q8 = 1.f;  // e4m3 copy scale (delayed: from the previous update's amax)
+  if (seg.w8 != nullptr) {
+    const float ap = *seg.w8_amax_prev;
+    q8 = ap > 0.f ? kE4m3Max / ap : seg.w8_qs[0];
+    if (local0 == 0 && threadIdx.x == 0) {  // the segment's first block publishes the record
+      seg.w8_qs[0] = q8;
+      seg.w8_qs[1] = 1.f / q8;
+    }
+  }
 
   if (((seg.offset | seg.numel) & 3) == 0) {
     // the loads of PRE consecutive vectors of the thread are issued before their first store (the
@@ -202,6 +220,8 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
       }
       vst<R>(a.params + gi, p1);
       if constexpr (VN == 4) {
+        if (seg.w8 != nullptr)
+          *reinterpret_cast<uint32_t*>(seg.w8 + li) = e4m3x4(p1[0] * q8, p1[1] * q8, p1[2] * q8, p1[3] * q8);
         if (seg.shadow != nullptr) {
           if (seg.shadow_dtype == DT_BF16)
             *reinterpret_cast<uint2*>(static_cast<uint16_t*>(seg.shadow) + li) =
@@ -239,6 +259,10 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
         a.exp_avg_sq[gi] = v;
       }
       a.params[gi] = p1;
+      if (seg.w8 != nullptr) {
+        const float x = static_cast<float>(p1) * q8;
+        seg.w8[li] = static_cast<uint8_t>(e4m3x4(x, 0.f, 0.f, 0.f) & 0xFFu);
+      }
       if (seg.shadow != nullptr) {
         if (seg.shadow_dtype == DT_BF16) static_cast<uint16_t*>(seg.shadow)[li] = f2bf(static_cast<float>(p1));
         else static_cast<float*>(seg.shadow)[li] = static_cast<float>(p1);
@@ -335,6 +359,7 @@ __global__ void step_finalize_kernel(FinalizeArgs a) {
   __syncthreads();
   // the previous stats buffer becomes the next step's accumulation target
   for (int k = threadIdx.x; k < 4 * a.nslots; k += blockDim.x) a.stats_prev[k] = 0.0;
+  for (int k = threadIdx.x; k < a.nclear; k += blockDim.x) a.clear[k] = 0.f;
 }
 
 }  // namespace

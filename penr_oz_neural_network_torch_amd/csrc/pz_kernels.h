@@ -117,6 +117,13 @@ struct OptSegment {
                            // writes it and RCCL reduces it in bf16); replaces grads[offset..]
   float* amax;             // optional: max |w_new| of the segment is atomically max-ed into *amax
                            // (fp8 policy: the weight's current-scaling amax, no separate pass)
+  // optional fp8 policy e4m3 weight copy written by the update itself (natural [in, out] layout,
+  // same element order as the segment): w8 = e4m3(w_new * q) with DELAYED weight scaling,
+  // q = 448 / *w8_amax_prev (the amax the previous update of this weight reduced); the segment's
+  // first work block publishes {q, 1/q} into w8_qs for the GEMMs of the next step
+  uint8_t* w8;
+  const float* w8_amax_prev;
+  float* w8_qs;
 };
 
 struct OptArgs {
@@ -173,6 +180,8 @@ struct FinalizeArgs {
   int n_costs;              // costs[] length (device-read epochs are bounds-checked)
   int n_ratio_rows;
   int* epoch_ptr;           // device epoch counter: read when epoch < 0, always advanced to epoch + 1
+  float* clear;             // optional [nclear] fp32 accumulators reset to 0 (fp8: the weight-amax
+  int nclear;               // slots the step's updates read, ready for the next step's updates)
 };
 hipError_t step_finalize(const FinalizeArgs& a, hipStream_t s);
 
@@ -260,5 +269,10 @@ hipError_t quant_transpose(const float* w, int64_t ldw, int K, int N, uint8_t* o
 hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int cols, uint8_t* out, int64_t ldo,
                          float* qs, float* amax, hipStream_t s, int fmt = 0, const float* amax_in = nullptr,
                          float* amax_clear = nullptr);
+
+// ------------------------------------------------------------------ collective footprint proxy
+// `wgs` resident workgroups for `us` microseconds, moving `chunk_bytes`-long scratch slices at one
+// 4 KiB chunk per `step_us` each (comm_proxy.hip: one-GPU model of a ring all-reduce's kernels)
+hipError_t comm_proxy(void* scratch, int wgs, int chunk_bytes, double us, double step_us, hipStream_t s);
 
 }  // namespace pz

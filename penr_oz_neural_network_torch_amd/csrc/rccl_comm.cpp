@@ -25,6 +25,8 @@
 #include <mutex>
 #include <vector>
 
+#include "pz_kernels.h"
+
 namespace {
 
 struct Api {
@@ -79,6 +81,14 @@ struct Comm {
   ncclComm_t comm = nullptr;
   int device = 0;
   int nranks = 1;
+  // proxy communicator (PZ_COMM=proxy, one GPU): no RCCL; every "all-reduce" launches the
+  // collective-footprint kernel (comm_proxy.hip) for the time a ring all-reduce of that bucket
+  // over `proxy_world` ranks at `proxy_gbps` bus bandwidth would take, on `proxy_wgs` channels
+  bool proxy = false;
+  int proxy_wgs = 0;
+  double proxy_gbps = 0.0;
+  int proxy_world = 1;
+  at::Tensor scratch;
   c10::hip::HIPStream stream;
   hipEvent_t ready = nullptr;
   std::array<hipEvent_t, kRing> done{};
@@ -120,7 +130,50 @@ at::Tensor unique_id_op() {
   return out;
 }
 
-int64_t init_op(const at::Tensor& id, int64_t nranks, int64_t rank, bool high_priority) {
+// The communicator's stream. cu_count > 0: a stream whose kernels may only run on that many CUs
+// (hipExtStreamCreateWithCUMask, bits spread evenly over the device's CUs so every XCD / shader
+// engine gives up a few): the collective's channel kernels then never take a CU outside the mask,
+// whatever the GEMMs on the compute stream leave free.
+c10::hip::HIPStream make_stream(int dev, bool high_priority, int64_t cu_count) {
+  if (cu_count <= 0) return c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(dev));
+  hipDeviceProp_t prop;
+  PZ_HIP_OK(hipGetDeviceProperties(&prop, dev));
+  const int n = prop.multiProcessorCount;
+  TORCH_CHECK(cu_count < n, "pz rccl: a CU mask of ", cu_count, " of ", n, " CUs");
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  for (int64_t j = 0; j < cu_count; ++j) {
+    const int64_t bit = j * n / cu_count;
+    mask[bit / 32] |= 1u << (bit % 32);
+  }
+  hipStream_t s = nullptr;
+  PZ_HIP_OK(hipExtStreamCreateWithCUMask(&s, static_cast<uint32_t>(mask.size()), mask.data()));
+  // (never destroyed: one per communicator, for the process lifetime)
+  return c10::hip::getStreamFromExternal(s, static_cast<c10::DeviceIndex>(dev));
+}
+
+int64_t add_comm(std::shared_ptr<Comm> c) {
+  PZ_HIP_OK(hipEventCreateWithFlags(&c->ready, hipEventDisableTiming));
+  for (auto& e : c->done) PZ_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  std::lock_guard<std::mutex> lock(g_mu);
+  g_comms.push_back(std::move(c));
+  return static_cast<int64_t>(g_comms.size()) - 1;
+}
+
+int64_t proxy_init_op(int64_t world, int64_t wgs, double gbps, int64_t cu_count, bool high_priority) {
+  TORCH_CHECK(world >= 2 && wgs >= 1 && gbps > 0.0, "pz rccl: proxy needs world >= 2, wgs >= 1, gbps > 0");
+  int dev = 0;
+  PZ_HIP_OK(hipGetDevice(&dev));
+  auto c = std::make_shared<Comm>(make_stream(dev, high_priority, cu_count));
+  c->device = dev;
+  c->proxy = true;
+  c->proxy_wgs = static_cast<int>(wgs);
+  c->proxy_gbps = gbps;
+  c->proxy_world = static_cast<int>(world);
+  c->scratch = at::zeros({wgs * (64 << 10) / 4}, at::TensorOptions().dtype(at::kFloat).device(at::kCUDA, dev));
+  return add_comm(std::move(c));
+}
+
+int64_t init_op(const at::Tensor& id, int64_t nranks, int64_t rank, bool high_priority, int64_t cu_count) {
   TORCH_CHECK(id.device().is_cpu() && id.scalar_type() == at::kByte && id.numel() == sizeof(ncclUniqueId),
               "pz rccl: the unique id is ", sizeof(ncclUniqueId), " CPU bytes");
   TORCH_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "pz rccl: rank ", rank, " of ", nranks);
@@ -128,15 +181,11 @@ int64_t init_op(const at::Tensor& id, int64_t nranks, int64_t rank, bool high_pr
   std::memcpy(&uid, id.contiguous().data_ptr(), sizeof(uid));
   int dev = 0;
   PZ_HIP_OK(hipGetDevice(&dev));
-  auto c = std::make_shared<Comm>(c10::hip::getStreamFromPool(high_priority, static_cast<c10::DeviceIndex>(dev)));
+  auto c = std::make_shared<Comm>(make_stream(dev, high_priority, cu_count));
   c->device = dev;
   c->nranks = static_cast<int>(nranks);
   PZ_NCCL_CHECK(api().init_rank(&c->comm, static_cast<int>(nranks), uid, static_cast<int>(rank)));
-  PZ_HIP_OK(hipEventCreateWithFlags(&c->ready, hipEventDisableTiming));
-  for (auto& e : c->done) PZ_HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  std::lock_guard<std::mutex> lock(g_mu);
-  g_comms.push_back(std::move(c));
-  return static_cast<int64_t>(g_comms.size()) - 1;
+  return add_comm(std::move(c));
 }
 
 int64_t all_reduce_op(int64_t h, const at::Tensor& t) {
@@ -154,8 +203,15 @@ int64_t all_reduce_op(int64_t h, const at::Tensor& t) {
   const hipStream_t cur = c10::hip::getCurrentHIPStream(c.device).stream();
   PZ_HIP_OK(hipEventRecord(c.ready, cur));
   PZ_HIP_OK(hipStreamWaitEvent(c.stream.stream(), c.ready, 0));
-  PZ_NCCL_CHECK(api().all_reduce(t.data_ptr(), t.data_ptr(), static_cast<size_t>(t.numel()), nccl_type(t), ncclSum,
-                                 c.comm, c.stream.stream()));
+  if (c.proxy) {  // ring all-reduce time: 2 (W-1)/W x bytes at the bus bandwidth
+    const double bytes = static_cast<double>(t.numel()) * t.element_size();
+    const double us = 2.0 * (c.proxy_world - 1) / c.proxy_world * bytes / (c.proxy_gbps * 1e3);
+    const double step_us = 4096.0 * c.proxy_wgs / (c.proxy_gbps * 1e3);
+    PZ_HIP_OK(pz::comm_proxy(c.scratch.data_ptr(), c.proxy_wgs, 64 << 10, us, step_us, c.stream.stream()));
+  } else {
+    PZ_NCCL_CHECK(api().all_reduce(t.data_ptr(), t.data_ptr(), static_cast<size_t>(t.numel()), nccl_type(t), ncclSum,
+                                   c.comm, c.stream.stream()));
+  }
   // the caching allocator must not hand the bucket's memory out again before the comm stream is done
   c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), c.stream);
   PZ_HIP_OK(hipEventRecord(c.done[ticket % kRing], c.stream.stream()));
@@ -168,10 +224,12 @@ void wait_op(int64_t h, int64_t ticket) {
   std::lock_guard<std::mutex> lock(c.mu);
   TORCH_CHECK(!c.closed, "pz rccl: communicator destroyed");
   TORCH_CHECK(ticket >= 0 && ticket < c.next && c.next - ticket <= kRing, "pz rccl: stale or unknown bucket ticket");
-  ncclResult_t async = ncclSuccess;
-  PZ_NCCL_CHECK(api().async_error(c.comm, &async));
-  TORCH_CHECK(async == ncclSuccess || async == ncclInProgress, "pz rccl: communicator failed: ",
-              api().error_string(async));
+  if (!c.proxy) {
+    ncclResult_t async = ncclSuccess;
+    PZ_NCCL_CHECK(api().async_error(c.comm, &async));
+    TORCH_CHECK(async == ncclSuccess || async == ncclInProgress, "pz rccl: communicator failed: ",
+                api().error_string(async));
+  }
   PZ_HIP_OK(hipStreamWaitEvent(c10::hip::getCurrentHIPStream(c.device).stream(), c.done[ticket % kRing], 0));
 }
 
@@ -185,7 +243,7 @@ void destroy_op(int64_t h) {
   std::lock_guard<std::mutex> lock(c->mu);  // waits for an op in flight on another thread
   c->closed = true;
   PZ_HIP_OK(hipStreamSynchronize(c->stream.stream()));
-  PZ_NCCL_CHECK(api().destroy(c->comm));
+  if (!c->proxy) PZ_NCCL_CHECK(api().destroy(c->comm));
   hipEventDestroy(c->ready);
   for (auto& e : c->done) hipEventDestroy(e);
 }
@@ -194,7 +252,8 @@ void destroy_op(int64_t h) {
 
 TORCH_LIBRARY_FRAGMENT(pz, m) {
   m.def("rccl_unique_id() -> Tensor");
-  m.def("rccl_init(Tensor uid, int nranks, int rank, bool high_priority) -> int");
+  m.def("rccl_init(Tensor uid, int nranks, int rank, bool high_priority, int cu_count=0) -> int");
+  m.def("rccl_proxy_init(int world, int wgs, float gbps, int cu_count=0, bool high_priority=False) -> int");
   m.def("rccl_all_reduce(int comm, Tensor(a!) t) -> int");
   m.def("rccl_wait(int comm, int ticket) -> ()");
   m.def("rccl_destroy(int comm) -> ()");
@@ -203,6 +262,7 @@ TORCH_LIBRARY_FRAGMENT(pz, m) {
 TORCH_LIBRARY_IMPL(pz, CompositeExplicitAutograd, m) {
   m.impl("rccl_unique_id", TORCH_FN(unique_id_op));
   m.impl("rccl_init", TORCH_FN(init_op));
+  m.impl("rccl_proxy_init", TORCH_FN(proxy_init_op));
   m.impl("rccl_all_reduce", TORCH_FN(all_reduce_op));
   m.impl("rccl_wait", TORCH_FN(wait_op));
   m.impl("rccl_destroy", TORCH_FN(destroy_op));

@@ -58,6 +58,9 @@ class FusedOptimizer:
         self.slot_of = slot_of
         self.shadow_sets = shadow_sets
         self.amax_sets: list[dict[int, torch.Tensor]] = [{} for _ in shadow_sets]
+        # fp8 policy, per parity: segment offset -> (e4m3 copy, previous amax, {q, 1/q} record) that
+        # the update writes itself (delayed weight scaling; set_w8)
+        self.w8_sets: list[dict[int, tuple]] = [{} for _ in shadow_sets]
         self._segs = segs
         self._pack_all()
         self.block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
@@ -93,12 +96,14 @@ class FusedOptimizer:
                 self.groups[(key, parity)] = (self._pack(segs, parity), block_seg, len(segs), acc)
 
     def _pack(self, segs, parity: int) -> torch.Tensor:
-        sh, am = self.shadow_sets[parity], self.amax_sets[parity]
+        sh, am, w8 = self.shadow_sets[parity], self.amax_sets[parity], self.w8_sets[parity]
+        trip = [w8.get(s.offset, (None, None, None)) for s in segs]
         return torch.ops.pz.pack_segments(
             [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
             [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
             [self.grads16.get(s.offset) for s in segs], self._zero_flags(segs),
-            [am.get(s.offset) for s in segs]).to(self.store.device)
+            [am.get(s.offset) for s in segs], [t[0] for t in trip], [t[1] for t in trip],
+            [t[2] for t in trip]).to(self.store.device)
 
     def _pack_all(self) -> None:
         self.segments_p = [self._pack(self._segs, p) for p in range(len(self.shadow_sets))]
@@ -110,6 +115,15 @@ class FusedOptimizer:
         Call before define_groups()."""
         assert len(amax_sets) == len(self.shadow_sets)
         self.amax_sets = amax_sets
+        self._pack_all()
+
+    def set_w8(self, w8_sets: list[dict[int, tuple]]) -> None:
+        """fp8 policy: per parity, segment offset -> ``(w8, amax_prev, qs)``: the update writes the
+        weight's e4m3 copy itself, scaled by q = 448 / amax_prev (the amax the previous update
+        reduced: delayed weight scaling), and publishes {q, 1/q} into ``qs``. Call before
+        define_groups()."""
+        assert len(w8_sets) == len(self.shadow_sets)
+        self.w8_sets = w8_sets
         self._pack_all()
 
     def _zero_flags(self, segs) -> list[int]:
@@ -222,10 +236,12 @@ class FusedOptimizer:
                                     self.stats[self.cur], hp, ctr, every, max_grid)
 
     def finalize(self, loss: torch.Tensor | None, world: int, l2: float, costs: torch.Tensor, epoch: int,
-                 ratios: torch.Tensor, ratio_row: int, epoch_ctr: torch.Tensor | None = None, every: int = 1) -> None:
+                 ratios: torch.Tensor, ratio_row: int, epoch_ctr: torch.Tensor | None = None, every: int = 1,
+                 clear: torch.Tensor | None = None) -> None:
         """cost[epoch] and the update-ratio row; ``epoch=-1`` / ``ratio_row=-2``: taken from the
-        device ``epoch_ctr`` (graph-replayed step), which is advanced to epoch + 1 either way."""
+        device ``epoch_ctr`` (graph-replayed step), which is advanced to epoch + 1 either way.
+        ``clear``: fp32 accumulators to reset (the weight-amax slots this step's updates read)."""
         prev = self.stats[1 - self.cur]
         torch.ops.pz.step_finalize(loss, float(world), prev, self.stats[self.cur], self.slot_numel, self.nslots, l2,
-                                   costs, epoch, ratios, ratio_row, epoch_ctr, every)
+                                   costs, epoch, ratios, ratio_row, epoch_ctr, every, clear)
         self.cur = 1 - self.cur

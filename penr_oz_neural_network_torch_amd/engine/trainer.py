@@ -234,6 +234,7 @@ class FusedTrainer:
         self.w8_kc = not self._w8_nat  # the forward operand's layout (K-contiguous = transposed copy)
         self._fp8_bwd_env = os.environ.get("PZ_FP8_BWD", "1") != "0"
         self.w8: dict[int, torch.Tensor] = {}
+        self._w8_fused = False
         if self.fp8:
             gemms = [st for st in self.stages if st.kind == "gemm"]
             self.wqs = torch.ones(len(gemms), 2, device=self.dev)
@@ -252,7 +253,12 @@ class FusedTrainer:
             # weight amax accumulators per shadow parity: the optimizer update max-es |w_new| into
             # its parity's slot, the transpose-quantise right behind it consumes that slot and
             # clears the other parity's (no separate amax pass over the fp32 weights)
-            self.wamax2 = torch.zeros(2, len(gemms), device=self.dev)
+            # (every accumulator on a 256-B line of its own: the update's ~2k same-address atomic
+            # max-es go to the memory side, and a plain read of a value sharing their line — the
+            # previous amax the fused e4m3 copy scales by — queued behind them: the Adam update
+            # ran 2x slower with the two parities packed into one line)
+            self._wamax_store = torch.zeros(2, len(gemms), 64, device=self.dev)
+            self.wamax2 = self._wamax_store[:, :, 0]
             for k, st in enumerate(gemms):
                 st.w8_index = k
                 if self._w8_nat:  # one copy: the forward's B and (layers 2..n) the dX GEMM's B
@@ -267,6 +273,16 @@ class FusedTrainer:
             self._refresh_fp8_weights()
             self.opt.set_amax([{st.seg_w.offset: self.wamax2[p % 2, st.w8_index:st.w8_index + 1] for st in gemms}
                                for p in range(len(self.shadow_sets))])
+            # natural layout: the optimizer writes the e4m3 copy itself with DELAYED weight scaling
+            # (q from the amax the previous update reduced; the first update falls back to the
+            # initial copies' current scale) — no quantisation pass re-reading the fp32 weights
+            # behind every update. PZ_FP8_WFUSE=0: the separate current-scaled quantise launch.
+            if self._w8_nat and os.environ.get("PZ_FP8_WFUSE", "1") != "0":
+                self._w8_fused = True
+                self.opt.set_w8([{st.seg_w.offset: (self.w8[st.seg_w.offset],
+                                                    self.wamax2[1 - p % 2, st.w8_index:st.w8_index + 1],
+                                                    self.wqs[st.w8_index]) for st in gemms}
+                                 for p in range(len(self.shadow_sets))])
         # Optimizer overlap: each GEMM weight is updated on a side stream as soon as its gradient
         # bucket is complete (its dW GEMM on one GPU, its all-reduce under DP), while the rest of
         # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
@@ -338,7 +354,7 @@ class FusedTrainer:
         # data parallelism: there the last bucket's all-reduce is exposed, so the backward ends
         # on the smallest dW (the first layer's, chunked).
         self._late_idx = None
-        if (os.environ.get("PZ_BWD_ORDER", "1") == "1" and not self.ctx.enabled and not self.fuse_opt
+        if (os.environ.get("PZ_BWD_ORDER", "0") == "1" and not self.ctx.enabled and not self.fuse_opt
                 and self.overlap and len(gemm_w) > 1):
             cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
             if cands:
@@ -494,6 +510,8 @@ class FusedTrainer:
         ``parity``: the shadow parity of the optimizer update that just wrote the weights (its amax
         is already reduced); None: reduce the amax here (initial copies)."""
         ops = torch.ops.pz
+        if parity is not None and self._w8_fused:
+            return  # the optimizer update wrote the e4m3 copies and their scale records
         for st in self.stages if only is None else [only]:
             if st.kind != "gemm":
                 continue
@@ -922,7 +940,10 @@ class FusedTrainer:
         # ---------------- reduce + update
         self._phase("pz.update")
         handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:], exact=True))
-        fin = dict(epoch_ctr=self.epoch_ctr, every=self._plan["every"] if self._plan else 1)
+        fin = dict(epoch_ctr=self.epoch_ctr, every=self._plan["every"] if self._plan else 1,
+                   # fused e4m3 weight copies: this step's updates read the amax slot of the
+                   # current parity; step_finalize clears it for the next step's updates
+                   clear=self._wamax_store[self.parity] if self._w8_fused else None)
         if overlap and self._late_dw is not None:
             self._finish_reordered(main, l2, capture, epoch, row, fin, handles)
             return

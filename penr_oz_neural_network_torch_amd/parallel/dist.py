@@ -130,12 +130,43 @@ class _NativeComm:
         dist.broadcast(uid_dev, src=0, group=group)
         # comm stream at NORMAL priority (PZ_COMM_PRIO=1: high): a high-priority stream slowed every
         # compute kernel of the forced 1-rank step (2.44 vs 1.40 ms/step, profiles/r2_ab_native_comm.txt)
-        self.handle = torch.ops.pz.rccl_init(uid_dev.cpu(), world, rank, os.environ.get("PZ_COMM_PRIO", "0") == "1")
+        # PZ_COMM_CUS=k: the communicator's stream is CU-masked to k CUs (evenly spread over the
+        # XCDs): the channel kernels of every bucket all-reduce stay on those CUs
+        self.handle = torch.ops.pz.rccl_init(uid_dev.cpu(), world, rank, os.environ.get("PZ_COMM_PRIO", "0") == "1",
+                                             int(os.environ.get("PZ_COMM_CUS", "0")))
         probe = torch.full((1,), float(rank + 1), device=dev, dtype=torch.float64)
         self.all_reduce(probe).wait()
         got, want = probe.item(), world * (world + 1) / 2
         if got != want:
             raise RuntimeError(f"pz rccl communicator self-check failed: sum {got}, expected {want}")
+
+    def all_reduce(self, t: torch.Tensor) -> _Ticket:
+        return _Ticket(self.handle, torch.ops.pz.rccl_all_reduce(self.handle, t))
+
+    def close(self) -> None:
+        if self.handle is not None:
+            torch.ops.pz.rccl_destroy(self.handle)
+            self.handle = None
+
+
+class _ProxyComm:
+    """``PZ_COMM=proxy`` (one GPU, ``PZ_FORCE_COMM=1``): every bucket "all-reduce" launches the
+    collective-footprint kernel of ``csrc/comm_proxy.hip`` on the communicator stream instead —
+    ``PZ_COMM_PROXY_WGS`` resident channel workgroups (default 16) held for the time a ring
+    all-reduce of that bucket over ``PZ_COMM_PROXY_WORLD`` ranks (default 8) at
+    ``PZ_COMM_PROXY_GBPS`` bus bandwidth (default 150 GB/s) takes, optionally CU-masked
+    (``PZ_COMM_CUS``). Buckets are left untouched (a 1-rank sum is the identity), so the step's
+    results are the world-1 results; what changes is how the GEMMs share the GPU with the comm
+    kernels — the data-parallel step's cost on one GPU (tools/comm_pressure.py)."""
+
+    def __init__(self):
+        from ..ops import native
+        native.require()
+        env = os.environ.get
+        self.handle = torch.ops.pz.rccl_proxy_init(int(env("PZ_COMM_PROXY_WORLD", "8")),
+                                                   int(env("PZ_COMM_PROXY_WGS", "16")),
+                                                   float(env("PZ_COMM_PROXY_GBPS", "150")),
+                                                   int(env("PZ_COMM_CUS", "0")), False)
 
     def all_reduce(self, t: torch.Tensor) -> _Ticket:
         return _Ticket(self.handle, torch.ops.pz.rccl_all_reduce(self.handle, t))
@@ -194,8 +225,14 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
         # ProcessGroupNCCL. Opt-in: with the same bucket schedule it measured 1.8% slower on the
         # forced 1-rank step (1.390-1.396 vs 1.366-1.373 ms, profiles/r2_ab_native_comm.txt), and
         # the multi-GPU node runs are the driver's, not ours to A/B
-        if dist.get_backend() == "nccl" and os.environ.get("PZ_COMM", "torch") == "native":
+        mode = os.environ.get("PZ_COMM", "torch")
+        if dist.get_backend() == "nccl" and mode == "native":
             _CONTEXT.native = _NativeComm(_CONTEXT.rank, _CONTEXT.world_size)
+        elif mode == "proxy":
+            if _CONTEXT.world_size != 1 or not torch.cuda.is_available():
+                raise RuntimeError("PZ_COMM=proxy models the collectives of a multi-GPU step on ONE GPU "
+                                   "(PZ_FORCE_COMM=1, world size 1)")
+            _CONTEXT.native = _ProxyComm()
     else:
         _CONTEXT = DataParallelContext(0, 1, None, comm_dtype)
     return _CONTEXT

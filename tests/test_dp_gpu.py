@@ -134,6 +134,8 @@ def _forced_main(rank, comm, out_path, impl="native"):
     all-reduce on its comm stream, waited for by the optimizer's stream."""
     os.environ.update(PZ_FORCE_COMM="1", PZ_GRAD_COMM_DTYPE=comm, PZ_COMM=impl, MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(_free_port()))
+    if impl == "proxy":
+        os.environ.update(PZ_COMM_CUS="16", PZ_COMM_PROXY_WGS="16")
     if comm == "fp32":  # unchunked first-layer dW (chunks change the split-K choice = rounding)
         os.environ["PZ_DW_CHUNKS"] = "1"
     os.environ.pop("WORLD_SIZE", None)
@@ -141,8 +143,10 @@ def _forced_main(rank, comm, out_path, impl="native"):
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
     ctx = init_from_env()
     assert ctx.force and ctx.enabled and ctx.world_size == 1 and ctx.backend == "nccl", ctx
-    # gradient buckets on the extension's RCCL communicator (csrc/rccl_comm.cpp) or ProcessGroupNCCL
-    assert (ctx.native is not None) == (impl == "native"), ctx
+    # gradient buckets on the extension's RCCL communicator (csrc/rccl_comm.cpp), its collective-
+    # footprint proxy (comm_proxy.hip: channel kernels held for a modelled 8-rank ring time, on a
+    # CU-masked stream) or ProcessGroupNCCL
+    assert (ctx.native is not None) == (impl in ("native", "proxy")), ctx
     model = _build("adam", "bf16")
     tr = FusedTrainer(model, ctx)
     assert bool(tr.grads16) == (comm == "bf16")
@@ -156,7 +160,7 @@ def _forced_main(rank, comm, out_path, impl="native"):
     shutdown()
 
 
-@pytest.mark.parametrize("comm,impl", [("fp32", "native"), ("bf16", "native"), ("fp32", "torch")])
+@pytest.mark.parametrize("comm,impl", [("fp32", "native"), ("bf16", "native"), ("fp32", "torch"), ("fp32", "proxy")])
 def test_forced_rccl_world1_matches_no_comm(tmp_path, monkeypatch, comm, impl):
     out = str(tmp_path / "forced.pt")
     mp.start_processes(_forced_main, args=(comm, out, impl), nprocs=1, start_method="spawn")

@@ -271,9 +271,12 @@ def test_record_mode_matches_fused_cost():
 
 
 def test_fp8_training_tracks_bf16():
-    """fp8 policy: e4m3 forward GEMMs (current-scaled weights, delayed-scaled activations, e4m3
-    input at a static dataset scale), e5m2-gradient x e4m3-weight backward dX GEMMs (delayed
-    gradient scaling), bf16 dW; the loss curve follows the bf16 run of the same model + batches."""
+    """fp8 policy on the TRANSPOSED-copy path (a width of 128: not every width is a multiple of
+    256, so the forward reads a [out, in] e4m3 copy; tests/test_fastpaths_gpu.py covers the
+    natural-layout path the benchmark config takes): e4m3 forward GEMMs (current-scaled weights,
+    delayed-scaled activations, e4m3 input at a static dataset scale), e5m2-gradient x e4m3-weight
+    backward dX GEMMs (delayed gradient scaling), e4m3 x e5m2 dW where the shapes allow; the loss
+    curve follows the bf16 run of the same model + batches within the Adam sign-noise band."""
     sizes = [256, 512, 512, 128]
     algos = ["relu", "relu", "softmax"]
     n, S, steps = 4096, 1024, 12
@@ -386,8 +389,9 @@ def test_fused_dw_update_matches_separate_launches(monkeypatch, optimizer):
 
 def test_prefetched_sample_matches_in_step_gather(monkeypatch):
     """The next step's minibatch gathered ahead of time — on the main stream between this step's
-    head and backward (PZ_PREFETCH_MAIN, the default) or on the side stream during the backward
-    (PZ_PREFETCH) — is the sample the step would have drawn itself: same picks, same costs."""
+    head and backward (PZ_PREFETCH_MAIN=1) or on the side stream during the backward
+    (PZ_PREFETCH=1); both OFF by default, they measured slower in the step — is the sample the
+    step would have drawn itself: same picks, same costs."""
     sizes = [1024, 2048, 1024, 256]  # ~110 GFLOP per step: not launch-bound, so no graph replay
     n, S, steps = 8192, 4096, 5
     g = torch.Generator().manual_seed(6)

@@ -43,10 +43,13 @@ def _close_fp8(got: torch.Tensor, ref: torch.Tensor) -> None:
     assert torch.all((g - r).abs() <= r.abs() * 0.125 + 2 ** -9)
 
 
-@pytest.mark.parametrize("fp8_bwd", ["1", "0"])
-def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd):
-    """BASELINE config 5 shape family at reduced size: [1024, 2048, 1024], batch 1024."""
+@pytest.mark.parametrize("fp8_bwd,wfuse", [("1", "1"), ("0", "1"), ("1", "0")])
+def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd, wfuse):
+    """BASELINE config 5 shape family at reduced size: [1024, 2048, 1024], batch 1024. wfuse: the
+    optimizer writes the e4m3 weight copies itself (delayed weight scaling, the default) or a
+    separate current-scaled quantisation launch follows each update (PZ_FP8_WFUSE=0)."""
     monkeypatch.setenv("PZ_FP8_BWD", fp8_bwd)
+    monkeypatch.setenv("PZ_FP8_WFUSE", wfuse)
     sizes = [1024, 2048, 1024]
     algos = ["relu", "softmax"]
     n, S, steps = 8192, 1024, 12
@@ -78,11 +81,18 @@ def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd):
         assert tr.stages[0].g8_from_epi and 0 in tr._g8_epi_ready
         assert tr._fp8_dw_ready_cached(tr.stages[0])
         torch.cuda.synchronize()
+        assert tr._w8_fused == (wfuse == "1")
         gemms = [st for st in tr.stages if st.kind == "gemm"]
+        amax = torch.stack([tr.store.view(st.seg_w).abs().max() for st in gemms]).cpu()
+        rows = tr.wamax2.cpu()  # the last update's amax slot holds max|w|, the other was cleared
+        assert (rows == 0).all(dim=1).sum() == 1, rows
+        assert torch.equal(rows.max(dim=0).values, amax), (rows, amax)
         for st in gemms:
             w = tr.store.view(st.seg_w)
             q = tr.wqs[st.w8_index, 0].item()
-            assert math.isclose(q, 448.0 / w.abs().max().item(), rel_tol=1e-6)
+            # current scaling: q from this amax; delayed: from the previous update's (a step of
+            # Adam moves max|w| by ~lr)
+            assert math.isclose(q, 448.0 / w.abs().max().item(), rel_tol=1e-6 if wfuse == "0" else 0.05)
             assert math.isclose(tr.wqs[st.w8_index, 1].item(), 1.0 / q, rel_tol=1e-6)
             w8 = tr.w8[st.seg_w.offset]
             assert w8.shape == w.shape and w8 is tr.w8n[st.seg_w.offset]  # natural [in, out], one copy
@@ -104,8 +114,50 @@ def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd):
     bf, f8 = curves["bfloat16"], curves["fp8"]
     assert all(math.isfinite(c) for c in f8)
     assert f8[-1] < f8[0] - 0.05, f8  # it learns
+    # Adam's first steps move every weight by ~lr * sign(g): the gradient quantisation noise of
+    # e5m2 dZ (2 mantissa bits) flips signs of small gradients and the early trajectories wander
+    # apart by a few percent (in either direction); the SGD test below pins the gradients tightly
     for a, b in zip(bf, f8):
-        assert abs(a - b) < 0.02 * abs(a) + 0.01, (bf, f8)
+        assert abs(a - b) < 0.05 * abs(a) + 0.02, (bf, f8)
+
+
+def test_fp8_natural_layout_gradients_and_sgd_curve():
+    """The fp8 policy's gradients on the natural-layout path against the bf16 policy's, from the
+    same weights and batches: per-layer weight-gradient relative error (one SGD step: delta =
+    -lr * grad) within fp8 quantisation noise, and the SGD loss curve within 2 % + 0.01."""
+    sizes = [1024, 2048, 1024]
+    n, S, steps, lr = 8192, 1024, 12, 0.05
+    g = torch.Generator().manual_seed(31)
+    inputs = torch.randn(n, sizes[0], generator=g)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    idx = torch.randint(0, n, (steps, S), generator=g)
+    runs = {}
+    for dtype in ("bfloat16", "fp8"):
+        torch.manual_seed(0)
+        model = NeuralNetworkModel("f8g", sizes, "xavier", "random", ["relu", "softmax"], "stochastic", dtype=dtype,
+                                   device="cuda")
+        tr = FusedTrainer(model)
+        tr.load_tensors(inputs, labels, seed=9)
+        tr.begin(steps)
+        deltas = []
+        for e in range(steps):
+            before = [p.detach().float().clone() for p in model.params[0::2]]
+            tr.step(e, lr, S, 0.0, 0.0, want_ratios=False, record=False, indices=idx[e])
+            if e in (1, 2):  # step 0 calibrates the delayed scales on its own amax
+                torch.cuda.synchronize()
+                deltas.append([p.detach().float() - b for p, b in zip(model.params[0::2], before)])
+        runs[dtype] = ([c for _, c, _, _ in tr.drain()], deltas)
+        if dtype == "fp8":
+            assert tr._w8_nat and [st.fp8 for st in tr.stages] == [True, True]
+            assert tr._fp8_dw_ready_cached(tr.stages[0]) and tr._fp8_dw_ready_cached(tr.stages[1])
+    (cb, db), (c8, d8) = runs["bfloat16"], runs["fp8"]
+    for step_b, step_8 in zip(db, d8):
+        for k, (a, b) in enumerate(zip(step_b, step_8)):
+            rel = ((a - b).norm() / a.norm()).item()
+            assert rel < 0.08, (k, rel)  # e4m3 forward, e5m2 x e4m3 dX, e4m3 x e5m2 dW
+    assert c8[-1] < c8[0] - 0.05, c8
+    for a, b in zip(cb, c8):
+        assert abs(a - b) < 0.02 * abs(a) + 0.01, (cb, c8)
 
 
 @pytest.mark.parametrize("optimizer", ["stochastic", "adam"])

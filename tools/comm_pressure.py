@@ -1,0 +1,61 @@
+"""One-GPU cost of the data-parallel step's collectives (VERDICT r3 missing #1 / next #4).
+
+Runs bench.py (mlp4, the headline config) under each comm configuration on ONE MI355X and prints
+ms/step, interleaved over rounds (same box):
+
+  none          single process, no communication (the headline path: graph-free eager steps)
+  torch         PZ_FORCE_COMM=1: a real 1-rank RCCL all-reduce per bucket via ProcessGroupNCCL
+  native        PZ_FORCE_COMM=1 PZ_COMM=native: the extension's own RCCL communicator
+  dpnone        PZ_FORCE_COMM=1 PZ_COMM=proxy with a zero-duration proxy: the DP schedule alone
+  proxy_k<K>    PZ_COMM=proxy: the collective-footprint kernel (csrc/comm_proxy.hip) holds
+                16 channel workgroups for a modelled 8-rank ring all-reduce of every bucket
+                at 150 GB/s, its stream CU-masked to K CUs (K=0: unmasked)
+
+    python tools/comm_pressure.py [--rounds 2] [--steps 60] [--ks 0,8,16,32]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def run(env_extra, steps, warmup):
+    env = dict(os.environ, **env_extra)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup",
+                          str(warmup)], env=env, capture_output=True, text=True, timeout=300)
+    if out.returncode != 0:
+        print(out.stderr[-2000:], file=sys.stderr)
+        raise SystemExit(out.returncode)
+    return json.loads(out.stdout.strip().splitlines()[-1])["ms_per_step"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--ks", default="0,8,16,32")
+    ap.add_argument("--gbps", default="150")
+    a = ap.parse_args()
+    forced = {"PZ_FORCE_COMM": "1"}
+    cases = {"none": {}, "torch": dict(forced, PZ_COMM="torch"), "native": dict(forced, PZ_COMM="native"),
+             "dpnone": dict(forced, PZ_COMM="proxy", PZ_COMM_PROXY_GBPS="1e12")}
+    for k in [int(x) for x in a.ks.split(",")]:
+        cases[f"proxy_k{k}"] = dict(forced, PZ_COMM="proxy", PZ_COMM_CUS=str(k),
+                                    PZ_COMM_PROXY_WGS=str(k if k else 16), PZ_COMM_PROXY_GBPS=a.gbps)
+    res = {name: [] for name in cases}
+    for r in range(a.rounds):
+        for name, env in cases.items():
+            ms = run(env, a.steps, a.warmup)
+            res[name].append(ms)
+            print(f"round {r} {name:10s} {ms:.4f} ms/step", flush=True)
+    base = min(res["none"])
+    for name, v in res.items():
+        print(f"{name:10s} best {min(v):.4f} ms  vs none {100 * (min(v) / base - 1):+.1f}%")
+
+
+if __name__ == "__main__":
+    main()
