@@ -178,7 +178,7 @@ def _native_rank(rank, world, port, out_dir):
             return torch.arange(128, dtype=torch.uint8)
 
         @staticmethod
-        def rccl_init(uid, nranks, r, high_priority):
+        def rccl_init(uid, nranks, r, high_priority, cu_count=0):
             log["init"].append((uid.tolist(), nranks, r, high_priority))
             return 7
 
