@@ -340,6 +340,45 @@ void gemm_update_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, cons
   PZ_HIP_CHECK(pz::gemm(p, cur_stream(A)));
 }
 
+// two weight-gradient GEMMs C0 = op(A0)·op(B0), C1 = op(A1)·op(B1) (A, B M/N-contiguous, plain
+// stores, one K) in ONE launch (pz::gemm_pair); fp8 operands take their dequantisation scalars
+pz::GemmArgs pair_args(const Tensor& A, const Tensor& B, const Tensor& C, int64_t M, int64_t N, int64_t K,
+                       const optional<Tensor>& scale_a, const optional<Tensor>& scale_b) {
+  auto p = gemm_args(A, false, B, false, C, c10::nullopt, c10::nullopt, c10::nullopt, 0, {}, {}, 1.0, false, M, N, K,
+                     0, false);
+  p.scale_a = f32_scalar_ptr(scale_a, "scale_a");
+  p.scale_b = f32_scalar_ptr(scale_b, "scale_b");
+  return p;
+}
+
+int64_t gemm_pair_split_op(const Tensor& A0, const Tensor& B0, const Tensor& C0, const Tensor& A1, const Tensor& B1,
+                           const Tensor& C1, int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
+  return pz::gemm_pair_split(pair_args(A0, B0, C0, M0, N0, K, c10::nullopt, c10::nullopt),
+                             pair_args(A1, B1, C1, M1, N1, K, c10::nullopt, c10::nullopt));
+}
+
+void gemm_pair_op(const Tensor& A0, const Tensor& B0, const Tensor& C0, const Tensor& A1, const Tensor& B1,
+                  const Tensor& C1, int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K,
+                  const optional<Tensor>& scale_a0, const optional<Tensor>& scale_b0,
+                  const optional<Tensor>& scale_a1, const optional<Tensor>& scale_b1) {
+  check_dev(A0, "A0");
+  auto a = pair_args(A0, B0, C0, M0, N0, K, scale_a0, scale_b0);
+  auto b = pair_args(A1, B1, C1, M1, N1, K, scale_a1, scale_b1);
+  const int split = pz::gemm_pair_split(a, b);
+  TORCH_CHECK(split > 0, "pz::gemm_pair: the two GEMMs cannot share a launch (check gemm_pair_split first)");
+  at::Tensor ws0, ws1;  // split-K slabs, one set per GEMM
+  a.split_k = b.split_k = split;
+  if (split > 1) {
+    ws0 = at::empty({(M0 / 256) * (N0 / 256) * split * 65536}, A0.options().dtype(at::kFloat));
+    ws1 = at::empty({(M1 / 256) * (N1 / 256) * split * 65536}, A0.options().dtype(at::kFloat));
+    a.ws = ws0.data_ptr<float>();
+    b.ws = ws1.data_ptr<float>();
+    a.counters = split_counters(static_cast<int>((M0 / 256) * (N0 / 256)), A0.device());
+    b.counters = split_counters(static_cast<int>((M1 / 256) * (N1 / 256)), A0.device());
+  }
+  PZ_HIP_CHECK(pz::gemm_pair(a, b, cur_stream(A0)));
+}
+
 int64_t gemm_path_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, int64_t M, int64_t N,
                      int64_t K) {
   auto p = gemm_args(A, a_kc, B, b_kc, C, c10::nullopt, c10::nullopt, c10::nullopt, 0, {}, {}, 1.0, false, M, N, K, 0,
@@ -904,6 +943,11 @@ TORCH_LIBRARY(pz, m) {
         "Tensor(f!)? amax, bool adam, float lr, float beta1, float beta2, float eps, float bias_c1, "
         "float bias_c2_sqrt, float grad_scale, float l2, Tensor? hp=None, Tensor? epoch=None, int stats_every=1) -> ()");
   m.def("gemm_path(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor C, int M, int N, int K) -> int");
+  m.def("gemm_pair_split(Tensor A0, Tensor B0, Tensor C0, Tensor A1, Tensor B1, Tensor C1, int M0, int N0, int M1, "
+        "int N1, int K) -> int");
+  m.def("gemm_pair(Tensor A0, Tensor B0, Tensor(a!) C0, Tensor A1, Tensor B1, Tensor(b!) C1, int M0, int N0, int M1, "
+        "int N1, int K, Tensor? scale_a0=None, Tensor? scale_b0=None, Tensor? scale_a1=None, "
+        "Tensor? scale_b1=None) -> ()");
   m.def("stage_fwd(Tensor x, Tensor(a!) y, int[] epi_i, float[] epi_f) -> ()");
   m.def("stage_bwd(Tensor g, Tensor y, Tensor(a!) dx, int[] epi_i, float[] epi_f) -> ()");
   m.def("xent_head(Tensor logits, Tensor labels, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "
@@ -955,6 +999,8 @@ TORCH_LIBRARY(pz, m) {
 TORCH_LIBRARY_IMPL(pz, CUDA, m) {
   m.impl("gemm", TORCH_FN(gemm_op));
   m.impl("gemm_path", TORCH_FN(gemm_path_op));
+  m.impl("gemm_pair_split", TORCH_FN(gemm_pair_split_op));
+  m.impl("gemm_pair", TORCH_FN(gemm_pair_op));
   m.impl("gemm_update", TORCH_FN(gemm_update_op));
   m.impl("stage_fwd", TORCH_FN(stage_fwd_op));
   m.impl("stage_bwd", TORCH_FN(stage_bwd_op));

@@ -381,13 +381,16 @@ PZ_DEV f32x4_t epi_apply(const GemmArgs& p, f32x4_t a, f32x4_t bias4, int m, int
   return f32x4_t{v[0], v[1], v[2], v[3]};
 }
 
-// XCD-aware bijective remap of the launch order (consecutive ids share an XCD's L2), then
-// tile = id / split, slice = id % split (a tile's K slices stay on one XCD), then grouped
-// tile order for L2 reuse.
-PZ_DEV void tile_coords(int nwg, int tiles_m, int tiles_n, int split, int& tm, int& tn, int& tile, int& slice) {
-  const int bid = blockIdx.x;
+// XCD-aware bijective remap of the launch order: consecutive ids share an XCD's L2 (blocks are
+// dealt round-robin over the 8 XCDs; speed only, never correctness)
+PZ_DEV int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// remapped id -> tile = id / split, slice = id % split (a tile's K slices stay on one XCD), then
+// grouped tile order for L2 reuse.
+PZ_DEV void tile_coords(int wgid, int tiles_m, int tiles_n, int split, int& tm, int& tn, int& tile, int& slice) {
   tile = wgid / split;
   slice = wgid - tile * split;
   wgid = tile;
@@ -521,9 +524,9 @@ PZ_DEV void epilogue_opt(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
 }
 
 
+// The body of one workgroup: the GEMM `p`, workgroup `wgid` of its (XCD-remapped) grid
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR, int EK = EK_ANY>
-__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(var_waves_per_eu<VAR>())))
-gemm_mfma_kernel(const GemmArgs p) {
+PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
   static_assert(EK == EK_ANY || std::is_same<OutT, uint16_t>::value, "specialised epilogues: bf16 output");
   PZ_STAMP(0);
   constexpr int BK = var_bk<VAR>();
@@ -536,7 +539,7 @@ gemm_mfma_kernel(const GemmArgs p) {
   const int tiles_n = (p.N + BN - 1) / BN;
   const int split = p.split_k > 1 ? p.split_k : 1;
   int tm, tn, tile_id, slice;
-  tile_coords(tiles_m * tiles_n * split, tiles_m, tiles_n, split, tm, tn, tile_id, slice);
+  tile_coords(wgid, tiles_m, tiles_n, split, tm, tn, tile_id, slice);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1006,6 +1009,30 @@ gemm_mfma_kernel(const GemmArgs p) {
 }
 
 template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR, int EK = EK_ANY>
+__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(var_waves_per_eu<VAR>())))
+gemm_mfma_kernel(const GemmArgs p) {
+  gemm_body<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR, EK>(p, xcd_remap(blockIdx.x, gridDim.x));
+}
+
+// Two independent GEMMs of one layout / epilogue kind in ONE launch (gemm_pair): the first nwg0
+// remapped workgroup ids run GEMM 0, the rest GEMM 1 — e.g. the two skinny weight-gradient GEMMs
+// of a 3-layer MLP (64 tiles each at batch 8192) that alone would each need a 4-way split-K to
+// fill the CUs: together they fill them with a 2-way split (or none), half (or none) of the slab
+// hand-offs, and one launch instead of two
+struct GemmPairArgs {
+  GemmArgs p[2];
+  int nwg0;
+};
+
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR, int EK = EK_ANY>
+__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(var_waves_per_eu<VAR>())))
+gemm_mfma_pair_kernel(const GemmPairArgs g) {
+  const int w = xcd_remap(blockIdx.x, gridDim.x);
+  const int second = w >= g.nwg0 ? 1 : 0;  // workgroup-uniform
+  gemm_body<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR, EK>(g.p[second], w - second * g.nwg0);
+}
+
+template <int BM, int BN, int WM, int WN, bool A_KC, bool B_KC, typename OutT, typename AuxT, int VAR, int EK = EK_ANY>
 hipError_t launch_cfg(const GemmArgs& p, hipStream_t s) {
   using C = Cfg<BM, BN, WM, WN, var_ns<VAR>(), var_bk<VAR>()>;
   auto kern = gemm_mfma_kernel<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR, EK>;
@@ -1217,6 +1244,21 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
              : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
 }
 
+template <typename OutT, int VAR, int EK>
+hipError_t launch_pair_cfg(const GemmPairArgs& g, int nwg, hipStream_t s) {
+  using C = Cfg<256, 256, 2, 4, var_ns<VAR>(), var_bk<VAR>()>;
+  auto kern = gemm_mfma_pair_kernel<256, 256, 2, 4, false, false, OutT, uint16_t, VAR, EK>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, C::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(nwg), dim3(C::NT), C::LDS_BYTES, s, g);
+  return hipGetLastError();
+}
+
 #endif  // PZ_GEMM_LAB
 }  // namespace
 
@@ -1337,6 +1379,44 @@ int64_t gemm_split_ws_floats(const GemmArgs& p) {
   const int sp = gemm_split(p);
   if (sp <= 1) return 0;
   return static_cast<int64_t>((p.M + 255) / 256) * ((p.N + 255) / 256) * sp * 256 * 256;
+}
+
+// gemm_pair: both GEMMs in the weight-gradient layout (A and B M/N-contiguous), plain stores of
+// whole 256 x 256 tiles, one K; returns the split-K factor of the pair, or 0 if it cannot be paired
+int gemm_pair_split(const GemmArgs& a, const GemmArgs& b) {
+  for (const GemmArgs* q : {&a, &b}) {
+    const GemmArgs& p = *q;
+    if (p.a_kc || p.b_kc || p.epi_mode != EPI_STORE || p.accumulate || p.force_generic) return 0;
+    if (p.bias || p.colsum || p.mask || p.out8 || p.aux || p.bias64 || p.colsum64) return 0;
+    if (p.M % 256 || p.N % 256 || p.K % 64 || !mfma_eligible(p)) return 0;
+    if (p.in_dtype != DT_FP8 && (!buffer_ok(p) || epi_kind(p) != (p.out_dtype == DT_BF16 ? EK_STORE : EK_ANY)))
+      return 0;
+  }
+  if (a.K != b.K || a.in_dtype != b.in_dtype || a.out_dtype != b.out_dtype || a.a_fmt != b.a_fmt ||
+      a.b_fmt != b.b_fmt)
+    return 0;
+  if (a.in_dtype == DT_FP8 && a.out_dtype != DT_BF16) return 0;
+  const int tiles = (a.M / 256) * (a.N / 256) + (b.M / 256) * (b.N / 256);
+  const int nk = a.K / 64;
+  constexpr int kFill = 240;
+  for (int sp : {1, 2, 4, 8})
+    if (tiles * sp >= kFill && nk % sp == 0 && nk / sp >= 16) return sp;
+  return nk % 8 == 0 && nk / 8 >= 16 ? 8 : 1;
+}
+
+hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
+  const int split = gemm_pair_split(a, b);
+  if (split == 0 || a.split_k != split || b.split_k != split) return hipErrorInvalidValue;
+  if (split > 1 && (a.ws == nullptr || a.counters == nullptr || b.ws == nullptr || b.counters == nullptr))
+    return hipErrorInvalidValue;
+  GemmPairArgs g;
+  g.p[0] = a;
+  g.p[1] = b;
+  g.nwg0 = (a.M / 256) * (a.N / 256) * split;
+  const int nwg = g.nwg0 + (b.M / 256) * (b.N / 256) * split;
+  if (a.in_dtype == DT_FP8) return launch_pair_cfg<uint16_t, 14, EK_STORE>(g, nwg, s);
+  if (a.out_dtype == DT_BF16) return launch_pair_cfg<uint16_t, 30, EK_STORE>(g, nwg, s);
+  return launch_pair_cfg<float, 30, EK_ANY>(g, nwg, s);
 }
 
 hipError_t gemm_mfma(const GemmArgs& p, hipStream_t s) {

@@ -103,6 +103,11 @@ int64_t gemm_split_ws_floats(const GemmArgs& args);
 
 // returns hipSuccess or an error; chooses the MFMA path when the shape allows
 hipError_t gemm(const GemmArgs& args, hipStream_t stream);
+// two weight-gradient-layout GEMMs (A, B M/N-contiguous; plain stores; equal K; whole 256-tiles)
+// in one launch. gemm_pair_split: the pair's split-K factor (set it as split_k of both, with
+// gemm_split_ws_floats-sized workspaces for that factor), 0 = the pair is not eligible
+int gemm_pair_split(const GemmArgs& a, const GemmArgs& b);
+hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t stream);
 // exposed for tests / benchmarks: which path gemm() would take
 int gemm_path(const GemmArgs& args);  // 0 = generic VALU, 1 = MFMA bf16 / fp8, 2 = MFMA fp32 / fp64
 

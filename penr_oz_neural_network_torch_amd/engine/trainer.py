@@ -360,6 +360,19 @@ class FusedTrainer:
             if cands:
                 self._late_idx = max(cands, key=lambda st: (st.seg_w.numel, st.index)).index
         self._late_dw = None       # (stage, x_in, dZ) of the deferred weight-gradient GEMM
+        # PAIRED weight-gradient GEMMs (one process): the dW GEMM of the GEMM stage after the first
+        # with the fewest output tiles is deferred to the end of the backward and launched
+        # TOGETHER with the first layer's (pz::gemm_pair): two skinny GEMMs that alone each need a
+        # 4-way split-K to fill the CUs (mlp4: 64 tiles each) share one launch with a 2-way split
+        # (mlp8192: none) — half the slab hand-offs, one launch and one ramp fewer. Its update
+        # then joins the side stream right behind the pair. PZ_DW_PAIR=0: one launch per dW.
+        self._pair_idx = None
+        if (os.environ.get("PZ_DW_PAIR", "1") == "1" and not self.ctx.enabled and not self.fuse_opt
+                and self.overlap and self.stages[0].kind == "gemm"):
+            cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0 and st.index != self._late_idx]
+            if cands:
+                self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
+        self._pair_dw = None       # (stage, x_in, dZ) of the dW GEMM that waits for its partner
         self._fwd_waits: dict = {}  # stage index -> event the next step's forward waits for
         self._pf_args = None       # (epoch, parity, batch) of the sample _prefetch gathers next
         self._pf_ready = None      # ((epoch, parity, batch, data id), event) of a gathered sample
@@ -1186,6 +1199,11 @@ class FusedTrainer:
         if self.fuse_opt and self._ov is not None:
             self._dw_update(st, x_in, g)
             return self._backward_dx(st, before, g, batch, p, keys, rec)
+        if st.index == self._pair_idx and rec is None and self._ov is not None:
+            # paired backward: this weight's gradient GEMM shares the first layer's launch
+            out = self._backward_dx(st, before, g, batch, p, keys, rec)
+            self._pair_dw = (st, x_in, g)
+            return out
         if st.index == self._late_idx and rec is None and self._ov is not None:
             # reordered backward: this weight's gradient GEMM is issued after the whole dX chain
             # (its operands — the stage input and dZ — stay untouched until then)
@@ -1206,7 +1224,11 @@ class FusedTrainer:
         # (measured, not kept: these dW GEMMs on a stream of their own beside the dX chain, without
         # split-K: the concurrent GEMMs stretch each other, mlp4 1.26 vs 1.23 ms —
         # profiles/r3_ab_dw_stream.txt)
-        for c in range(chunks):
+        paired = self._pair_dw if st.index == 0 and chunks == 1 else None
+        self._pair_dw = None if st.index == 0 else self._pair_dw
+        if paired is not None:
+            mine.append(self._run_pair(paired, st, x_in, g, w_grad, f8, handles))
+        for c in range(chunks if paired is None else 0):
             sl = slice(c * rows, (c + 1) * rows)
             out = w_grad[sl] if chunks > 1 else w_grad
             if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
@@ -1235,6 +1257,36 @@ class FusedTrainer:
                 self._opt_async(self._side_pending)
                 self._side_pending = []
         return out
+
+    def _run_pair(self, paired, st0: Stage, x0, g0, w0, f8_0, handles):
+        """The first layer's dW GEMM together with the deferred partner's (``_pair_idx``) in one
+        launch when both take the same operand precision and the pair is eligible, else one
+        after the other. The partner's update joins the side-stream queue (flushed with the
+        step's remaining side updates); returns the first layer's bucket handle."""
+        sp, xp, gp = paired
+        wp = self._w_grad(sp.seg_w)
+        f8_p = self._fp8_dw(sp, gp, wp)
+        ops0 = (f8_0[0], f8_0[2]) if f8_0 is not None else (x0, g0)
+        opsp = (f8_p[0], f8_p[2]) if f8_p is not None else (xp, gp)
+        key = ("pair", (f8_0 is None), (f8_p is None), ops0[0].shape, ops0[1].shape, opsp[0].shape, opsp[1].shape)
+        ok = self._y_dead_cache.get(key)
+        if ok is None:
+            ok = self._y_dead_cache[key] = ((f8_0 is None) == (f8_p is None)
+                                            and PF.gemm_pair_split(ops0[0], ops0[1], w0, opsp[0], opsp[1], wp) > 0)
+        if ok:
+            PF.gemm_pair(ops0[0], ops0[1], w0, opsp[0], opsp[1], wp,
+                         scales0=(f8_0[1], f8_0[3]) if f8_0 is not None else (None, None),
+                         scales1=(f8_p[1], f8_p[3]) if f8_p is not None else (None, None))
+        else:
+            for st, (a, b), f8, w in ((sp, opsp, f8_p, wp), (st0, ops0, f8_0, w0)):
+                if f8 is not None:
+                    PF.gemm(a, False, b, False, w, scale_a=f8[1], scale_b=f8[3])
+                else:
+                    PF.gemm(a, False, b, False, w)
+        hp = self.ctx.all_reduce_async(wp)
+        handles.append(hp)
+        self._side_pending.append((sp.seg_w.offset, [hp], [sp]))
+        return self.ctx.all_reduce_async(w0)
 
     def _finish_reordered(self, main, l2, capture, epoch, row, fin, handles) -> None:
         """End of a reordered step (``PZ_BWD_ORDER``, one process). Main stream: the deferred

@@ -676,3 +676,56 @@ def test_quant_transpose_matches_torch_cast(native_lib, K, N):
     assert abs(qs[0].item() - q) <= 1e-6 * q and clear.item() == 0.0
     ref = (w.t() * qs[0]).clamp(-448, 448).to(torch.float8_e4m3fn)
     assert (out.view(torch.uint8) != ref.view(torch.uint8)).float().mean().item() < 1e-4
+
+
+@pytest.mark.parametrize("shapes,out", [
+    (((1024, 4096), (4096, 1024), 8192), torch.bfloat16),  # mlp4's dW_L1 + dW_L3: 128 tiles, split 2
+    (((1024, 4096), (4096, 1024), 8192), torch.float32),
+    (((1024, 8192), (8192, 1024), 8192), torch.bfloat16),  # mlp8192's two dW: 256 tiles, no split
+    (((256, 512), (512, 256), 1024), torch.bfloat16),      # small: split 4
+])
+def test_gemm_pair_matches_two_launches(native_lib, shapes, out):
+    """pz::gemm_pair: two weight-gradient GEMMs in one launch (first workgroups GEMM 0, the rest
+    GEMM 1, each with its own split-K slabs and tickets) == each against fp64; repeated launches
+    reuse the tile counters."""
+    (m0, n0), (m1, n1), K = shapes
+    a0 = torch.randn(K, m0, device=DEV).to(torch.bfloat16)
+    b0 = torch.randn(K, n0, device=DEV).to(torch.bfloat16)
+    a1 = torch.randn(K, m1, device=DEV).to(torch.bfloat16)
+    b1 = torch.randn(K, n1, device=DEV).to(torch.bfloat16)
+    c0 = torch.empty(m0, n0, device=DEV, dtype=out)
+    c1 = torch.empty(m1, n1, device=DEV, dtype=out)
+    assert PF.gemm_pair_split(a0, b0, c0, a1, b1, c1) > 0
+    r0 = a0.double().t() @ b0.double()
+    r1 = a1.double().t() @ b1.double()
+    for _ in range(3):
+        c0.fill_(float("nan"))
+        c1.fill_(float("nan"))
+        PF.gemm_pair(a0, b0, c0, a1, b1, c1)
+        for c, r in ((c0, r0), (c1, r1)):
+            tol = (2.0 ** -7 if out == torch.bfloat16 else 1e-5) * r.abs().max().item() + 1e-3 * math.sqrt(K)
+            assert (c.double() - r).abs().max().item() < tol
+
+
+def test_gemm_pair_fp8_and_ineligible(native_lib):
+    """The fp8 weight-gradient pair (e4m3 activations x e5m2 gradients, per-GEMM dequant scales)
+    against fp64 on the quantised values; mixed precisions or unequal K are not paired."""
+    K, (m0, n0), (m1, n1) = 8192, (1024, 8192), (8192, 1024)
+    x0 = (torch.randn(K, m0, device=DEV) * 4).to(torch.float8_e4m3fn)
+    g0 = (torch.randn(K, n0, device=DEV) * 1000).to(torch.float8_e5m2)
+    x1 = (torch.randn(K, m1, device=DEV) * 2).to(torch.float8_e4m3fn)
+    g1 = (torch.randn(K, n1, device=DEV) * 500).to(torch.float8_e5m2)
+    s = [torch.tensor([v], device=DEV) for v in (0.25, 1.0 / 4096, 0.5, 1.0 / 2048)]
+    c0 = torch.empty(m0, n0, device=DEV, dtype=torch.bfloat16)
+    c1 = torch.empty(m1, n1, device=DEV, dtype=torch.bfloat16)
+    assert PF.gemm_pair_split(x0, g0, c0, x1, g1, c1) == 1
+    PF.gemm_pair(x0, g0, c0, x1, g1, c1, scales0=(s[0], s[1]), scales1=(s[2], s[3]))
+    for c, x, gg, f in ((c0, x0, g0, 0.25 / 4096), (c1, x1, g1, 0.5 / 2048)):
+        ref = (x.double().t() @ gg.double()) * f
+        assert (c.double() - ref).abs().max().item() <= 2.0 ** -8 * ref.abs().max().item()
+    b16 = torch.randn(K, m1, device=DEV).to(torch.bfloat16)
+    assert PF.gemm_pair_split(x0, g0, c0, b16, torch.randn(K, n1, device=DEV).to(torch.bfloat16), c1) == 0
+    short = torch.randn(K // 2, m1, device=DEV).to(torch.bfloat16)
+    bb = torch.randn(K, n0, device=DEV).to(torch.bfloat16)
+    assert PF.gemm_pair_split(torch.randn(K, m0, device=DEV).to(torch.bfloat16), bb, c0, short,
+                              torch.randn(K // 2, n1, device=DEV).to(torch.bfloat16), c1) == 0
