@@ -50,12 +50,16 @@ template <int VAR> constexpr int var_bk() {
   return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31 || VAR == 32 || VAR == 12 || VAR == 13) ? 64 : 32;
 }
 template <int VAR> constexpr int var_ns() {
-  return (VAR == 5 || VAR == 7) ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4);
+  return (VAR == 5 || VAR == 7 || VAR == 16 || VAR == 17) ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4);
 }
 // VAR 7: buffer DMA on a 3-slot 32-deep ring, for 4-wave 256x128 tiles that run TWO workgroups
 // per CU (72 KiB of LDS and <= 256 VGPRs each): one workgroup's epilogue overlaps the other's
 // main loop (the hardware interleaves the two instead of a barrier-phased ping-pong)
-template <int VAR> constexpr int var_waves_per_eu() { return VAR == 7 ? 2 : 1; }
+// VAR 16 / 17: the fp8 forward (VAR 15) / e5m2 x e4m3 dX (VAR 9) the same way — 4-wave 256x128
+// tiles, 3-slot ring (72 KiB), two workgroups per CU: at K = 1024 an fp8 tile's epilogue (the
+// stage math, the e4m3 / e5m2 copies, the bitmask) costs about what its main loop does, and the
+// other workgroup's MFMAs run through it
+template <int VAR> constexpr int var_waves_per_eu() { return (VAR == 7 || VAR == 16 || VAR == 17) ? 2 : 1; }
 
 // K-contiguous slot [rows][BK]. BK 32: 64-B rows = 4 chunks; chunk XOR for conflict-free
 // ds_read_b128 under the gfx950 b128 lane grouping (row groups of 4 rows map to permutation
@@ -234,7 +238,14 @@ PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int c
 // and output gradients): k rows [k0, k0+KROWS) x bytes [col0, col0+RB) -> slot [KROWS][RB]. The
 // 16-B chunk of k-row kr is XOR-ed with (kr & 7) << 1, so the transposing 8-bit reads below
 // (8 k-rows x 16 bytes per 16-lane group, two groups per 32-lane bank half) are conflict-free.
-PZ_DEV int swz_mn8(int krow) { return (krow & 7) << 1; }
+// 128-B rows (256x128 tiles' B, VAR 16): two k-rows share a 256-B bank row, so the XOR takes
+// k-row bits 1-2 and the row parity selects the half — the same 16 distinct 16-B slots per
+// 8 k-rows x 2 chunks of a 32-lane read
+template <int RB>
+PZ_DEV int swz_mn8(int krow) {
+  if constexpr (RB >= 256) return (krow & 7) << 1;
+  else return ((krow >> 1) & 3) << 1;
+}
 template <int RB, int NW, int KROWS>
 PZ_DEV void stage_mn8(int64_t ld16, int col0, int k0, PZ_LDS char* tile, int wave, int lane, i32x4_t rs) {
   constexpr int CHUNKS = RB / 16;
@@ -245,7 +256,7 @@ PZ_DEV void stage_mn8(int64_t ld16, int col0, int k0, PZ_LDS char* tile, int wav
   for (int i = 0; i < INSTR; ++i) {
     const int kbase = (wave * INSTR + i) * ROWS_PER;
     const int kr = kbase + lane / CHUNKS;
-    const int chunk = (lane % CHUNKS) ^ swz_mn8(kr);
+    const int chunk = (lane % CHUNKS) ^ swz_mn8<RB>(kr);
     const uint32_t voff = (static_cast<uint32_t>(kr) * static_cast<uint32_t>(ld16)) * 2u +
                           static_cast<uint32_t>(col0 + chunk * 16);
     blds16<0>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * static_cast<uint32_t>(ld16) * 2u),
@@ -267,7 +278,7 @@ PZ_DEV i32x8_t frag_mn8(const PZ_LDS char* tile, int col32, int lane) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int k = 32 * (lane >> 5) + 8 * i + q;
-    const PZ_LDS char* a = tile + k * RB + ((chunk ^ swz_mn8(k)) << 4) + within;
+    const PZ_LDS char* a = tile + k * RB + ((chunk ^ swz_mn8<RB>(k)) << 4) + within;
     const i32x2_t r = __builtin_amdgcn_ds_read_tr8_b64_v2i32((PZ_LDS i32x2_t*)(a));
     out[2 * i] = r[0];
     out[2 * i + 1] = r[1];
@@ -560,9 +571,10 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
   // VAR 15: the fp8 forward X8 · W8 with the e4m3 weights in their natural [in, out] layout
   // (B N-contiguous, transposing 8-bit reads) — the same copy the backward dX GEMM reads as its
   // K-contiguous B, so one e4m3 weight copy serves both and no transposed copy is made
-  constexpr bool F8_MNB = VAR == 15;
-  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11 || VAR == 12 || VAR == 13 || F8_MN || F8_MNB;
-  constexpr bool F8_BWD = VAR == 9 || VAR == 11 || VAR == 13;
+  constexpr bool F8_MNB = VAR == 15 || VAR == 16;
+  constexpr bool F8 = VAR == 8 || VAR == 9 || VAR == 10 || VAR == 11 || VAR == 12 || VAR == 13 || VAR == 17 || F8_MN ||
+                      F8_MNB;
+  constexpr bool F8_BWD = VAR == 9 || VAR == 11 || VAR == 13 || VAR == 17;
   constexpr int F8_FMT_A = F8_BWD ? 1 : 0;  // MFMA format codes: 0 = fp8 e4m3, 1 = bf8 e5m2
   constexpr int F8_FMT_B = F8_MN ? 1 : 0;
   static_assert(!F8 || ((F8_MN ? (!A_KC && !B_KC) : F8_MNB ? (A_KC && !B_KC) : (A_KC && B_KC)) &&
@@ -1187,12 +1199,38 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   return buf ? launch_layout<128, 128, 2, 2, OutT, AuxT, 6>(p, s) : launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
 }
 
+// PZ_F8_2WG (default 1): fp8 GEMMs with at least two 256x256 tiles per CU and no split-K run as
+// 256x128 tiles on 4-wave workgroups, two per CU (VAR 16 / 17): one workgroup's epilogue beside
+// the other's main loop. 0: the 8-wave ping-pong 256x256 kernels (VAR 15 / 9)
+bool f8_two_wg(const GemmArgs& p) {
+  static const bool on = [] {
+    const char* e = getenv("PZ_F8_2WG");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
+  return on && p.split_k <= 1 && t256 >= 480 && p.N % 128 == 0;
+}
+
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   if (!p.a_kc && !p.b_kc)  // e4m3 x e5m2 weight gradient (fp8_eligible: full 256-tiles, buffer-addressable,
                           // plain store)
     return launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14, EK_STORE>(p, s);
   int ek = epi_kind(p);
+  if (f8_two_wg(p)) {
+    if (p.a_kc && !p.b_kc) {
+      if (ek == EK_RELU) return launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, EK_RELU>(p, s);
+      if (ek == EK_F_RELU_POST) return launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, EK_F_RELU_POST>(p, s);
+      if (ek == EK_F_RELU_PREPOST)
+        return launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, EK_F_RELU_PREPOST>(p, s);
+      if (ek == EK_F_PRE) return launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, EK_F_PRE>(p, s);
+      return launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16>(p, s);
+    }
+    if (p.a_kc && p.b_kc && p.a_fmt == 1) {
+      if (ek == EK_BWD_MASK) return launch_cfg<256, 128, 2, 2, true, true, uint16_t, uint16_t, 17, EK_BWD_MASK>(p, s);
+      return launch_cfg<256, 128, 2, 2, true, true, uint16_t, uint16_t, 17>(p, s);
+    }
+  }
   if (p.a_kc && !p.b_kc) {  // e4m3 X x e4m3 W[in, out] (fp8_eligible: N % 256 — B's transposed image
                            // rows are whole 256-B tiles, swz_mn8 — buffer-addressable B; split-K
                            // when the tiles do not fill the CUs, gemm_split)
