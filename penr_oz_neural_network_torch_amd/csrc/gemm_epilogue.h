@@ -385,27 +385,49 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       vv[s] = *reinterpret_cast<const PZ_LDS u32x4_t*>(smem + cimg_off<BN>(s * ROWS_PER_PASS + my_row, my_chunk * 8));
     const int gn = n0 + my_chunk * 8;
     const int64_t row0 = static_cast<int64_t>(m0 + my_row);
+    // p.store_wt: write-through (sc1) buffer stores from the tile's base (32-bit byte offsets within
+    // the tile's rows), so the kernel leaves no dirty lines behind in the L2s
+    constexpr int kSc1 = 16;
+    const bool wt = p.store_wt != 0;
     if (Cp != nullptr) {  // (fp8 policy: a bf16 output nobody reads is not written — only its copies)
       uint16_t* dst = Cp + row0 * p.ldc + gn;
       const int64_t step = static_cast<int64_t>(ROWS_PER_PASS) * p.ldc;
+      if (wt) {
+        const auto rs = __builtin_amdgcn_make_buffer_rsrc(Cp + static_cast<int64_t>(m0) * p.ldc, 0, 0x7FFFFFFF, 0x00020000);
+        const uint32_t off0 = static_cast<uint32_t>((my_row * p.ldc + gn) * 2);
 #pragma unroll
-      for (int s = 0; s < PASSES; ++s) *reinterpret_cast<u32x4_t*>(dst + s * step) = vv[s];
+        for (int s = 0; s < PASSES; ++s)
+          __builtin_amdgcn_raw_buffer_store_b128(vv[s], rs, off0 + static_cast<uint32_t>(s * step * 2), 0, kSc1);
+      } else {
+#pragma unroll
+        for (int s = 0; s < PASSES; ++s) *reinterpret_cast<u32x4_t*>(dst + s * step) = vv[s];
+      }
     }
     if (!bwd && use_mask) {
       uint8_t* mdst = p.mask + row0 * p.ldmask + gn / 8;
       const int64_t mstep = static_cast<int64_t>(ROWS_PER_PASS) * p.ldmask;
+      const auto rsm = __builtin_amdgcn_make_buffer_rsrc(p.mask + static_cast<int64_t>(m0) * p.ldmask, 0, 0x7FFFFFFF,
+                                                         0x00020000);
+      const uint32_t moff0 = static_cast<uint32_t>(my_row * p.ldmask + gn / 8);
 #pragma unroll
       for (int s = 0; s < PASSES; ++s) {
         const uint32_t byte = relu_bits8(vv[s]);  // bit b = element gn+b > 0
         const uint32_t b1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0x55, 0xF, 0xF, false));
         const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xAA, 0xF, 0xF, false));
         const uint32_t b3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xFF, 0xF, 0xF, false));
-        if ((my_chunk & 3) == 0) *reinterpret_cast<uint32_t*>(mdst + s * mstep) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        const uint32_t word = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        if ((my_chunk & 3) == 0) {
+          if (wt) __builtin_amdgcn_raw_buffer_store_b32(word, rsm, moff0 + static_cast<uint32_t>(s * mstep), 0, kSc1);
+          else *reinterpret_cast<uint32_t*>(mdst + s * mstep) = word;
+        }
       }
     }
     if (want8) {  // fp8 copy of the stored bf16 values + running |y| max
       uint8_t* d8 = p.out8 + row0 * p.ldout8 + gn;
       const int64_t step8 = static_cast<int64_t>(ROWS_PER_PASS) * p.ldout8;
+      const auto rs8 = __builtin_amdgcn_make_buffer_rsrc(p.out8 + static_cast<int64_t>(m0) * p.ldout8, 0, 0x7FFFFFFF,
+                                                         0x00020000);
+      const uint32_t off8 = static_cast<uint32_t>(my_row * p.ldout8 + gn);
 #pragma unroll
       for (int s = 0; s < PASSES; ++s) {
         float x[8];
@@ -415,7 +437,9 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
           x[2 * q + 1] = bf2f(vv[s][q] >> 16);
           amax = fmaxf(amax, fmaxf(fabsf(x[2 * q]), fabsf(x[2 * q + 1])));
         }
-        *reinterpret_cast<u32x2_t*>(d8 + s * step8) = bwd ? to_e5m2x8(x, qs) : to_e4m3x8(x, qs);
+        const u32x2_t q8 = bwd ? to_e5m2x8(x, qs) : to_e4m3x8(x, qs);
+        if (wt) __builtin_amdgcn_raw_buffer_store_b64(q8, rs8, off8 + static_cast<uint32_t>(s * step8), 0, kSc1);
+        else *reinterpret_cast<u32x2_t*>(d8 + s * step8) = q8;
       }
     }
   }

@@ -1419,6 +1419,16 @@ int64_t gemm_split_ws_floats(const GemmArgs& p) {
   return static_cast<int64_t>((p.M + 255) / 256) * ((p.N + 255) / 256) * sp * 256 * 256;
 }
 
+// PZ_GEMM_WT=1: whole-tile epilogue stores write through (sc1) instead of leaving dirty L2 lines
+// for the kernel boundary's write-back (GemmArgs::store_wt)
+int store_wt_default() {
+  static const int on = [] {
+    const char* e = getenv("PZ_GEMM_WT");
+    return e != nullptr ? atoi(e) : 0;
+  }();
+  return on;
+}
+
 // gemm_pair: both GEMMs in the weight-gradient layout (A and B M/N-contiguous), plain stores of
 // whole 256 x 256 tiles, one K; returns the split-K factor of the pair, or 0 if it cannot be paired
 int gemm_pair_split(const GemmArgs& a, const GemmArgs& b) {
@@ -1450,6 +1460,7 @@ hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
   GemmPairArgs g;
   g.p[0] = a;
   g.p[1] = b;
+  g.p[0].store_wt = g.p[1].store_wt = store_wt_default();
   g.nwg0 = (a.M / 256) * (a.N / 256) * split;
   const int nwg = g.nwg0 + (b.M / 256) * (b.N / 256) * split;
   if (a.in_dtype == DT_FP8) return launch_pair_cfg<uint16_t, 14, EK_STORE>(g, nwg, s);
@@ -1457,7 +1468,9 @@ hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
   return launch_pair_cfg<float, 30, EK_ANY>(g, nwg, s);
 }
 
-hipError_t gemm_mfma(const GemmArgs& p, hipStream_t s) {
+hipError_t gemm_mfma(const GemmArgs& in, hipStream_t s) {
+  GemmArgs p = in;
+  p.store_wt = store_wt_default();
   if (p.split_k > 1 && (p.ws == nullptr || p.counters == nullptr)) return hipErrorInvalidValue;
   if (p.in_dtype == DT_FP8) return launch_fp8(p, s);
   if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);

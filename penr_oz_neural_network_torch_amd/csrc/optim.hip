@@ -119,14 +119,26 @@ PZ_DEV void add_stats(double st[4], R p0, R p1, bool full) {
 template <typename R> struct Vec;
 template <> struct Vec<float> { using T = float4; static constexpr int N = 4; };
 template <> struct Vec<double> { using T = double2; static constexpr int N = 2; };
-template <typename R>
+// NT: non-temporal (streaming) access for the once-per-step state streams (PZ_OPT_NT): the update
+// moves ~28 B per parameter that nothing re-reads before the next step, and default-policy
+// accesses let it evict the GEMMs' operands from the L2s and the Infinity Cache
+template <typename R, bool NT = false>
 PZ_DEV void vld(const R* p, R (&x)[Vec<R>::N]) {
+  if constexpr (NT && Vec<R>::N == 4) {
+    const f32x4_t q = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p));
+    x[0] = q[0]; x[1] = q[1]; x[2] = q[2]; x[3] = q[3];
+    return;
+  }
   const typename Vec<R>::T q = *reinterpret_cast<const typename Vec<R>::T*>(p);
   if constexpr (Vec<R>::N == 4) { x[0] = q.x; x[1] = q.y; x[2] = q.z; x[3] = q.w; }
   else { x[0] = q.x; x[1] = q.y; }
 }
-template <typename R>
+template <typename R, bool NT = false>
 PZ_DEV void vst(R* p, const R (&x)[Vec<R>::N]) {
+  if constexpr (NT && Vec<R>::N == 4) {
+    __builtin_nontemporal_store(f32x4_t{x[0], x[1], x[2], x[3]}, reinterpret_cast<f32x4_t*>(p));
+    return;
+  }
   typename Vec<R>::T q;
   if constexpr (Vec<R>::N == 4) { q.x = x[0]; q.y = x[1]; q.z = x[2]; q.w = x[3]; }
   else { q.x = x[0]; q.y = x[1]; }
@@ -140,7 +152,7 @@ PZ_DEV void vst(R* p, const R (&x)[Vec<R>::N]) {
 // Grid: min(total_blocks, kOptMaxResident) workgroups loop over the 4096-element work blocks, so
 // a launch that overlaps the MFMA-bound GEMMs (side stream) gets all its workgroups resident
 // beside the GEMM's instead of queueing behind the GEMM's pending ones.
-template <bool ADAM, typename R, int PRE>
+template <bool ADAM, typename R, int PRE, bool NT = false>
 PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block, bool full) {
   constexpr int VN = Vec<R>::N;
   const int seg_id = find_segment(args.block_seg, args.num_segments, block);
@@ -186,7 +198,7 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
 #pragma unroll
       for (int k = 0; k < VN; ++k) m[u][k] = v[u][k] = R(0);
       if (!ok[u]) continue;
-      vld<R>(P + gi, p0[u]);
+      vld<R, NT>(P + gi, p0[u]);
       if constexpr (VN == 4) {
         if (G16 != nullptr) {
           const uint2 q = *reinterpret_cast<const uint2*>(G16 + lc);
@@ -198,8 +210,8 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
         vld<R>(Gr + gi, g[u]);
       }
       if constexpr (ADAM) {
-        vld<R>(Mm + gi, m[u]);
-        vld<R>(Vv + gi, v[u]);
+        vld<R, NT>(Mm + gi, m[u]);
+        vld<R, NT>(Vv + gi, v[u]);
       }
     }
 #pragma unroll
@@ -215,10 +227,10 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
 #pragma unroll
       for (int k = 0; k < VN; ++k) p1[k] = update_one<ADAM, R>(a, p0[u][k], g[u][k], l2x2, step_size, m[u][k], v[u][k]);
       if constexpr (ADAM) {
-        vst<R>(a.exp_avg + gi, m[u]);
-        vst<R>(a.exp_avg_sq + gi, v[u]);
+        vst<R, NT>(a.exp_avg + gi, m[u]);
+        vst<R, NT>(a.exp_avg_sq + gi, v[u]);
       }
-      vst<R>(a.params + gi, p1);
+      vst<R, NT>(a.params + gi, p1);
       if constexpr (VN == 4) {
         if (seg.w8 != nullptr)
           *reinterpret_cast<uint32_t*>(seg.w8 + li) = e4m3x4(p1[0] * q8, p1[1] * q8, p1[2] * q8, p1[3] * q8);
@@ -275,7 +287,7 @@ PZ_DEV void optimizer_block(const OptArgs& args, const OptView<R>& a, int block,
   if (seg.amax != nullptr) block_amax_commit(am, seg.amax);
 }
 
-template <bool ADAM, typename R, int PRE>
+template <bool ADAM, typename R, int PRE, bool NT = false>
 __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   int epoch = -1;
   if (a.epoch_ptr != nullptr) epoch = *a.epoch_ptr;
@@ -288,7 +300,7 @@ __global__ void __launch_bounds__(kThreads) optimizer_kernel(OptArgs a) {
   const OptView<R> view(a);
   const bool full = a.stats_every == 1 || (a.stats_every > 1 && (epoch < 0 || epoch % a.stats_every == 0));
   for (int b = blockIdx.x; b < a.total_blocks; b += gridDim.x) {
-    optimizer_block<ADAM, R, PRE>(a, view, b, full);
+    optimizer_block<ADAM, R, PRE, NT>(a, view, b, full);
     __syncthreads();  // the block reductions reuse their LDS slots
   }
 }
@@ -384,8 +396,17 @@ hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
     if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((optimizer_kernel<false, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   } else {
-    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
-    else hipLaunchKernelGGL((optimizer_kernel<false, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+    static const bool nt = [] {  // PZ_OPT_NT=1: non-temporal state streams (A/B)
+      const char* e = getenv("PZ_OPT_NT");
+      return e != nullptr && atoi(e) == 1;
+    }();
+    if (nt) {
+      if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
+      else hipLaunchKernelGGL((optimizer_kernel<false, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    } else {
+      if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+      else hipLaunchKernelGGL((optimizer_kernel<false, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
+    }
   }
   return hipGetLastError();
 }

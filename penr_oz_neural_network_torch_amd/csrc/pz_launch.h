@@ -95,6 +95,11 @@ struct GemmArgs {
   int* counters;   // [tiles], zero; reset by the last arriver
   GemmOpt opt;     // EPI_OPT only
   uint64_t* dbg;   // diagnostic phase stamps (tools/gemm_stamps.hip builds only); nullptr otherwise
+  // epilogue stores of whole tiles (C, the ReLU bitmask, the fp8 copy) as write-through `sc1`
+  // buffer stores (set by the launcher, PZ_GEMM_WT): a kernel boundary writes back every line a
+  // kernel left dirty in the XCD L2s (~B / 6 TB/s for B dirty bytes, MI355X_MICROARCH "boundary"),
+  // and a GEMM that stores 64 MB of output leaves the L2s full of them
+  int store_wt;
 };
 
 // split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().

@@ -59,6 +59,10 @@ def main():
         ("f8_8k_L1", B, 8192, 1024, True, True, "fp8", "fwd"),
         ("f8_8k_L2", B, 1024, 8192, True, True, "fp8", "fwd_nodrop"),
         ("f8_fwd_L2", B, 4096, 4096, True, True, "fp8", "fwd"),
+        # the trainer's fp8 fast paths: natural [in, out] e4m3 weights (VAR 15 / 16) with the ReLU
+        # bitmask epilogue, and the e5m2 x e4m3 dX with the bitmask derivative (VAR 9 / 17)
+        ("f8n_8k_L1", B, 8192, 1024, True, False, "fp8", "fwd_mask"),
+        ("f8_8k_dX", B, 8192, 1024, True, True, "fp8bwd", "bwd_mask"),
         ("bf_8k_L1", B, 8192, 1024, True, False, torch.bfloat16, "fwd"),
         ("bf_8k_L2", B, 1024, 8192, True, False, torch.bfloat16, "fwd_nodrop"),
     ]
@@ -67,10 +71,11 @@ def main():
     for name, M, N, K, akc, bkc, odt, mode in cases:
         if (only and name not in only) or (not only and "_" in name.split("L")[-1][1:]):
             continue
-        fp8 = odt == "fp8"
+        fp8 = odt in ("fp8", "fp8bwd")
         idt = torch.float8_e4m3fn if fp8 else torch.bfloat16
+        adt = torch.float8_e5m2 if odt == "fp8bwd" else idt
         odt = torch.bfloat16 if fp8 else odt
-        a = torch.randn((M, K) if akc else (K, M), device=dev).to(idt)
+        a = torch.randn((M, K) if akc else (K, M), device=dev).to(adt)
         b = torch.randn((N, K) if bkc else (K, N), device=dev).to(idt)
         c = torch.empty(M, N, device=dev, dtype=odt)
         bias = torch.randn(N, device=dev)
@@ -115,7 +120,8 @@ def main():
         Bm = b.t() if bkc else b
         if fp8:  # hipBLASLt fp8 GEMM through torch._scaled_mm (row-major A, column-major B)
             one = torch.ones((), device=dev)
-            ref = lambda: torch._scaled_mm(a, b.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
+            bt = b if bkc else b.t().contiguous()  # [N, K]: column-major B
+            ref = lambda: torch._scaled_mm(a, bt.t(), scale_a=one, scale_b=one, out_dtype=torch.bfloat16)
         else:
             ref = lambda: torch.matmul(A, Bm)
         fl = 2.0 * M * N * K
