@@ -462,3 +462,38 @@ def test_graph_replay_matches_eager_steps(optimizer):
     if s0 is not None:
         for k in s0["state"]:
             assert float(s0["state"][k]["step"]) == float(s1["state"][k]["step"]) == epochs
+
+
+@pytest.mark.parametrize("dtype", ["bfloat16", "fp8"])
+def test_paired_dw_matches_separate_launches(monkeypatch, dtype):
+    """PZ_DW_PAIR: the first layer's and the smallest later layer's weight-gradient GEMMs in one
+    launch (pz::gemm_pair, at the end of the backward; that layer's update then follows the pair)
+    reproduce one launch per dW GEMM: costs, parameters and update ratios within the run-to-run
+    noise of the unpaired schedule (split-K summation order)."""
+    sizes = [1024, 2048, 1024, 512]
+    algos = ["relu", "relu", "softmax"]
+    n, S, steps = 8192, 4096, 4
+    g = torch.Generator().manual_seed(12)
+    inputs = torch.randn(n, sizes[0], generator=g)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    idx = torch.randint(0, n, (steps, S), generator=g)
+    runs = {}
+    for run in ("0", "0b", "1"):
+        monkeypatch.setenv("PZ_DW_PAIR", run[0])
+        torch.manual_seed(0)
+        model = NeuralNetworkModel("pr", sizes, "xavier", "random", algos, "adam", dtype=dtype, device="cuda")
+        tr = FusedTrainer(model)
+        assert (tr._pair_idx is not None) == (run == "1")
+        tr.load_tensors(inputs, labels, seed=3)
+        tr.begin(steps)
+        for e in range(steps):
+            tr.step(e, 0.003, S, 0.1, 1e-3, want_ratios=True, record=False, indices=idx[e])
+        out = tr.drain()
+        if run == "1":
+            assert tr._pair_idx == 2 and any(k[0] == "pair" and v for k, v in tr._y_dead_cache.items())
+        runs[run] = ([c for _, c, _, _ in out], model._param_store.flat.clone())
+    (c0, p0), (cn, pn), (c1, p1) = runs["0"], runs["0b"], runs["1"]
+    for a, b, nb in zip(c0, c1, cn):
+        assert abs(a - b) <= 3 * abs(a - nb) + 1e-3 * max(1.0, abs(a)), (c0, c1, cn)
+    d, dn = (p0 - p1).abs(), (p0 - pn).abs()
+    assert d.mean().item() <= 3 * dn.mean().item() + 2e-5, (d.mean().item(), dn.mean().item())

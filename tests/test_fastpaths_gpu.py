@@ -241,7 +241,8 @@ def test_torch_backward_scenario_on_gpu_fp64():
         for a in acts:
             a.retain_grad()
         cost.backward()
-        grads[name] = (cost.detach().cpu(), [a.detach().cpu() for a in acts], [a.grad.cpu() for a in acts],
+        grads[name] = (cost.detach().cpu(), [a.detach().cpu() for a in acts],
+                       [a.grad.cpu() if a.grad is not None else None for a in acts],  # (probs: not in the loss)
                        [p.grad.detach().cpu() for p in m.params])
         for p in m.params:
             p.requires_grad_(False)
@@ -250,8 +251,11 @@ def test_torch_backward_scenario_on_gpu_fp64():
     torch.testing.assert_close(c1, c0, rtol=1e-12, atol=0)
     for i, (x, y) in enumerate(zip(a0, a1)):
         torch.testing.assert_close(y, x, rtol=1e-10, atol=1e-13, msg=f"activation {i}")
+    assert [g is None for g in ag0] == [g is None for g in ag1]
+    assert sum(g is not None for g in ag0) == len(ag0) - 1  # every activation but the softmax output
     for i, (x, y) in enumerate(zip(ag0, ag1)):
-        torch.testing.assert_close(y, x, rtol=1e-10, atol=1e-15, msg=f"activation grad {i}")
+        if x is not None:
+            torch.testing.assert_close(y, x, rtol=1e-10, atol=1e-15, msg=f"activation grad {i}")
     names = ["c", "w1", "b1", "bn_gain", "bn_bias", "w2", "b2"]
     for nm, x, y in zip(names, pg0, pg1):
         torch.testing.assert_close(y, x, rtol=1e-10, atol=1e-15, msg=nm)

@@ -729,3 +729,54 @@ def test_gemm_pair_fp8_and_ineligible(native_lib):
     bb = torch.randn(K, n0, device=DEV).to(torch.bfloat16)
     assert PF.gemm_pair_split(torch.randn(K, m0, device=DEV).to(torch.bfloat16), bb, c0, short,
                               torch.randn(K // 2, n1, device=DEV).to(torch.bfloat16), c1) == 0
+
+
+_WT_SCRIPT = r"""
+import sys, torch
+sys.path.insert(0, sys.argv[2])
+from penr_oz_neural_network_torch_amd.ops import functional as PF
+torch.manual_seed(0)
+D = "cuda"
+M, N, K = 8192, 4096, 1024
+a = torch.randn(M, K, device=D).to(torch.bfloat16)
+w = torch.randn(K, N, device=D).to(torch.bfloat16)
+bias = torch.randn(N, device=D)
+epi = PF.epi_spec(act=PF.ACT_RELU, drop_post=2, p=0.2, seed=(1, 2))
+y = torch.empty(M, N, device=D, dtype=torch.bfloat16)
+mask = torch.empty(M, PF.relu_mask_cols(N), device=D, dtype=torch.uint8)
+PF.gemm(a, True, w, False, y, bias=bias, mode=PF.EPI_FWD, epi=epi, mask=mask)
+x8 = (torch.randn(M, K, device=D) * 4).to(torch.float8_e4m3fn)
+w8 = (torch.randn(K, N, device=D) * 2).to(torch.float8_e4m3fn)
+y8 = torch.empty(M, N, device=D, dtype=torch.float8_e4m3fn)
+yf = torch.empty(M, N, device=D, dtype=torch.bfloat16)
+one = torch.ones(1, device=D)
+PF.gemm(x8, True, w8, False, yf, bias=bias, mode=PF.EPI_FWD, epi=epi, scale_a=one, scale_b=one, out8=y8,
+        out8_qscale=one, amax=torch.zeros(1, device=D))
+dw = torch.empty(K, N, device=D, dtype=torch.bfloat16)
+PF.gemm(a, False, y, False, dw)  # [K=8192 rows] x: dW layout (M/N-contiguous), split-K
+torch.save({"y": y.cpu(), "mask": mask.cpu(), "y8": y8.view(torch.uint8).cpu(), "yf": yf.cpu(), "dw": dw.cpu()},
+           sys.argv[1])
+"""
+
+
+def test_write_through_epilogue_stores_are_bit_identical(tmp_path):
+    """PZ_GEMM_WT=1 (whole-tile epilogue stores as write-through sc1 buffer stores: C, the ReLU
+    bitmask, the fp8 copy; bf16 forward, fp8 forward, split-K dW) writes exactly the bytes the
+    default stores write. The policy is read once per process: one subprocess per setting."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    script = tmp_path / "wt.py"
+    script.write_text(_WT_SCRIPT)
+    outs = []
+    for wt in ("0", "1"):
+        out = tmp_path / f"wt{wt}.pt"
+        env = dict(os.environ, PZ_GEMM_WT=wt)
+        subprocess.run([sys.executable, str(script), str(out), root], env=env, check=True, timeout=240)
+        outs.append(torch.load(out, weights_only=True))
+    for k in outs[0]:
+        if k == "dw":  # split-K: the last-arriving slice (run-dependent) sets the fp32 summation order
+            torch.testing.assert_close(outs[0][k].float(), outs[1][k].float(), rtol=2 ** -7, atol=1e-2)
+        else:
+            assert torch.equal(outs[0][k], outs[1][k]), k
