@@ -965,9 +965,11 @@ class FusedTrainer:
             # stream right behind the last dW: the next step's first GEMM follows it in order (no
             # cross-stream wait), and it overlaps the side stream's still-running updates instead
             # of queueing behind them; step_finalize (side) waits for both
-            if self._side_pending:  # (merged side updates not flushed by their last layer)
+            after_rest = self._side_after_rest()
+            late_side = sorted(self._side_pending, key=lambda it: it[2][0].index) if after_rest else []
+            if self._side_pending and not after_rest:  # (merged side updates not flushed by their last layer)
                 self._opt_async(self._side_pending)
-                self._side_pending = []
+            self._side_pending = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
@@ -977,8 +979,21 @@ class FusedTrainer:
             self._ov = None
             rest_ev = torch.cuda.Event()
             rest_ev.record(main)
+            fwd_waits = {}
             with torch.cuda.stream(self.opt_stream):
                 self.opt_stream.wait_event(rest_ev)
+                for key, hs, stages in late_side:  # paired backward: one event per updated weight
+                    for h in hs:
+                        self.ctx.wait_one(h)
+                    self.opt.step_group(key, self.grads, l2, 1.0, 1 - self.parity)
+                    if self.fp8:
+                        for st in stages:
+                            self._refresh_fp8_weights(st, 1 - self.parity)
+                    if not capture:
+                        wev = torch.cuda.Event()
+                        wev.record(self.opt_stream)
+                        for st in stages:
+                            fwd_waits[st.index] = wev
                 for key, hs, stages in self._deferred:  # PZ_OPT_DEFER
                     for h in hs:
                         self.ctx.wait_one(h)
@@ -999,7 +1014,8 @@ class FusedTrainer:
                 # update) finishes long before the next step's first GEMM does, and its loss-slot
                 # and statistics resets are then ordered before the head and the updates
                 self._opt_done = ev
-                self._early_done = ev
+                self._early_done = None if after_rest else ev
+                self._fwd_waits = fwd_waits
                 self._last_event = ev
             self.parity = 1 - self.parity
             self._phase(None)
@@ -1253,10 +1269,19 @@ class FusedTrainer:
         if self._ov is not None and own and not early and not trickle:
             item = (st.seg_w.offset, mine, [st])
             (self._deferred if st.seg_w.offset == self._defer_key else self._side_pending).append(item)
-            if (not self._merge_side or st.seg_w.offset == self._flush_key) and self._side_pending:
+            if ((not self._merge_side or st.seg_w.offset == self._flush_key) and self._side_pending
+                    and not self._side_after_rest()):
                 self._opt_async(self._side_pending)
                 self._side_pending = []
         return out
+
+    def _side_after_rest(self) -> bool:
+        """Paired backward (PZ_DW_PAIR): the side-stream updates wait for the step's last launch
+        (the first-layer / bias update on the main stream, which then has the HBM to itself right
+        behind the pair) and run beside the NEXT step's first forward GEMMs, each forward stage
+        waiting only for its own weight's update (PZ_PAIR_SIDE=0: flushed as before)."""
+        return (self._pair_idx is not None and self._ov is not None
+                and os.environ.get("PZ_PAIR_SIDE", "1") == "1")
 
     def _run_pair(self, paired, st0: Stage, x0, g0, w0, f8_0, handles):
         """The first layer's dW GEMM together with the deferred partner's (``_pair_idx``) in one

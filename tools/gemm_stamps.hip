@@ -47,6 +47,7 @@ struct Case {
   LaunchFn fn;
   int f8 = 0;  // 0 bf16, 1 e4m3 x e4m3 (forward), 2 e5m2 x e4m3 (backward dX), 3 e4m3 x e5m2 (dW)
   int tile_m = 0, tile_n = 0;  // 0: 256x256 (128x128 for the small fp8 config)
+  int wt = 0;                  // write-through (sc1) epilogue stores (GemmArgs::store_wt)
 };
 
 static double med(std::vector<double> v) {
@@ -106,6 +107,13 @@ int main(int argc, char** argv) {
       {"f8_dX_L2", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9, M>, 2},
       {"f8_dX_L2_gen", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9, G>, 2},
       {"f8_dW_L2", 8192, 1024, B, false, false, false, 0, 2, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14, S>, 3},
+      // r4: the fp8 GEMMs on two 4-wave 256x128 workgroups per CU (VAR 16 / 17)
+      {"f8n_fwd_L1_2wg", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, F1>, 1, 256, 128},
+      {"f8_dX_L2_2wg", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 128, 2, 2, true, true, uint16_t, uint16_t, 17, M>, 2, 256, 128},
+      // r4: write-through (sc1) epilogue stores
+      {"fwd_L2_wt", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, F2>, 0, 0, 0, 1},
+      {"dX_L2_wt", B, 4096, 4096, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30, M>, 0, 0, 0, 1},
+      {"f8n_fwd_L1_fx_wt", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, F1>, 1, 0, 0, 1},
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -177,6 +185,7 @@ int main(int argc, char** argv) {
       p.colsum = colsum;
     }
     p.epi = e;
+    p.store_wt = c.wt;
     int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, R> ? 128 : 256, bn = bm;
     if (c.tile_m) bm = c.tile_m, bn = c.tile_n;
     const int tiles = ((c.M + bm - 1) / bm) * ((c.N + bn - 1) / bn);
