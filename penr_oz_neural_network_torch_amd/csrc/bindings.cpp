@@ -168,9 +168,9 @@ pz::GemmArgs gemm_args(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, c
   p.idx_ld = idx_ld > 0 ? idx_ld : N;
   p.force_generic = force_generic;
   if (mask.has_value() && mask->defined()) {
-    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->dim() == 2 && mask->stride(1) == 1 && mask->size(0) >= M &&
-                    mask->size(1) >= (N + 63) / 64 * 8,
-                "pz::gemm: mask must be uint8 [M, ceil(N/64)*8]");
+    TORCH_CHECK(mask->scalar_type() == at::kByte && mask->dim() == 2 && mask->is_contiguous() &&
+                    mask->size(0) >= (M + 255) / 256 * 256 && mask->size(1) == (N + 255) / 256 * 32,
+                "pz::gemm: mask must be a contiguous uint8 [roundup(M, 256), ceil(N/256)*32] (tile-blocked)");
     p.mask = mask->data_ptr<uint8_t>();
     p.ldmask = mask->stride(0);
   }

@@ -7,7 +7,8 @@
 //      Branches sit outside the unrolled fragment loops, so the code is the SUM of the passes,
 //      not their product (a per-fragment switch produced ~5k basic blocks and I-cache stalls);
 //   3. results go to the LDS image as bf16 and leave it as full 16-B-per-lane row segments;
-//   4. ReLU stages: the forward also writes a 1-bit-per-element mask of y > 0, and the backward
+//   4. ReLU stages: the forward also writes a 1-bit-per-element mask of y > 0 (tile-blocked, see
+//      GemmArgs::mask), and the backward
 //      reads 8 mask bytes per accumulator row instead of the 512-B aux row segment (dX GEMMs
 //      with K = 1024 spent a third of their time streaming the bf16 aux tile);
 //   5. fp8 consumers: the forward can also emit an e4m3 copy of y (scaled by a device-side
@@ -240,6 +241,11 @@ PZ_DEV void fixed_fwd_row(f32x4_t (&v)[L::COLS], const EpiSpec& e, uint32_t pr_r
   }
 }
 
+// byte of the tile-blocked ReLU bitmask holding element (m, n) (GemmArgs::mask)
+PZ_DEV int64_t mask_off(int64_t m, int n, int64_t ldmask) {
+  return (m >> 8) * 256 * ldmask + static_cast<int64_t>(n >> 8) * 8192 + (m & 255) * 32 + ((n & 255) >> 3);
+}
+
 template <int BM, int BN, int WM, int WN, class L, bool FWD_ONLY = false, int EK = EK_ANY, class Acc>
 PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0, int n0, int wm, int wn, int lane,
                          float alpha) {
@@ -265,12 +271,12 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   // loads fly while the slower waves finish their last MFMAs
   u32x2_t mbits[ROWS];
   if (bwd && use_mask) {
-    const uint8_t* mrow = p.mask + (n0 + wn * WTN) / 8;
+    // (the tile's rows lie in one 256-row block: 32-B row pitch, 64-column aligned 8-B reads)
+    const uint8_t* mrow = p.mask + mask_off(m0, n0 + wn * WTN, p.ldmask);
 #pragma unroll
     for (int i = 0; i < ROWS; ++i) {
       const int m = m0 + ml0 + L::MSTEP * i;
-      mbits[i] = m < p.M ? *reinterpret_cast<const u32x2_t*>(mrow + static_cast<int64_t>(m) * p.ldmask)
-                         : u32x2_t{0u, 0u};
+      mbits[i] = m < p.M ? *reinterpret_cast<const u32x2_t*>(mrow + (ml0 + L::MSTEP * i) * 32) : u32x2_t{0u, 0u};
     }
   }
 
@@ -404,11 +410,13 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       }
     }
     if (!bwd && use_mask) {
-      uint8_t* mdst = p.mask + row0 * p.ldmask + gn / 8;
-      const int64_t mstep = static_cast<int64_t>(ROWS_PER_PASS) * p.ldmask;
-      const auto rsm = __builtin_amdgcn_make_buffer_rsrc(p.mask + static_cast<int64_t>(m0) * p.ldmask, 0, 0x7FFFFFFF,
-                                                         0x00020000);
-      const uint32_t moff0 = static_cast<uint32_t>(my_row * p.ldmask + gn / 8);
+      // tile-blocked mask: row r of the tile at +32 r, chunk c at +c — with BN = 256 the pass's
+      // 512 bytes are contiguous (offset s * 512 + tid), written as 4-B words by the quad leaders
+      uint8_t* mtile = p.mask + mask_off(m0, n0, p.ldmask);
+      uint8_t* mdst = mtile + my_row * 32 + my_chunk;
+      constexpr int mstep = ROWS_PER_PASS * 32;
+      const auto rsm = __builtin_amdgcn_make_buffer_rsrc(mtile, 0, 0x7FFFFFFF, 0x00020000);
+      const uint32_t moff0 = static_cast<uint32_t>(my_row * 32 + my_chunk);
 #pragma unroll
       for (int s = 0; s < PASSES; ++s) {
         const uint32_t byte = relu_bits8(vv[s]);  // bit b = element gn+b > 0
@@ -477,8 +485,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       const uint32_t b2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xAA, 0xF, 0xF, false));
       const uint32_t b3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(byte), 0xFF, 0xF, 0xF, false));
       if (in_range && (my_chunk & 3) == 0)
-        *reinterpret_cast<uint32_t*>(p.mask + static_cast<int64_t>(gm) * p.ldmask + gn / 8) =
-            byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
+        *reinterpret_cast<uint32_t*>(p.mask + mask_off(gm, gn, p.ldmask)) = byte | (b1 << 8) | (b2 << 16) | (b3 << 24);
     }
   }
   }  // !full_tile

@@ -396,9 +396,9 @@ hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
     if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((optimizer_kernel<false, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   } else {
-    static const bool nt = [] {  // PZ_OPT_NT=1: non-temporal state streams (A/B)
+    static const bool nt = [] {  // non-temporal state streams, on by default (PZ_OPT_NT=0: off)
       const char* e = getenv("PZ_OPT_NT");
-      return e != nullptr && atoi(e) == 1;
+      return e == nullptr || atoi(e) != 0;
     }();
     if (nt) {
       if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);

@@ -69,9 +69,14 @@ struct GemmArgs {
   EpiSpec epi;
   int64_t idx_ld;     // logical row stride used for dropout element indices (usually N)
   int force_generic;  // testing: bypass the MFMA path
-  // ReLU bitmask [M][ldmask bytes], bit (n & 7) of byte n / 8 = (y[m][n] > 0). EPI_FWD writes it
-  // (from the final stage output); EPI_BWD with act == RELU reads it INSTEAD of aux: 1/16 of
-  // the bytes of re-reading the stored bf16 activation. MFMA path only.
+  // ReLU bitmask, bit (n & 7) of byte mask_off(m, n) = (y[m][n] > 0), tile-blocked: 256 x 256
+  // element blocks of 8 KiB (256 rows of 32 B), block (m / 256, n / 256) at byte
+  // ((m / 256) * ldmask / 32 + n / 256) * 8192 — a [roundup(M, 256), ldmask] uint8 tensor with
+  // ldmask = 32 * ceil(N / 256). One 256 x 256 tile's bits are one contiguous 8 KiB run: the
+  // forward epilogue writes it as 512-B runs per store pass (a row-major [M][N/8] mask scattered
+  // them as 32-B row segments over 256 rows), and the dX epilogue's 8-B reads stay inside it.
+  // EPI_FWD writes it (from the final stage output); EPI_BWD with act == RELU reads it INSTEAD of
+  // aux: 1/16 of the bytes of re-reading the stored bf16 activation. MFMA path only.
   uint8_t* mask;
   int64_t ldmask;
   // fp8 (e4m3) operands: A/B hold e4m3 bytes; the products are dequantised by the device-side

@@ -673,8 +673,7 @@ class FusedTrainer:
                 continue
             if PF.gemm_path(nxt.buffers["g"], True, self._w(nxt), True, st.buffers["g"]) != "mfma":
                 continue
-            st.buffers["mask"] = torch.empty(rows_b * st.pos_out, PF.relu_mask_cols(st.out_width),
-                                             device=self.dev, dtype=torch.uint8)
+            st.buffers["mask"] = PF.relu_mask_empty(rows_b * st.pos_out, st.out_width, device=self.dev)
 
     # ------------------------------------------------------------------------------------
     def _keys(self, epoch: int | None) -> tuple:

@@ -104,7 +104,7 @@ def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Ten
     """``out[M,N] = op(a) @ op(b)`` with a fused epilogue.
 
     ``a_kc``: ``a`` is stored ``[M,K]`` (else ``[K,M]``); ``b_kc``: ``b`` is stored ``[N,K]`` (else ``[K,N]``).
-    ``mask`` (uint8 ``[M, relu_mask_cols(N)]``, MFMA shapes only): EPI_FWD writes the bitmask
+    ``mask`` (uint8 :func:`relu_mask_shape` ``(M, N)``, tile-blocked, MFMA shapes only): EPI_FWD writes the bitmask
     ``y > 0`` of the final output; EPI_BWD with a ReLU stage reads it instead of ``aux``.
     fp8: ``a``/``b`` may be ``float8_e4m3fn`` (both K-contiguous); products are multiplied by the
     device scalars ``scale_a * scale_b``. ``out8`` (e4m3, EPI_FWD) receives ``sat(y * out8_qscale)``
@@ -139,9 +139,35 @@ def gemm_pair_split(a0: Tensor, b0: Tensor, out0: Tensor, a1: Tensor, b1: Tensor
                                       out1.shape[1], a0.shape[0]))
 
 
-def relu_mask_cols(n: int) -> int:
-    """Bytes per row of a ReLU bitmask for ``n`` columns (padded to 64 columns)."""
-    return (n + 63) // 64 * 8
+def relu_mask_shape(m: int, n: int) -> tuple[int, int]:
+    """Shape of the tile-blocked ReLU bitmask of an ``[m, n]`` output (csrc/pz_launch.h
+    GemmArgs::mask): 256 x 256 element blocks of 8 KiB (256 rows of 32 B) in block-row-major order,
+    held as a uint8 ``[roundup(m, 256), 32 * ceil(n / 256)]`` tensor."""
+    return (m + 255) // 256 * 256, (n + 255) // 256 * 32
+
+
+def relu_mask_empty(m: int, n: int, device=None) -> Tensor:
+    return torch.empty(relu_mask_shape(m, n), device=device, dtype=torch.uint8)
+
+
+def relu_mask_bits(mask: Tensor, m: int, n: int) -> Tensor:
+    """Unpack a tile-blocked ReLU bitmask into a bool ``[m, n]`` (bit ``n & 7`` of each byte)."""
+    rows, ld = mask.shape
+    tn = ld // 32
+    rowmajor = mask.reshape(rows // 256, tn, 256, 32).permute(0, 2, 1, 3).reshape(rows, ld)
+    bits = (rowmajor.unsqueeze(-1).int() >> torch.arange(8, device=mask.device, dtype=torch.int32)) & 1
+    return bits.reshape(rows, ld * 8)[:m, :n].bool()
+
+
+def relu_mask_pack(y_pos: Tensor) -> Tensor:
+    """The tile-blocked bitmask of a bool ``[m, n]`` (inverse of :func:`relu_mask_bits`)."""
+    m, n = y_pos.shape
+    rows, ld = relu_mask_shape(m, n)
+    full = torch.zeros(rows, ld * 8, device=y_pos.device, dtype=torch.int32)
+    full[:m, :n] = y_pos.int()
+    rowmajor = (full.reshape(rows, ld, 8) << torch.arange(8, device=y_pos.device, dtype=torch.int32)).sum(-1)
+    blocked = rowmajor.to(torch.uint8).reshape(rows // 256, 256, ld // 32, 32).permute(0, 2, 1, 3)
+    return blocked.contiguous().reshape(rows, ld)
 
 
 def gemm_path(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor) -> str:

@@ -92,3 +92,23 @@ def test_forced_single_rank_context_over_gloo():
     env = dict(os.environ, PYTHONPATH=ROOT + os.pathsep + os.environ.get("PYTHONPATH", ""))
     r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, env=env, timeout=300, cwd=ROOT)
     assert r.returncode == 0 and "dist ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+
+
+@pytest.mark.parametrize("m,n", [(256, 256), (300, 264), (8192, 4096), (5, 1000)])
+def test_relu_mask_tile_blocked_layout(m, n):
+    """The tile-blocked ReLU bitmask helpers (ops/functional.py) agree with the kernels' byte
+    address (csrc/gemm_epilogue.h mask_off): element (m, n) is bit n & 7 of byte
+    (m >> 8) * 256 * ld + (n >> 8) * 8192 + (m & 255) * 32 + (n & 255) >> 3, and pack / unpack
+    round-trip."""
+    from penr_oz_neural_network_torch_amd.ops import functional as PF
+    g = torch.Generator().manual_seed(m * 7 + n)
+    pos = torch.rand(m, n, generator=g) > 0.5
+    mask = PF.relu_mask_pack(pos)
+    rows, ld = PF.relu_mask_shape(m, n)
+    assert mask.shape == (rows, ld) and mask.is_contiguous() and rows % 256 == 0 and ld % 32 == 0
+    assert torch.equal(PF.relu_mask_bits(mask, m, n), pos)
+    flat = mask.reshape(-1)
+    for _ in range(64):
+        i, j = (int(torch.randint(0, m, (1,), generator=g)), int(torch.randint(0, n, (1,), generator=g)))
+        off = (i >> 8) * 256 * ld + (j >> 8) * 8192 + (i & 255) * 32 + ((j & 255) >> 3)
+        assert bool((int(flat[off]) >> (j & 7)) & 1) == bool(pos[i, j])

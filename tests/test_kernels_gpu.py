@@ -125,7 +125,7 @@ def test_gemm_fixed_forward_kinds(native_lib, M, N, K, act, pre, post):
     bias = torch.randn(N, device=DEV)
     y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     relu = act == "relu"
-    mask = torch.zeros((M, PF.relu_mask_cols(N)), device=DEV, dtype=torch.uint8) if relu else None
+    mask = torch.zeros(PF.relu_mask_shape(M, N), device=DEV, dtype=torch.uint8) if relu else None
     epi = PF.epi_spec(act=PF.ACT_RELU if relu else PF.ACT_NONE, drop_pre=3 if pre else -1,
                       drop_post=4 if post else -1, p=p, seed=seed)
     assert PF.gemm_path(x, True, w, False, y) == "mfma"
@@ -141,8 +141,7 @@ def test_gemm_fixed_forward_kinds(native_lib, M, N, K, act, pre, post):
     assert err.max().item() < 1e-2 * ref.abs().max().item(), err.max().item()
     assert torch.equal(y == 0, ref == 0) or (y == 0).ne(ref == 0).double().mean().item() < 1e-5
     if relu:
-        bits = torch.stack([(mask[:, :N // 8].int() >> b) & 1 for b in range(8)], dim=2).reshape(M, N)
-        assert torch.equal(bits.bool(), y.float() > 0)
+        assert torch.equal(PF.relu_mask_bits(mask, M, N), y.float() > 0)
 
 
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (8192 + 64, 1024 + 64, 256), (256, 4096, 64)])
@@ -153,11 +152,10 @@ def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
     w = (torch.randn(K, N, device=DEV) / 8).to(torch.bfloat16)
     bias = torch.randn(N, device=DEV)
     y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
-    mask = torch.full((M, PF.relu_mask_cols(N)), 0xAB, device=DEV, dtype=torch.uint8)
+    mask = torch.full(PF.relu_mask_shape(M, N), 0xAB, device=DEV, dtype=torch.uint8)
     epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=3, drop_post=4, p=p, seed=seed)
     PF.gemm(x, True, w, False, y, bias=bias, mode=PF.EPI_FWD, epi=epi, mask=mask)
-    bits = torch.stack([(mask[:, :N // 8].int() >> b) & 1 for b in range(8)], dim=2).reshape(M, N)
-    assert torch.equal(bits.bool(), y.float() > 0)
+    assert torch.equal(PF.relu_mask_bits(mask, M, N), y.float() > 0)
     # backward: dX = dZ @ Wᵀ with the ReLU derivative from the bits vs from y
     gz = torch.randn(M, K, device=DEV).to(torch.bfloat16)
     wt = torch.randn(N, K, device=DEV).to(torch.bfloat16)
@@ -195,14 +193,13 @@ def test_gemm_fp8_e5m2_backward(native_lib, M, N, K):
     w8 = (torch.randn(N, K, device=DEV) * 8).to(torch.float8_e4m3fn)  # W stored [in, out] = B[n][k]
     sb = torch.tensor([1.0 / 16], device=DEV)
     y = torch.relu(torch.randn(M, N, device=DEV)).to(torch.bfloat16)
-    mask = torch.zeros(M, PF.relu_mask_cols(N), device=DEV, dtype=torch.uint8)
-    yb = (y.float() > 0).reshape(M, N // 8, 8) if N % 8 == 0 else None
+    yb = y.float() > 0 if N % 8 == 0 else None
     out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
     colsum = torch.zeros(N, device=DEV)
     epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=p, seed=seed)
     if yb is not None:  # the trainer's form: ReLU bitmask written by the forward
-        bits = (yb.int() << torch.arange(8, device=DEV, dtype=torch.int32)).sum(-1).to(torch.uint8)
-        mask[:, :N // 8] = bits
+        mask = PF.relu_mask_pack(yb)
+        assert torch.equal(PF.relu_mask_bits(mask, M, N), yb)
         PF.gemm(g8, True, w8, True, out, colsum=colsum, mode=PF.EPI_BWD, epi=epi, mask=mask, scale_a=qs[1:2],
                 scale_b=sb)
     else:
@@ -258,7 +255,7 @@ def test_gemm_fp8_forward(native_lib, M, N, K):
     y8 = torch.empty(M, N, device=DEV, dtype=f8)
     qs = torch.tensor([8.0], device=DEV)
     amax = torch.zeros(1, device=DEV)
-    mask = torch.empty(M, PF.relu_mask_cols(N), device=DEV, dtype=torch.uint8)
+    mask = PF.relu_mask_empty(M, N, device=DEV)
     epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=p, seed=seed)
     assert PF.gemm_path(x8, True, w8, True, y) == "mfma"
     PF.gemm(x8, True, w8, True, y, bias=bias, mode=PF.EPI_FWD, epi=epi, scale_a=sa, scale_b=sb, out8=y8,
@@ -273,15 +270,15 @@ def test_gemm_fp8_forward(native_lib, M, N, K):
     assert amax.item() == yf.abs().max().item()
     exp8 = (yf * 8.0).clamp(-448, 448).to(f8)
     assert (y8.view(torch.uint8) != exp8.view(torch.uint8)).float().mean().item() < 1e-4
-    bits = torch.stack([(mask[:, :N // 8].int() >> b) & 1 for b in range(8)], dim=2).reshape(M, N)
-    assert torch.equal(bits.bool(), yf > 0)
+    assert torch.equal(PF.relu_mask_bits(mask, M, N), yf > 0)
     # store_c=False (the fp8 policy's unread bf16 outputs): C untouched, side outputs identical
     y_skip = torch.full_like(y, 7.0)
     y8_skip, mask_skip, amax_skip = torch.empty_like(y8), torch.empty_like(mask), torch.zeros(1, device=DEV)
     PF.gemm(x8, True, w8, True, y_skip, bias=bias, mode=PF.EPI_FWD, epi=epi, scale_a=sa, scale_b=sb, out8=y8_skip,
             out8_qscale=qs, amax=amax_skip, mask=mask_skip, store_c=False)
     assert (y_skip == 7.0).all()
-    assert torch.equal(y8_skip.view(torch.uint8), y8.view(torch.uint8)) and torch.equal(mask_skip, mask)
+    assert torch.equal(y8_skip.view(torch.uint8), y8.view(torch.uint8))
+    assert torch.equal(PF.relu_mask_bits(mask_skip, M, N), PF.relu_mask_bits(mask, M, N))
     assert amax_skip.item() == amax.item()
 
 
@@ -302,7 +299,7 @@ def test_gemm_fp8_forward_natural_weights(native_lib, M, N, K):
     for w, kc in ((w8n, False), (w8t, True)):
         y = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
         y8 = torch.empty(M, N, device=DEV, dtype=f8)
-        mask = torch.empty(M, PF.relu_mask_cols(N), device=DEV, dtype=torch.uint8)
+        mask = PF.relu_mask_empty(M, N, device=DEV)
         amax = torch.zeros(1, device=DEV)
         assert PF.gemm_path(x8, True, w, kc, y) == "mfma"
         PF.gemm(x8, True, w, kc, y, bias=bias, mode=PF.EPI_FWD, epi=epi, scale_a=sa, scale_b=sb, out8=y8,
@@ -316,7 +313,7 @@ def test_gemm_fp8_forward_natural_weights(native_lib, M, N, K):
     assert (y.double() - ref).abs().max().item() < 0.01 * ref.abs().max().item()
     torch.testing.assert_close(y.float(), yt.float(), rtol=2 ** -7, atol=1e-3 * ref.abs().max().item())
     assert (y8.view(torch.uint8) != y8t.view(torch.uint8)).float().mean().item() < 1e-3
-    assert (mask != maskt).float().mean().item() < 1e-3
+    assert (PF.relu_mask_bits(mask, M, N) != PF.relu_mask_bits(maskt, M, N)).float().mean().item() < 1e-3
     assert abs(amax.item() - amaxt.item()) <= 2 ** -7 * amaxt.item()
 
 
@@ -327,7 +324,7 @@ def test_gemm_fp8_backward_store_c_false(native_lib, M, N, K):
     g8 = (torch.randn(M, K, device=DEV) * 100).to(torch.float8_e5m2)
     w8 = (torch.randn(N, K, device=DEV) * 8).to(torch.float8_e4m3fn)
     sa, sb = torch.tensor([1e-3], device=DEV), torch.tensor([1.0 / 16], device=DEV)
-    mask = torch.randint(0, 256, (M, PF.relu_mask_cols(N)), device=DEV, dtype=torch.uint8)
+    mask = torch.randint(0, 256, PF.relu_mask_shape(M, N), device=DEV, dtype=torch.uint8)
     epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=0.2, seed=(5, 6))
     qs = torch.tensor([4.0], device=DEV)
     outs = []
@@ -743,7 +740,7 @@ w = torch.randn(K, N, device=D).to(torch.bfloat16)
 bias = torch.randn(N, device=D)
 epi = PF.epi_spec(act=PF.ACT_RELU, drop_post=2, p=0.2, seed=(1, 2))
 y = torch.empty(M, N, device=D, dtype=torch.bfloat16)
-mask = torch.empty(M, PF.relu_mask_cols(N), device=D, dtype=torch.uint8)
+mask = PF.relu_mask_empty(M, N, device=D)
 PF.gemm(a, True, w, False, y, bias=bias, mode=PF.EPI_FWD, epi=epi, mask=mask)
 x8 = (torch.randn(M, K, device=D) * 4).to(torch.float8_e4m3fn)
 w8 = (torch.randn(K, N, device=D) * 2).to(torch.float8_e4m3fn)

@@ -82,7 +82,7 @@ def main():
         aux = torch.randn(M, N, device=dev).to(torch.bfloat16)
         colsum = torch.zeros(N, device=dev)
         epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=0.2, seed=(1, 2))
-        mask = torch.randint(0, 256, (M, PF.relu_mask_cols(N)), device=dev, dtype=torch.uint8)
+        mask = torch.randint(0, 256, PF.relu_mask_shape(M, N), device=dev, dtype=torch.uint8)
         if mode == "fwd":
             fused = lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=epi)
         elif mode == "fwd_nodrop":

@@ -133,11 +133,12 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&C, nc * 2));
     CK(hipMalloc(&bias, c.N * 4));
     CK(hipMalloc(&colsum, c.N * 4));
-    const int64_t ldmask = (c.N + 63) / 64 * 8;
-    CK(hipMalloc(&mask, c.M * ldmask));
+    const int64_t ldmask = (c.N + 255) / 256 * 32;  // tile-blocked (GemmArgs::mask)
+    const int64_t mrows = (c.M + 255) / 256 * 256;
+    CK(hipMalloc(&mask, mrows * ldmask));
     CK(hipMemset(bias, 0, c.N * 4));
     CK(hipMemset(colsum, 0, c.N * 4));
-    CK(hipMemset(mask, 0x5A, c.M * ldmask));
+    CK(hipMemset(mask, 0x5A, mrows * ldmask));
     hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, A, na, 12345u);
     hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, Bm, nb, 777u);
     GemmArgs p{};
