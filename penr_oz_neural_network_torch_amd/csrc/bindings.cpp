@@ -212,6 +212,7 @@ pz::ScaleUpd scale_upd(const optional<Tensor>& amax, const optional<Tensor>& qs,
   su.n = static_cast<int>(amax->numel());
   su.headroom = static_cast<float>(headroom);
   su.maxval = static_cast<float>(maxval);
+  su.qs_prev = nullptr;
   return su;
 }
 
@@ -406,7 +407,7 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
                   const optional<Tensor>& probs, at::IntArrayRef ei, at::ArrayRef<double> ef, int64_t idx_ld,
                   const optional<Tensor>& out8, const optional<Tensor>& out8_qscale, const optional<Tensor>& amax,
                   bool store_dh, const optional<Tensor>& su_amax, const optional<Tensor>& su_qs, double su_headroom,
-                  double su_maxval) {
+                  double su_maxval, const optional<Tensor>& su_qs_prev) {
   check_dev(logits, "logits");
   TORCH_CHECK(logits.dim() == 2 && logits.stride(1) == 1, "pz::xent_head: 2-D logits");
   TORCH_CHECK(labels.scalar_type() == at::kLong && labels.is_contiguous(), "pz::xent_head: int64 labels");
@@ -448,6 +449,12 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
   }
   a.skip_dh = store_dh ? 0 : 1;
   a.su = scale_upd(su_amax, su_qs, su_headroom, su_maxval);
+  if (su_qs_prev.has_value() && su_qs_prev->defined()) {
+    TORCH_CHECK(a.su.n > 0 && su_qs_prev->scalar_type() == at::kFloat && su_qs_prev->is_contiguous() &&
+                    su_qs_prev->numel() >= 2 * a.su.n && su_qs_prev->data_ptr<float>() != a.su.qs,
+                "pz::xent_head: su_qs_prev: fp32 qs[2n] of the current step, not su_qs itself");
+    a.su.qs_prev = su_qs_prev->data_ptr<float>();
+  }
   TORCH_CHECK((a.out8 == nullptr && !a.skip_dh) || pz::xent_head_out8_ok(a),
               "pz::xent_head: out8 / store_dh=False need the bf16 fast path (bf16, cols % 8 == 0, <= 2048, aligned)");
   PZ_HIP_CHECK(pz::xent_head(a, cur_stream(logits)));
@@ -953,7 +960,8 @@ TORCH_LIBRARY(pz, m) {
   m.def("xent_head(Tensor logits, Tensor labels, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "
         "float grad_scale, Tensor(c!)? colsum, Tensor(d!)? probs, int[] epi_i, float[] epi_f, int idx_ld, "
         "Tensor(e!)? out8=None, Tensor? out8_qscale=None, Tensor(f!)? amax=None, bool store_dh=True, "
-        "Tensor(s!)? su_amax=None, Tensor(t!)? su_qs=None, float su_headroom=1.0, float su_maxval=448.0) -> ()");
+        "Tensor(s!)? su_amax=None, Tensor(t!)? su_qs=None, float su_headroom=1.0, float su_maxval=448.0, "
+        "Tensor? su_qs_prev=None) -> ()");
   m.def("mse_head(Tensor y, Tensor target, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "
         "float grad_scale, Tensor(c!)? colsum, int[] epi_i, float[] epi_f, int idx_ld) -> ()");
   m.def("softmax_rows(Tensor x, Tensor(a!) y) -> ()");

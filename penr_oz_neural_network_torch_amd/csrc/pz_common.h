@@ -91,6 +91,9 @@ PZ_DEV void apply_scale_update(const SU& su) {
     const float q = su.maxval / (a * su.headroom);
     su.qs[2 * i] = q;
     su.qs[2 * i + 1] = 1.f / q;
+  } else if (su.qs_prev != nullptr) {
+    su.qs[2 * i] = su.qs_prev[2 * i];
+    su.qs[2 * i + 1] = su.qs_prev[2 * i + 1];
   }
   su.amax[i] = 0.f;
 }

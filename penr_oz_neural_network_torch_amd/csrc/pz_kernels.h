@@ -9,12 +9,15 @@ namespace pz {
 // ------------------------------------------------------------------ elementwise / heads
 // A folded fp8 delayed-scale update (the scale_update op inside another launch): block 0 turns
 // amax[i] into qs[2i] = q = maxval / (amax[i] * headroom), qs[2i+1] = 1/q and clears amax[i]
-// (i < n). Only for launches in which nothing reads qs or writes amax.
+// (i < n). Only for launches in which nothing reads qs or writes amax. qs_prev (optional): the
+// records in use this step when qs is the NEXT step's copy (double-buffered scales): an entry
+// with no amax this step carries its current (q, 1/q) over instead of keeping qs's stale one.
 struct ScaleUpd {
   float* amax;
   float* qs;
   int n;
   float headroom, maxval;
+  const float* qs_prev;
 };
 
 struct XentArgs {

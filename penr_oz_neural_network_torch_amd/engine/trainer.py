@@ -239,7 +239,11 @@ class FusedTrainer:
             gemms = [st for st in self.stages if st.kind == "gemm"]
             self.wqs = torch.ones(len(gemms), 2, device=self.dev)
             self.wamax = torch.zeros(len(gemms), device=self.dev)
-            self.aqs = torch.ones(len(self.stages), 2, device=self.dev)     # activations (delayed)
+            # activations (delayed), double-buffered by step parity: step t's forward quantises
+            # with, and its backward dequantises the same e4m3 copies with, _aqs_store[parity]; the
+            # head folds this step's amax into the other parity's records for step t+1
+            self._aqs_store = torch.ones(2, len(self.stages), 2, device=self.dev)
+            self.aqs = self._aqs_store[0]
             self.aamax = torch.zeros(len(self.stages), device=self.dev)
             # backward dX GEMMs: e5m2 gradients (delayed scaling, q = 57344 / (2 amax of the previous
             # step; the first step calibrates on its own amax) x e4m3 weights [in, out] (current
@@ -858,6 +862,8 @@ class FusedTrainer:
             if idx.numel() < batch:
                 raise ValueError(f"need {batch} indices, got {idx.numel()}")
         self.x_in, self.lab, self.picked = self._sample_sets[self.parity]
+        if self.fp8:
+            self.aqs = self._aqs_store[self.parity]
         pf, self._pf_ready = self._pf_ready, None
         if pf is not None and idx is None and not capture and pf[0] == (epoch, self.parity, batch, id(self.data)):
             main.wait_event(pf[1])  # gathered by the previous step's side stream (_prefetch)
@@ -904,7 +910,11 @@ class FusedTrainer:
         last = prev
         # this step's activation amax -> next step's scales: folded into the softmax head's launch
         # (nothing reads them there), else its own launch
-        self._act_su = (self.aamax, self.aqs, 1.25, 448.0) if (self.fp8 and not record) else None
+        # (into the other parity's records: this step's backward still dequantises the e4m3
+        # copies its forward wrote, the weight-gradient GEMMs' X8, with this step's)
+        self._act_su = (self.aamax, self._aqs_store[1 - self.parity], 1.25, 448.0) if (self.fp8 and not record) else None
+        if self.fp8 and record:  # (no update folded: the next step keeps this step's records)
+            self._aqs_store[1 - self.parity].copy_(self.aqs)
 
         # ---------------- head
         for ev in self._fwd_waits.values():  # (stages skipped above: record mode, no GEMM)
@@ -917,7 +927,8 @@ class FusedTrainer:
         self._g8_done = {}  # this step's e5m2 dZ copies are produced anew (the head's included)
         self._phase("pz.head")
         g_pre = self._head(last, x, batch, dropout, keys, rec)
-        if self._act_su is not None:
+        if self._act_su is not None:  # (the head did not take it)
+            self._act_su[1].copy_(self.aqs)
             ops.scale_update(self._act_su[0], self._act_su[1], self._act_su[2], True)
             self._act_su = None
         # PZ_PREFETCH_MAIN=1: the NEXT step's minibatch is gathered into the other sample set
@@ -1156,7 +1167,7 @@ class FusedTrainer:
                 self._g8_done[k] = g
             if self._act_su is not None:
                 kw8.update(su_amax=self._act_su[0], su_qs=self._act_su[1], su_headroom=self._act_su[2],
-                           su_maxval=self._act_su[3])
+                           su_maxval=self._act_su[3], su_qs_prev=self.aqs)
                 self._act_su = None
             ops.xent_head(y, self.lab, batch, self.loss_slot, 1.0 / gb, g, 1.0 / gb,
                           bias_grad if fuse else None, probs, ei, ef, 0, **kw8)
@@ -1278,9 +1289,10 @@ class FusedTrainer:
         """Paired backward (PZ_DW_PAIR): the side-stream updates wait for the step's last launch
         (the first-layer / bias update on the main stream, which then has the HBM to itself right
         behind the pair) and run beside the NEXT step's first forward GEMMs, each forward stage
-        waiting only for its own weight's update (PZ_PAIR_SIDE=0: flushed as before)."""
+        waiting only for its own weight's update. Off by default (PZ_PAIR_SIDE=1: on): r4, one box,
+        mlp4 1.1157 / 1.1181 ms on vs 1.1011 / 1.1002 off; fp8 mlp8192 0.5229 / 0.526 vs 0.5214 / 0.5192."""
         return (self._pair_idx is not None and self._ov is not None
-                and os.environ.get("PZ_PAIR_SIDE", "1") == "1")
+                and os.environ.get("PZ_PAIR_SIDE", "0") == "1")
 
     def _run_pair(self, paired, st0: Stage, x0, g0, w0, f8_0, handles):
         """The first layer's dW GEMM together with the deferred partner's (``_pair_idx``) in one

@@ -26,6 +26,7 @@ def main():
     keep = sys.argv[2:] or ["gemm_mfma", "Cijk"]
     acc = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
+    passes = collections.defaultdict(lambda: collections.defaultdict(set))
     for db in sorted(glob.glob(os.path.join(root, "**", "*.db"), recursive=True)):
         con = sqlite3.connect(db)
         rows = list(con.execute("select dispatch_id, kernel_name, grid_size, counter_name, value "
@@ -46,11 +47,13 @@ def main():
             key = (run, short(kname), int(grid))
             acc[key][cname] += float(val)
             disp[key].add((db, did))
+            passes[key][cname].add(db)
     hdr = f"{'kernel':60} {'grid':>8} {'disp':>5} {'MFMA':>6} {'WAIT_ANY':>8} {'WAIT_INST':>9} {'WAIT_LDS':>8} " \
           f"{'ACTIVE':>6} {'LDS instr/disp':>14} {'bank confl/disp':>15}"
     print(hdr)
     for key in sorted(acc):
-        c = acc[key]
+        # a counter collected in several passes (GRBM_GUI_ACTIVE rides along in each): per-pass mean
+        c = {k: v / len(passes[key][k]) for k, v in acc[key].items()}
         n = len(disp[key]) // max(1, len({d for d, _ in disp[key]}))
         wc = c.get("SQ_WAVE_CYCLES", 0.0) or float("nan")
         gui = c.get("GRBM_GUI_ACTIVE", 0.0)
