@@ -322,7 +322,11 @@ class FusedTrainer:
         self._fuse_ok: dict = {}
         self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
         self._after_dx = os.environ.get("PZ_OPT_AFTER_DX", "1") == "1"  # measured 0.6% faster on one GPU
-        self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "2")))  # first-layer dW under DP
+        # first-layer dW under DP in row chunks (chunk c's bucket travels while chunk c+1 runs).
+        # Off by default: the chunk GEMMs ([512, 4096] x K 8192 on mlp4) need split-K 8 and took
+        # 71 + 80 us against 76 us for the whole dW (r4 step profile at world 1), more than the
+        # half bucket they hide (8 MB bf16 over an 8-rank ring: ~25 us at 300 GB/s)
+        self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "1")))
         self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
         # PZ_OPT_MERGE=1: the side-stream updates of all layers but the first are queued together
         # behind the last of their gradients (one event instead of one per layer). Default on:
@@ -1238,8 +1242,8 @@ class FusedTrainer:
             return out
         w_grad = self._w_grad(st.seg_w)
         # Data parallel: the first layer's gradient is the last bucket of the backward and nothing
-        # is left to hide its all-reduce behind, so its dW GEMM runs in row chunks and chunk c's
-        # all-reduce travels while chunk c+1 is computed (only the last chunk's is exposed)
+        # is left to hide its all-reduce behind; PZ_DW_CHUNKS=c runs its dW GEMM in c row chunks so
+        # chunk i's all-reduce travels while chunk i+1 is computed (off by default, see __init__)
         chunks = self._dw_chunk_count(st)
         mine = []
         rows = w_grad.shape[0] // chunks

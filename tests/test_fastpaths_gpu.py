@@ -375,7 +375,8 @@ def _model8():
 
 
 def _rank8(rank, world, store, out_path):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world))
+    # (chunking is off by default since r4 — it cost more GEMM time than it hid — so it is asked for)
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), PZ_DW_CHUNKS="2")
     torch.set_num_threads(2)
     dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
