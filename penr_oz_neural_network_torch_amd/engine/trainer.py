@@ -40,6 +40,7 @@ import torch
 from ..ops import functional as PF
 from ..ops import native
 from ..parallel.dist import DataParallelContext, get_context
+from .events import StreamEvents
 from .optim import FusedOptimizer
 
 ROW_PAD = 64  # batch rows padded to the GEMM K-tile so dW = XᵀdZ stays on the MFMA path
@@ -403,7 +404,11 @@ class FusedTrainer:
         self._warm: set = set()
         self._graph_pool = None
         self._last_event = None
-        self._pending: list = []   # (epoch, ratio_row or None, event)
+        self._capturing = False
+        self._pending: list = []   # (epoch, ratio_row or None, timestamp event)
+        # device-scope ordering events + fence-free step timestamps (engine/events.py): a default
+        # torch event's system-scope fence idled the compute stream ~7 us per record / wait
+        self.events = StreamEvents(self.dev)
         self._drained = 0
         self._record = None
         self.data = None
@@ -565,10 +570,10 @@ class FusedTrainer:
         behind their gradients: ONE event recorded on the compute stream for all of them (each
         record / cross-stream wait costs the compute stream a few microseconds of idle)."""
         main, l2, scale = self._ov
-        ready = torch.cuda.Event()
+        ready = self.events.sync(self._capturing)
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
-            self.opt_stream.wait_event(ready)
+            ready.wait(self.opt_stream)
             if self._pf_args is not None:
                 self._prefetch()
             for key, handles, stages in items:
@@ -588,7 +593,7 @@ class FusedTrainer:
         seed = self._gather_seed(epoch)
         torch.ops.pz.gather_rows(self.data, None, seed[0], seed[1], x, batch, self.labels, lab, picked, None, None,
                                  None)
-        ev = torch.cuda.Event()
+        ev = self.events.sync(self._capturing)
         ev.record(torch.cuda.current_stream(self.dev))
         self._pf_ready = ((epoch, sel, batch, id(self.data)), ev)
 
@@ -805,10 +810,10 @@ class FusedTrainer:
     def _replay(self, gkey, epoch: int, lr: float, batch: int, dropout: float, l2: float, row) -> None:
         main = torch.cuda.current_stream(self.dev)
         if self._opt_done is not None:
-            main.wait_event(self._opt_done)
+            self._opt_done.wait(main)
             self._opt_done = None
         for ev in self._fwd_waits.values():
-            main.wait_event(ev)
+            ev.wait(main)
         self._fwd_waits = {}
         self._early_done = None
         if self._ctr_epoch != epoch:
@@ -830,16 +835,15 @@ class FusedTrainer:
             self.parity = parity  # capture does not execute: the replay below runs this epoch
         self.opt.begin_step(lr)  # host bookkeeping only (step counter, param_group lr)
         graph.replay()
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record(main)
         self.parity = 1 - parity
-        self._pending.append((epoch, row, ev))
+        self._pending.append((epoch, row, self.events.stamp(main)))
 
     def _run(self, epoch: int | None, lr: float, batch: int, dropout: float, l2: float, row: int, record: bool,
              indices: torch.Tensor | None) -> None:
         """Enqueue one step. ``epoch=None``: hipGraph capture (epoch-dependent values from the
         device counter / tables; the side stream joins the capture stream at the end)."""
         capture = epoch is None
+        self._capturing = capture  # (torch events inside a capture: engine/events.py)
         self._run_epoch = epoch  # None while a hipGraph is captured
         keys = self._keys(epoch)
         ops = torch.ops.pz
@@ -870,7 +874,7 @@ class FusedTrainer:
             self.aqs = self._aqs_store[self.parity]
         pf, self._pf_ready = self._pf_ready, None
         if pf is not None and idx is None and not capture and pf[0] == (epoch, self.parity, batch, id(self.data)):
-            main.wait_event(pf[1])  # gathered by the previous step's side stream (_prefetch)
+            pf[1].wait(main)  # gathered by the previous step's side stream (_prefetch)
             self.prefetched_steps += 1
         else:
             # the previous step's gradient amax -> this step's e5m2 scales rides on the gather
@@ -904,11 +908,11 @@ class FusedTrainer:
         prev = None
         for st in self.stages:
             if self._early_done is not None and st.kind == "gemm" and st.seg_w.offset in self._early_keys:
-                main.wait_event(self._early_done)
+                self._early_done.wait(main)
                 self._early_done = self._opt_done = None
             ev = self._fwd_waits.pop(st.index, None)
             if ev is not None:  # reordered backward: this stage's weights were updated on the side stream
-                main.wait_event(ev)
+                ev.wait(main)
             x = self._forward_stage(st, x, batch, dropout, keys, rec)
             prev = st
         last = prev
@@ -922,10 +926,10 @@ class FusedTrainer:
 
         # ---------------- head
         for ev in self._fwd_waits.values():  # (stages skipped above: record mode, no GEMM)
-            main.wait_event(ev)
+            ev.wait(main)
         self._fwd_waits = {}
         if self._opt_done is not None:
-            main.wait_event(self._opt_done)
+            self._opt_done.wait(main)
             self._opt_done = None
         self._early_done = None
         self._g8_done = {}  # this step's e5m2 dZ copies are produced anew (the head's included)
@@ -991,11 +995,11 @@ class FusedTrainer:
                 for st in self._late_stages:
                     self._refresh_fp8_weights(st, 1 - self.parity)
             self._ov = None
-            rest_ev = torch.cuda.Event()
+            rest_ev = self.events.sync(capture)
             rest_ev.record(main)
             fwd_waits = {}
             with torch.cuda.stream(self.opt_stream):
-                self.opt_stream.wait_event(rest_ev)
+                rest_ev.wait(self.opt_stream)
                 for key, hs, stages in late_side:  # paired backward: one event per updated weight
                     for h in hs:
                         self.ctx.wait_one(h)
@@ -1004,7 +1008,7 @@ class FusedTrainer:
                         for st in stages:
                             self._refresh_fp8_weights(st, 1 - self.parity)
                     if not capture:
-                        wev = torch.cuda.Event()
+                        wev = self.events.sync()
                         wev.record(self.opt_stream)
                         for st in stages:
                             fwd_waits[st.index] = wev
@@ -1018,10 +1022,10 @@ class FusedTrainer:
                 self._deferred = []
                 self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
-                ev = torch.cuda.Event(enable_timing=not capture)
+                ev = self.events.sync(capture)
                 ev.record(self.opt_stream)
             if capture:  # join the side stream into the capture stream
-                main.wait_event(ev)
+                ev.wait(main)
             else:
                 # ONE cross-stream wait in the next step, before the first GEMM that reads a
                 # side-stream-updated weight: step_finalize (behind this stream's first-layer
@@ -1030,7 +1034,7 @@ class FusedTrainer:
                 self._opt_done = ev
                 self._early_done = None if after_rest else ev
                 self._fwd_waits = fwd_waits
-                self._last_event = ev
+                self._last_event = self.events.stamp(self.opt_stream)
             self.parity = 1 - self.parity
             self._phase(None)
             return
@@ -1042,9 +1046,7 @@ class FusedTrainer:
         if self.fp8:
             self._refresh_fp8_weights(parity=self.parity)
         self.opt.finalize(self.loss_slot, 1, l2, self.costs, epoch, self.ratios, row, **fin)
-        ev = torch.cuda.Event(enable_timing=True)
-        ev.record()
-        self._last_event = ev
+        self._last_event = self.events.stamp(torch.cuda.current_stream(self.dev))
         self._phase(None)
 
     _in_phase = False
@@ -1343,15 +1345,15 @@ class FusedTrainer:
             self._side_pending = []
         for h in list(self._late_handles) + [handles[-1]]:
             self.ctx.wait_one(h)
-        ready = torch.cuda.Event()
+        ready = self.events.sync(capture)
         ready.record(main)  # the dX chain (bias column sums) and the first layer's dW are done
         with torch.cuda.stream(self.opt_stream):
-            self.opt_stream.wait_event(ready)
+            ready.wait(self.opt_stream)
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
             if self.fp8:
                 for s0 in self._late_stages:
                     self._refresh_fp8_weights(s0, 1 - self.parity)
-            rest_ev = torch.cuda.Event()
+            rest_ev = self.events.sync(capture)
             rest_ev.record(self.opt_stream)
         w_grad = self._w_grad(st.seg_w)
         f8 = self._fp8_dw(st, g, w_grad)
@@ -1364,16 +1366,16 @@ class FusedTrainer:
         self._ov = None
         with torch.cuda.stream(self.opt_stream):
             self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row, **fin)
-            ev = torch.cuda.Event(enable_timing=not capture)
+            ev = self.events.sync(capture)
             ev.record(self.opt_stream)
         if capture:  # join the side stream into the capture stream
-            main.wait_event(ev)
+            ev.wait(main)
         else:
             # stage 0 reads first-layer / embedding / batchnorm parameters of the rest group
             self._fwd_waits = {0: rest_ev, st.index: ev}
             self._opt_done = ev  # (the head: loss-slot reset by step_finalize)
             self._early_done = None
-            self._last_event = ev
+            self._last_event = self.events.stamp(self.opt_stream)
         self.parity = 1 - self.parity
         self._phase(None)
 
@@ -1583,8 +1585,8 @@ class FusedTrainer:
         self.ratios = torch.zeros(points * max(1, self.opt.nslots), device=self.dev, dtype=torch.float32)
         self._ratio_rows = 0
         self._pending = []
-        self._start_event = torch.cuda.Event(enable_timing=True)
-        self._start_event.record()
+        self.events.release()
+        self._start_event = self.events.stamp(torch.cuda.current_stream(self.dev))
         self._last_ms = 0.0
         self.step_ms = {}
         torch.cuda.synchronize(self.dev)
@@ -1600,13 +1602,14 @@ class FusedTrainer:
         out = []
         self.step_ms = {}  # epoch -> GPU time since the previous step ended (ms), for telemetry
         for epoch, row, ev in self._pending:
-            ms = self._start_event.elapsed_time(ev)
+            ms = self.events.elapsed(self._start_event, ev)
             when = (self._start_wall + timedelta(milliseconds=ms)).isoformat()
             r = ratios[row][:self.opt.nslots] if row is not None else None
             out.append((epoch, costs[epoch], r, when))
             self.step_ms[epoch] = ms - self._last_ms
             self._last_ms = ms
         self._pending = []
+        self.events.release(keep=self._start_event)  # (read: the step timestamps can go)
         self.opt.sync_torch_state()
         return out
 
