@@ -86,6 +86,9 @@ def _metric_label(key: str, cfg: dict) -> str:
     return f"training samples/sec (whole node), {cfg['name']}, {DTYPE_LABEL[cfg['dtype']]} on MI355X"
 
 
+_JSON_FD = None  # the original stdout (main() points fd 1 at stderr)
+
+
 def log(msg: str) -> None:
     print(f"[bench] {msg}", file=sys.stderr, flush=True)
 
@@ -137,7 +140,7 @@ def _emit(args, cfg, world, elapsed, costs, batch, ctx) -> None:
     if ctx.rank != 0:
         return
     log(f"cost first/last = {costs[0]:.4f} / {costs[-1]:.4f}, finite={finite}")
-    print(json.dumps({
+    line = json.dumps({
         "metric": _metric_label(args.config, cfg),
         "value": round(value, 1),
         "unit": "samples/s",
@@ -160,7 +163,11 @@ def _emit(args, cfg, world, elapsed, costs, batch, ctx) -> None:
                    # fp32 = exact fp32 gradients into the fp32-master Adam)
                    "grad_dtype": os.environ.get("PZ_GRAD_DTYPE", "bf16") if cfg["dtype"] in ("bfloat16", "fp8")
                    else DTYPE_LABEL[cfg["dtype"]]},
-    }), flush=True)
+    })
+    if _JSON_FD is None:
+        print(line, flush=True)
+    else:
+        os.write(_JSON_FD, (line + "\n").encode())
 
 
 def _bench_autograd(args, cfg, model, ctx, batch, local) -> int:
@@ -263,6 +270,12 @@ def main(argv=None) -> int:
     args = ap.parse_args(raw)
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         return _launch_ranks(args.gpus, raw)
+    # stdout carries exactly ONE line, the JSON result: everything else written to fd 1 — RCCL's
+    # version banner from its C library included — goes to stderr from here on
+    global _JSON_FD
+    sys.stdout.flush()
+    _JSON_FD = os.dup(1)
+    os.dup2(2, 1)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
