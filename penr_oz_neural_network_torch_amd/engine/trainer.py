@@ -296,6 +296,11 @@ class FusedTrainer:
         # a GEMM's pending ones); within noise of priority 0 (profiles/r2_ab_opt_sched.txt)
         prio = int(os.environ.get("PZ_OPT_PRIO", "0"))
         self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
+        # PZ_OPT_SERIAL=1 (one process): the overlap schedule's update launches (grouping, pairing,
+        # order) enqueued on the COMPUTE stream where they fall, with no cross-stream events: every
+        # record / wait costs the compute stream ~7 us of packet processing (r4 step timeline), and
+        # an update beside a one-tile-per-CU GEMM slows the GEMM by about its own duration anyway
+        self._serial = False
         self._g8_done: dict = {}  # stage index -> the dZ tensor whose e5m2 copy is current this step
         self._g8_epi_ready: set = set()  # stages whose epilogue-written e5m2 dZ scale is calibrated
         self._y_dead_cache: dict = {}  # fp8 policy: which bf16 GEMM outputs go unwritten (_y_dead)
@@ -382,6 +387,8 @@ class FusedTrainer:
             if cands:
                 self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
         self._pair_dw = None       # (stage, x_in, dZ) of the dW GEMM that waits for its partner
+        self._serial = (self.overlap and not self.ctx.enabled and self._late_idx is None
+                        and os.environ.get("PZ_OPT_SERIAL", "0") == "1")
         self._fwd_waits: dict = {}  # stage index -> event the next step's forward waits for
         self._pf_args = None       # (epoch, parity, batch) of the sample _prefetch gathers next
         self._pf_ready = None      # ((epoch, parity, batch, data id), event) of a gathered sample
@@ -570,6 +577,13 @@ class FusedTrainer:
         behind their gradients: ONE event recorded on the compute stream for all of them (each
         record / cross-stream wait costs the compute stream a few microseconds of idle)."""
         main, l2, scale = self._ov
+        if self._serial:  # in stream order on the compute stream (no events)
+            for key, handles, stages in items:
+                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity, max_grid)
+                if self.fp8:
+                    for st in stages:
+                        self._refresh_fp8_weights(st, 1 - self.parity)
+            return
         ready = self.events.sync(self._capturing)
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
@@ -995,6 +1009,22 @@ class FusedTrainer:
                 for st in self._late_stages:
                     self._refresh_fp8_weights(st, 1 - self.parity)
             self._ov = None
+            if self._serial:
+                for key, hs, stages in late_side + self._deferred:
+                    self.opt.step_group(key, self.grads, l2, 1.0, 1 - self.parity)
+                    if self.fp8:
+                        for st in stages:
+                            self._refresh_fp8_weights(st, 1 - self.parity)
+                self._deferred = []
+                self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row,
+                                  **fin)
+                self._opt_done = self._early_done = None
+                self._fwd_waits = {}
+                if not capture:
+                    self._last_event = self.events.stamp(main)
+                self.parity = 1 - self.parity
+                self._phase(None)
+                return
             rest_ev = self.events.sync(capture)
             rest_ev.record(main)
             fwd_waits = {}
