@@ -87,3 +87,11 @@ class StreamEvents:
         for ev in self._ring:
             torch.ops.pz.event_destroy(ev.h)
         self._ring = []
+
+    def __del__(self):  # (a trainer dropped without close(); nothing to do at interpreter exit)
+        try:
+            if self._ring or self._stamps:
+                torch.cuda.synchronize(self.dev)
+                self.close()
+        except Exception:
+            pass

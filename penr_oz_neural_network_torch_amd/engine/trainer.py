@@ -1648,6 +1648,11 @@ class FusedTrainer:
             raise RuntimeError("no record-mode step has run")
         return self._record
 
+    def close(self) -> None:
+        """Release the trainer's HIP events (after its last drain)."""
+        torch.cuda.synchronize(self.dev)
+        self.events.close()
+
     # convenience for benchmarks / tests --------------------------------------------------
     def synchronize(self) -> None:
         torch.cuda.synchronize(self.dev)

@@ -319,7 +319,10 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         try:
             trainer = self._fused_trainer() if self.on_gpu else None
             if trainer is not None:
-                self._train_fused(trainer, data, **hp)
+                try:
+                    self._train_fused(trainer, data, **hp)
+                finally:
+                    trainer.close()  # its HIP events (engine/events.py)
             else:
                 self._train_autograd(data, **hp)
         except Exception:

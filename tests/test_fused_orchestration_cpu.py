@@ -59,6 +59,9 @@ class FakeTrainer:
     def record(self):
         return self._rec
 
+    def close(self):
+        self.closed = True
+
 
 def test_fused_orchestration_schedule_progress_and_stats(models_tmpdir, monkeypatch):
     fakes = []
