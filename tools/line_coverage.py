@@ -101,6 +101,12 @@ def main(argv: list[str]) -> int:
     os.environ["PZ_LINECOV_DIR"] = sub_dir
     os.environ["PZ_LINECOV_FILES"] = json.dumps(sorted(files))
     os.environ["PYTHONPATH"] = hook + (os.pathsep + os.environ["PYTHONPATH"] if os.environ.get("PYTHONPATH") else "")
+    if os.environ.get("PZ_COV_GPU") == "1":
+        # autograd runs CUDA backward passes on its own device threads, created in C++ where
+        # threading.settrace never reaches: the GPU autograd Functions' backward() lines would read
+        # as unexecuted. Single-threaded autograd runs them on the calling (traced) thread.
+        import torch
+        torch.autograd.set_multithreading_enabled(False)
     sys.settrace(global_tracer)
     threading.settrace(global_tracer)
     try:
