@@ -340,6 +340,9 @@ class FusedTrainer:
         # deep16x8192 (SGD) within noise. PZ_OPT_MERGE=0 queues one update per layer.
         self._merge_side = os.environ.get("PZ_OPT_MERGE", "1") == "1"
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
+        # PZ_OPT_SIDE_GRID=G (> 0): the merged side-stream update runs on at most G workgroups, a
+        # smaller share of the HBM beside the step-boundary launches on the compute stream (A/B)
+        self._side_grid = int(os.environ.get("PZ_OPT_SIDE_GRID", "0"))
         # PZ_OPT_TRICKLE=G (> 0): the LARGEST side-updated weight is updated right behind its dW
         # GEMM by a G-workgroup launch that streams beside the remaining backward GEMMs (a few CUs'
         # worth of HBM traffic) instead of joining the merged updates after the last dX GEMM
@@ -1000,7 +1003,7 @@ class FusedTrainer:
             after_rest = self._side_after_rest()
             late_side = sorted(self._side_pending, key=lambda it: it[2][0].index) if after_rest else []
             if self._side_pending and not after_rest:  # (merged side updates not flushed by their last layer)
-                self._opt_async(self._side_pending)
+                self._opt_async(self._side_pending, self._side_grid)
             self._side_pending = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
@@ -1317,7 +1320,7 @@ class FusedTrainer:
             (self._deferred if st.seg_w.offset == self._defer_key else self._side_pending).append(item)
             if ((not self._merge_side or st.seg_w.offset == self._flush_key) and self._side_pending
                     and not self._side_after_rest()):
-                self._opt_async(self._side_pending)
+                self._opt_async(self._side_pending, self._side_grid)
                 self._side_pending = []
         return out
 
@@ -1615,6 +1618,7 @@ class FusedTrainer:
         self.ratios = torch.zeros(points * max(1, self.opt.nslots), device=self.dev, dtype=torch.float32)
         self._ratio_rows = 0
         self._pending = []
+        torch.cuda.synchronize(self.dev)  # (the previous run's stamps have completed)
         self.events.release()
         self._start_event = self.events.stamp(torch.cuda.current_stream(self.dev))
         self._last_ms = 0.0
