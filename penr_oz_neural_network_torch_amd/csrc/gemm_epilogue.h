@@ -246,20 +246,7 @@ PZ_DEV int64_t mask_off(int64_t m, int n, int64_t ldmask) {
   return (m >> 8) * 256 * ldmask + static_cast<int64_t>(n >> 8) * 8192 + (m & 255) * 32 + ((n & 255) >> 3);
 }
 
-// D8 (fp8 policy, the bf16 output itself not stored: GemmArgs C == nullptr with an out8 copy): the
-// e4m3 (forward) / e5m2 (backward dZ) copy is converted straight from the fp32 stage values into an
-// fp8 LDS image — one rounding instead of fp32 -> bf16 -> fp8, no bf16 pack / unpack — and the
-// forward's ReLU bits go to a nibble image (4 columns per byte) that the store pass pairs into
-// mask bytes; |y| max from the fp32 values. The store pass only copies. (r4: the fp8 forward
-// GEMMs spent ~40% of a tile in the epilogue, most of it VALU on the bf16 round trip.)
-template <int BN>
-PZ_DEV uint32_t i8img_off(int r, int col) {  // byte offset of fp8 element (r, col), col % 4 == 0
-  constexpr int CH = BN / 16;  // 16-B chunks per row
-  return static_cast<uint32_t>(r * BN + (((col >> 4) ^ (r & (CH - 1))) << 4) + (col & 15));
-}
-
-template <int BM, int BN, int WM, int WN, class L, bool FWD_ONLY = false, int EK = EK_ANY, bool D8 = false,
-          class Acc>
+template <int BM, int BN, int WM, int WN, class L, bool FWD_ONLY = false, int EK = EK_ANY, class Acc>
 PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0, int n0, int wm, int wn, int lane,
                          float alpha) {
   constexpr int NT = WM * WN * 64;
@@ -330,12 +317,6 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   const float rd_m1 = relu_on && both ? e.scale * e.scale : (e.drop_pre ? e.scale : 1.f);
   const float rd_m2 = relu_on && both ? 1.f : (e.drop_post ? e.scale : 1.f);
   const float fixed_sc = (ek_pre(EK) ? e.scale : 1.f) * (ek_post(EK) ? e.scale : 1.f);
-  constexpr int NIB_PITCH = BN / 4 + 4;  // odd dword count per row: 32 rows' nibble bytes on 32 banks
-  constexpr int NIB_BASE = BM * BN;      // behind the fp8 image
-  static_assert(!D8 || NIB_BASE + BM * NIB_PITCH <= BM * BN * 2, "D8 images fit where the bf16 image was");
-  float qs8 = 1.f, amax8 = 0.f;
-  if constexpr (D8) qs8 = *p.out8_qscale;
-  const bool d8_mask = D8 && !bwd && p.mask != nullptr;
   static_for<ROWS>([&](auto ic) {
     constexpr int i = decltype(ic)::value;
     const int ml = ml0 + L::MSTEP * i;
@@ -371,38 +352,10 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
       if (e.act != ACT_NONE) act_bwd_row<BN, L>(v, smem, ml, nl0, e.act, e.drop_post ? e.inv_scale : 1.f);
       if (e.drop_pre) dropout_row<L>(v, e, e.key_pre, pr_row);
     }
-    if constexpr (D8) {
-      const bool row_ok = m0 + ml < p.M;
 #pragma unroll
-      for (int j = 0; j < COLS; ++j) {
-        const int col = nl0 + L::n_off(j);
-        float c[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          if (row_ok && n0 + col + r < p.N) amax8 = fmaxf(amax8, fabsf(v[j][r]));
-          c[r] = bwd ? fminf(fmaxf(v[j][r] * qs8, -57344.f), 57344.f) : fminf(fmaxf(v[j][r] * qs8, -448.f), 448.f);
-        }
-        int w;
-        if (bwd) {
-          w = __builtin_amdgcn_cvt_pk_bf8_f32(c[0], c[1], 0, false);
-          w = __builtin_amdgcn_cvt_pk_bf8_f32(c[2], c[3], w, true);
-        } else {
-          w = __builtin_amdgcn_cvt_pk_fp8_f32(c[0], c[1], 0, false);
-          w = __builtin_amdgcn_cvt_pk_fp8_f32(c[2], c[3], w, true);
-        }
-        *reinterpret_cast<PZ_LDS int*>(smem + i8img_off<BN>(ml, col)) = w;
-        if (d8_mask) {
-          const uint32_t nib = (v[j][0] > 0.f ? 1u : 0u) | (v[j][1] > 0.f ? 2u : 0u) | (v[j][2] > 0.f ? 4u : 0u) |
-                               (v[j][3] > 0.f ? 8u : 0u);
-          *reinterpret_cast<PZ_LDS uint8_t*>(smem + NIB_BASE + ml * NIB_PITCH + (col >> 2)) = static_cast<uint8_t>(nib);
-        }
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < COLS; ++j)
-        *reinterpret_cast<PZ_LDS u32x2_t*>(smem + cimg_off<BN>(ml, nl0 + L::n_off(j))) =
-            u32x2_t{pack_bf2(v[j][0], v[j][1]), pack_bf2(v[j][2], v[j][3])};
-    }
+    for (int j = 0; j < COLS; ++j)
+      *reinterpret_cast<PZ_LDS u32x2_t*>(smem + cimg_off<BN>(ml, nl0 + L::n_off(j))) =
+          u32x2_t{pack_bf2(v[j][0], v[j][1]), pack_bf2(v[j][2], v[j][3])};
     if (kColsum && p.colsum != nullptr && m0 + ml < p.M) {
 #pragma unroll
       for (int j = 0; j < COLS; ++j) cs[j] += v[j];
@@ -430,41 +383,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   // from one base address advanced by a constant stride. The generic per-pass loop below waited
   // on each ds_read before its store and recomputed a 64-bit row address (two quarter-rate
   // multiplies) per pass behind per-pass range branches.
-  const bool full_tile = !D8 && EK != EK_ANY && m0 + BM <= p.M && n0 + BN <= p.N;
-  if constexpr (D8) {
-    // fp8 image -> out8 (16-B row segments), nibble image -> tile-blocked mask words
-    constexpr int I8_CH = BN / 16;
-    constexpr int PER = BM * I8_CH / NT;
-    static_assert(PER * NT == BM * I8_CH, "D8 copy split");
-#pragma unroll
-    for (int s8 = 0; s8 < PER; ++s8) {
-      const int q = s8 * NT + tid;
-      const int r = q / I8_CH, c = q % I8_CH;
-      const u32x4_t v = *reinterpret_cast<const PZ_LDS u32x4_t*>(smem + i8img_off<BN>(r, c * 16));
-      const int gm = m0 + r, gn = n0 + c * 16;
-      if (gm < p.M && gn < p.N) *reinterpret_cast<u32x4_t*>(p.out8 + static_cast<int64_t>(gm) * p.ldout8 + gn) = v;
-    }
-    if (d8_mask) {
-      constexpr int WPR = BN / 32;  // mask words (32 columns) per row
-      constexpr int PERW = BM * WPR / NT;
-      static_assert(PERW * NT == BM * WPR, "D8 mask split");
-#pragma unroll
-      for (int s8 = 0; s8 < PERW; ++s8) {
-        const int q = s8 * NT + tid;
-        const int r = q / WPR, w = q % WPR;
-        const PZ_LDS char* nb = smem + NIB_BASE + r * NIB_PITCH + 8 * w;
-        // 8 nibble bytes n0..n7 -> mask bytes n0 | n1 << 4, n2 | n3 << 4, ...: t = x | x >> 4 puts
-        // the pairs in bytes 0 and 2 of each half
-        const uint32_t lo = *reinterpret_cast<const PZ_LDS uint32_t*>(nb);
-        const uint32_t hi = *reinterpret_cast<const PZ_LDS uint32_t*>(nb + 4);
-        const uint32_t tl = lo | (lo >> 4), th = hi | (hi >> 4);
-        const uint32_t word = (tl & 0xFFu) | ((tl >> 8) & 0xFF00u) | ((th & 0xFFu) << 16) | ((th << 8) & 0xFF000000u);
-        const int gm = m0 + r, gn = n0 + 32 * w;
-        if (gm < p.M && gn < p.N) *reinterpret_cast<uint32_t*>(p.mask + mask_off(gm, gn, p.ldmask)) = word;
-      }
-    }
-    amax = amax8;
-  }
+  const bool full_tile = EK != EK_ANY && m0 + BM <= p.M && n0 + BN <= p.N;
   if (full_tile) {
     u32x4_t vv[PASSES];
 #pragma unroll
@@ -535,7 +454,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   // ragged tiles (and the generic kind): one pass at a time with range checks; the fixed forward
   // kinds keep it rolled by 4 (it indexes no accumulator)
   constexpr int kStoreUnroll = ek_fixed(EK) ? 4 : PASSES;
-  if (!D8 && !full_tile) {
+  if (!full_tile) {
 #pragma unroll kStoreUnroll
   for (int s = 0; s < PASSES; ++s) {
     const int r = s * ROWS_PER_PASS + my_row;

@@ -985,18 +985,8 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
   const int g4 = 4 * (lane >> 4);
   if constexpr (ACC32) {
     const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
-    // the bf16 output unstored and an fp8 copy wanted (the fp8 policy's dead bf16 tensors): the copy
-    // straight from fp32 (epilogue_lds D8); uniform per launch
-    constexpr bool kD8 = F8 && EK != EK_STORE && EK != EK_ANY;
-    const bool d8 = kD8 && p.d8 != 0 && p.C == nullptr && p.out8 != nullptr && p.out8_qscale != nullptr && p.ldout8 % 16 == 0 &&
-                    (reinterpret_cast<uintptr_t>(p.out8) & 15) == 0 && p.out8_fmt == (p.epi_mode == EPI_BWD ? 1 : 0);
-    if constexpr (F8_BWD || M32) {
-      if (d8) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, false, EK, kD8>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
-      else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
-    } else {
-      if (d8) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true, EK, kD8>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
-      else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true, EK>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
-    }
+    if constexpr (F8_BWD || M32) epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+    else epilogue_lds<BM, BN, WM, WN, Lay32<TM8, TN8>, true, EK>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
   } else if constexpr (std::is_same<OutT, uint16_t>::value) {
     epilogue_lds<BM, BN, WM, WN, Lay16<C::TM, C::TN>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
   } else if (p.epi_mode == EPI_OPT) {
@@ -1482,11 +1472,6 @@ hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
 hipError_t gemm_mfma(const GemmArgs& in, hipStream_t s) {
   GemmArgs p = in;
   p.store_wt = store_wt_default();
-  static const int d8_on = [] {
-    const char* e = getenv("PZ_F8_D8");
-    return e != nullptr ? atoi(e) : 1;
-  }();
-  p.d8 = d8_on;
   if (p.split_k > 1 && (p.ws == nullptr || p.counters == nullptr)) return hipErrorInvalidValue;
   if (p.in_dtype == DT_FP8) return launch_fp8(p, s);
   if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);

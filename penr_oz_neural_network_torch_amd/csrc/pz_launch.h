@@ -105,9 +105,6 @@ struct GemmArgs {
   // kernel left dirty in the XCD L2s (~B / 6 TB/s for B dirty bytes, MI355X_MICROARCH "boundary"),
   // and a GEMM that stores 64 MB of output leaves the L2s full of them
   int store_wt;
-  // fp8 kernels with the bf16 output unstored: the fp8 copy straight from fp32 (epilogue_lds D8);
-  // set by the launcher (PZ_F8_D8=0: through the bf16 image, A/B)
-  int d8;
 };
 
 // split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().

@@ -48,8 +48,6 @@ struct Case {
   int f8 = 0;  // 0 bf16, 1 e4m3 x e4m3 (forward), 2 e5m2 x e4m3 (backward dX), 3 e4m3 x e5m2 (dW)
   int tile_m = 0, tile_n = 0;  // 0: 256x256 (128x128 for the small fp8 config)
   int wt = 0;                  // write-through (sc1) epilogue stores (GemmArgs::store_wt)
-  int out8 = 0;                // 1: the trainer's fp8-policy output (bf16 C not stored, an fp8 copy +
-                               // amax); 2: the same with the fp8 copy straight from fp32 (GemmArgs::d8)
 };
 
 static double med(std::vector<double> v) {
@@ -116,14 +114,6 @@ int main(int argc, char** argv) {
       {"fwd_L2_wt", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30, F2>, 0, 0, 0, 1},
       {"dX_L2_wt", B, 4096, 4096, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30, M>, 0, 0, 0, 1},
       {"f8n_fwd_L1_fx_wt", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, F1>, 1, 0, 0, 1},
-      // the trainer's fp8 forward / dX launches (store_c=False: fp8 copy + amax, no bf16 C):
-      // through the bf16 image (o8) vs straight from fp32 (d8)
-      {"f8n_fwd_L1_o8", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, F1>, 1, 0, 0, 0, 1},
-      {"f8n_fwd_L1_d8", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, F1>, 1, 0, 0, 0, 2},
-      {"f8n_fwd_L1_2wg_o8", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, F1>, 1, 256, 128, 0, 1},
-      {"f8n_fwd_L1_2wg_d8", B, 8192, 1024, true, false, false, 1, 1, (F)launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, F1>, 1, 256, 128, 0, 2},
-      {"f8_dX_L2_2wg_o8", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 128, 2, 2, true, true, uint16_t, uint16_t, 17, M>, 2, 256, 128, 0, 1},
-      {"f8_dX_L2_2wg_d8", B, 8192, 1024, true, true, false, 3, 1, (F)launch_cfg<256, 128, 2, 2, true, true, uint16_t, uint16_t, 17, M>, 2, 256, 128, 0, 2},
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -197,18 +187,6 @@ int main(int argc, char** argv) {
     }
     p.epi = e;
     p.store_wt = c.wt;
-    uint8_t* buf8 = nullptr;
-    float* q8 = nullptr;  // {qscale, amax}
-    if (c.out8) {
-      CK(hipMalloc(&buf8, nc));
-      CK(hipMalloc(&q8, 8));
-      const float init[2] = {8.f, 0.f};
-      CK(hipMemcpy(q8, init, 8, hipMemcpyHostToDevice));
-      p.C = nullptr;
-      p.out8 = buf8; p.ldout8 = c.N; p.out8_qscale = q8; p.amax = q8 + 1;
-      p.out8_fmt = p.epi_mode == EPI_BWD ? 1 : 0;
-      p.d8 = c.out8 == 2;
-    }
     int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, R> ? 128 : 256, bn = bm;
     if (c.tile_m) bm = c.tile_m, bn = c.tile_n;
     const int tiles = ((c.M + bm - 1) / bm) * ((c.N + bn - 1) / bn);
@@ -274,7 +252,6 @@ int main(int argc, char** argv) {
     if (!emath.empty()) printf("    epilogue (wave 0): stage math + LDS image %.2f  image read + stores issued %.2f  store drain %.2f\n", med(emath), med(eissue), med(edrain));
     fflush(stdout);
     CK(hipFree(A)); CK(hipFree(Bm)); CK(hipFree(C)); CK(hipFree(bias)); CK(hipFree(colsum)); CK(hipFree(mask));
-    if (buf8) { CK(hipFree(buf8)); CK(hipFree(q8)); }
     if (ws) CK(hipFree(ws));
     CK(hipFree(counters)); CK(hipFree(stamps));
   }
