@@ -296,6 +296,11 @@ class FusedTrainer:
         # a GEMM's pending ones); within noise of priority 0 (profiles/r2_ab_opt_sched.txt)
         prio = int(os.environ.get("PZ_OPT_PRIO", "0"))
         self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
+        # PZ_MAIN_PRIO=-1 (A/B): the step's compute stream at high priority, so the dispatcher hands
+        # CUs that free up to the GEMMs' pending workgroups before the side stream's updates
+        mp = int(os.environ.get("PZ_MAIN_PRIO", "0"))
+        self._main_stream = torch.cuda.Stream(device=self.dev, priority=mp) if (mp < 0 and self.overlap) else None
+        self._main_synced = False
         # PZ_OPT_SERIAL=1 (one process): the overlap schedule's update launches (grouping, pairing,
         # order) enqueued on the COMPUTE stream where they fall, with no cross-stream events: every
         # record / wait costs the compute stream ~7 us of packet processing (r4 step timeline), and
@@ -478,6 +483,7 @@ class FusedTrainer:
         softmax head, ``[N, out]`` regression targets otherwise.
         """
         self._validate(inputs, targets.reshape(-1) if self.head == "softmax" else None)
+        self._main_synced = False  # (PZ_MAIN_PRIO: the step stream waits for this upload)
         host = torch.float64 if self.master == torch.float64 and self.stages[0].kind != "embed" else torch.float32
         self.data = self._table(inputs.to(dtype=host))
         self.block = self.data.shape[1] if self.stages[0].kind == "embed" else 1
@@ -748,6 +754,7 @@ class FusedTrainer:
         ``lr_schedule(epoch) -> lr`` (the learning rate :meth:`step` will be called with) enables
         hipGraph replay: the per-epoch optimizer hyper-parameters are tabulated on the device
         once, so a captured step needs nothing from the host but a replay."""
+        self._main_synced = False
         self._alloc_progress(epochs)
         self._invalidate_graphs()
         self._plan = None
@@ -781,6 +788,16 @@ class FusedTrainer:
 
     def step(self, epoch: int, lr: float, sample_size: int, dropout: float, l2: float, want_ratios: bool,
              record: bool, indices: torch.Tensor | None = None) -> None:
+        if self._main_stream is None:
+            return self._step(epoch, lr, sample_size, dropout, l2, want_ratios, record, indices)
+        if not self._main_synced:  # once: everything the caller enqueued so far (data, weights)
+            self._main_stream.wait_stream(torch.cuda.current_stream(self.dev))
+            self._main_synced = True
+        with torch.cuda.stream(self._main_stream):
+            return self._step(epoch, lr, sample_size, dropout, l2, want_ratios, record, indices)
+
+    def _step(self, epoch: int, lr: float, sample_size: int, dropout: float, l2: float, want_ratios: bool,
+              record: bool, indices: torch.Tensor | None = None) -> None:
         """One training epoch. ``indices`` (int64, this rank's ``batch`` rows) overrides the
         on-device sampler — used by the data-parallel equivalence tests.
 

@@ -9,3 +9,11 @@ for i in 1 2; do
     echo "mlp8192 side_grid=$g: $(python -c "import json;print(json.load(open('gpurun_out/r4p2/f.json'))['ms_per_step'])")"
   done
 done
+for i in 1 2; do
+  for env in "PZ_MAIN_PRIO=0" "PZ_MAIN_PRIO=-1"; do
+    env $env timeout -k 10 120 python bench.py --steps 100 --warmup 20 > gpurun_out/r4p2/m.json 2>>gpurun_out/r4p2/bench.log || exit 3
+    echo "mlp4 $env: $(python -c "import json;print(json.load(open('gpurun_out/r4p2/m.json'))['ms_per_step'])")"
+    env $env timeout -k 10 120 python bench.py --config mlp8192 --steps 100 --warmup 20 > gpurun_out/r4p2/f.json 2>>gpurun_out/r4p2/bench.log || exit 3
+    echo "mlp8192 $env: $(python -c "import json;print(json.load(open('gpurun_out/r4p2/f.json'))['ms_per_step'])")"
+  done
+done
