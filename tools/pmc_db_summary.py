@@ -1,6 +1,7 @@
 """Per-(kernel, grid) counter summary from rocprofv3 --pmc rocpd databases (ROCm 7 SQLite output).
 
-MFMA util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs) (MI355X_MICROARCH rocprofv3
+MFMA util = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs), LDS busy =
+SQ_LDS_IDX_ACTIVE / (GRBM_GUI_ACTIVE / 8 x 256 CUs) (MI355X_MICROARCH rocprofv3
 notes: GUI_ACTIVE is summed over the 8 XCDs, MFMA busy over every SIMD); the SQ_WAIT_* / ACTIVE_*
 columns are fractions of SQ_WAVE_CYCLES; LDS columns per dispatch. One row per kernel and grid size
 (gemm_bench runs each shape's kernels several times; rows group the dispatches of one shape).
@@ -49,7 +50,7 @@ def main():
             disp[key].add((db, did))
             passes[key][cname].add(db)
     hdr = f"{'kernel':60} {'grid':>8} {'disp':>5} {'MFMA':>6} {'WAIT_ANY':>8} {'WAIT_INST':>9} {'WAIT_LDS':>8} " \
-          f"{'ACTIVE':>6} {'LDS instr/disp':>14} {'bank confl/disp':>15}"
+          f"{'ACTIVE':>6} {'LDS instr/disp':>14} {'bank confl/disp':>15} {'LDS busy':>8}"
     print(hdr)
     for key in sorted(acc):
         # a counter collected in several passes (GRBM_GUI_ACTIVE rides along in each): per-pass mean
@@ -59,9 +60,11 @@ def main():
         gui = c.get("GRBM_GUI_ACTIVE", 0.0)
         util = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (gui / 8 * 1024) if gui and "SQ_VALU_MFMA_BUSY_CYCLES" in c else float("nan")
         f = lambda k: c[k] / wc if k in c else float("nan")  # noqa: E731
+        # LDS-array busy share per CU: SQ_LDS_IDX_ACTIVE (summed over CUs) / (GUI/8 x 256 CUs)
+        lds_busy = c["SQ_LDS_IDX_ACTIVE"] / (gui / 8 * 256) if gui and "SQ_LDS_IDX_ACTIVE" in c else float("nan")
         print(f"{key[0]:2d} {key[1][:57]:57} {key[2]:8d} {n:5d} {util:6.3f} {f('SQ_WAIT_ANY'):8.3f} {f('SQ_WAIT_INST_ANY'):9.3f} "
               f"{f('SQ_WAIT_INST_LDS'):8.3f} {f('SQ_ACTIVE_INST_ANY'):6.3f} {c.get('SQ_INSTS_LDS', float('nan')) / n:14.0f} "
-              f"{c.get('SQ_LDS_BANK_CONFLICT', float('nan')) / n:15.0f}")
+              f"{c.get('SQ_LDS_BANK_CONFLICT', float('nan')) / n:15.0f} {lds_busy:8.3f}")
 
 
 if __name__ == "__main__":
