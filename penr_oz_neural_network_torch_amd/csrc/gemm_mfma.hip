@@ -47,7 +47,7 @@ constexpr int kBK = 32;  // K depth of one ring slot (BK64 variants: two of thes
 // Per-variant ring geometry: VAR 20/21/30/31 stage 64-deep K steps into two 64 KiB slots (one
 // MFMA interval = 64 MFMAs per wave, half the barriers per FLOP of the 32-deep ring)
 template <int VAR> constexpr int var_bk() {
-  return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31 || VAR == 32 || VAR == 12 || VAR == 13) ? 64 : 32;
+  return (VAR == 20 || VAR == 21 || VAR == 30 || VAR == 31 || VAR == 32 || VAR == 33 || VAR == 12 || VAR == 13) ? 64 : 32;
 }
 template <int VAR> constexpr int var_ns() {
   return (VAR == 5 || VAR == 7 || VAR == 16 || VAR == 17) ? 3 : VAR == 23 ? 5 : (var_bk<VAR>() == 64 ? 2 : 4);
@@ -603,8 +603,10 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
       for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
 
+  // VAR 33 (lab A/B): VAR 30 without the s_setprio bracket around the MFMA block
+  constexpr bool PRIO = VAR != 33;
   auto mfma_step = [&](const Frags& f) {
-    __builtin_amdgcn_s_setprio(1);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
     if constexpr (M32) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -634,7 +636,7 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, f.b[kb][j]),
                                                                 __builtin_bit_cast(bf16x8_t, f.a[kb][i]), acc[i][j], 0, 0, 0);
     }
-    __builtin_amdgcn_s_setprio(0);
+    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   };
   auto read_frags = [&](int slot, Frags& f) {
     const PZ_LDS char* ta = smem + slot * C::SLOT_BYTES;
@@ -705,11 +707,11 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
   // or flat (64-bit pointers). Measured (tools/gemm_lab, same box): buffer is +6..10% on the
   // M/N-contiguous operands, whose k-row addresses otherwise cost 64-bit multiplies every step,
   // and 1.5..5% slower on K-contiguous ones (VAR 25 = buffer for M/N-contiguous only)
-  constexpr bool BUF_A = VAR == 6 || VAR == 7 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 32);
-  constexpr bool BUF_B = VAR == 6 || VAR == 7 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 32);
+  constexpr bool BUF_A = VAR == 6 || VAR == 7 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !A_KC) || (VAR >= 27 && VAR <= 33);
+  constexpr bool BUF_B = VAR == 6 || VAR == 7 || (VAR >= 10 && VAR <= 13) || VAR == 41 || (VAR == 25 && !B_KC) || (VAR >= 27 && VAR <= 33);
   constexpr int POL = VAR >= 27 && VAR <= 29 ? VAR - 26 : 0;
   // VAR 30/31: full row tiles of the K-contiguous operands (use_bk64 checks M % BM, N % BN)
-  constexpr bool FULL_KC = VAR == 30 || VAR == 31 || VAR == 32 || VAR == 12 || VAR == 13;
+  constexpr bool FULL_KC = VAR == 30 || VAR == 31 || VAR == 32 || VAR == 33 || VAR == 12 || VAR == 13;
   const i32x4_t rs_a = buf_rsrc(A), rs_b = buf_rsrc(B);
   // staging works in 16-bit units: an e4m3 row of 64 K-bytes is the same 64-B piece
   const int64_t lda = F8 ? p.lda / 2 : p.lda, ldb = F8 ? p.ldb / 2 : p.ldb;

@@ -98,6 +98,10 @@ int main(int argc, char** argv) {
       {"dW_L3", 4096, 1024, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, S>},
       {"dW_L1", 1024, 4096, B, false, false, false, 0, 4, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, S>},
       {"dW_L2", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, S>},
+      // VAR 33: VAR 30 without the s_setprio bracket around the MFMA block (lab A/B)
+      {"dX_L2_np", B, 4096, 4096, true, true, false, 3, 1, (F)launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 33, M>},
+      {"fwd_L2_np", B, 4096, 4096, true, false, false, 2, 1, (F)launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 33, R>},
+      {"dW_L2_np", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 33, S>},
       {"dW_L2_gen", 4096, 4096, B, false, false, false, 0, 1, (F)launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 30, G>},
       // the fp8 policy's GEMMs (mlp8192 [1024, 8192, 1024], batch 8192); operand bytes are
       // arbitrary (timing only)
