@@ -603,10 +603,12 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
       for (int j = 0; j < C::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
   }
 
-  // VAR 33 (lab A/B): VAR 30 without the s_setprio bracket around the MFMA block
+  // VAR 33 (lab A/B): VAR 30 without the s_setprio bracket around the MFMA block; GemmArgs::prio = 0
+  // (PZ_GEMM_PRIO=0) drops it at run time (a uniform scalar branch per MFMA block)
   constexpr bool PRIO = VAR != 33;
+  const bool prio = PRIO && p.prio != 0;
   auto mfma_step = [&](const Frags& f) {
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
+    if (prio) __builtin_amdgcn_s_setprio(1);
     if constexpr (M32) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -636,7 +638,7 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, f.b[kb][j]),
                                                                 __builtin_bit_cast(bf16x8_t, f.a[kb][i]), acc[i][j], 0, 0, 0);
     }
-    if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+    if (prio) __builtin_amdgcn_s_setprio(0);
   };
   auto read_frags = [&](int slot, Frags& f) {
     const PZ_LDS char* ta = smem + slot * C::SLOT_BYTES;
@@ -1424,6 +1426,14 @@ int64_t gemm_split_ws_floats(const GemmArgs& p) {
 // whole-tile epilogue stores write through (sc1) instead of leaving dirty L2 lines for the kernel
 // boundary's write-back (GemmArgs::store_wt); on by default, PZ_GEMM_WT=0 turns it off. r4 A/B,
 // mlp4 step: 1.1112 ms off, 1.1081 on; with PZ_OPT_NT on 1.1023 -> 1.0975
+int prio_default() {  // PZ_GEMM_PRIO=0: no s_setprio bracket around the ping-pong MFMA blocks (A/B)
+  static const int on = [] {
+    const char* e = getenv("PZ_GEMM_PRIO");
+    return e != nullptr ? atoi(e) : 1;
+  }();
+  return on;
+}
+
 int store_wt_default() {
   static const int on = [] {
     const char* e = getenv("PZ_GEMM_WT");
@@ -1464,6 +1474,7 @@ hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
   g.p[0] = a;
   g.p[1] = b;
   g.p[0].store_wt = g.p[1].store_wt = store_wt_default();
+  g.p[0].prio = g.p[1].prio = prio_default();
   g.nwg0 = (a.M / 256) * (a.N / 256) * split;
   const int nwg = g.nwg0 + (b.M / 256) * (b.N / 256) * split;
   if (a.in_dtype == DT_FP8) return launch_pair_cfg<uint16_t, 14, EK_STORE>(g, nwg, s);
@@ -1474,6 +1485,7 @@ hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
 hipError_t gemm_mfma(const GemmArgs& in, hipStream_t s) {
   GemmArgs p = in;
   p.store_wt = store_wt_default();
+  p.prio = prio_default();
   if (p.split_k > 1 && (p.ws == nullptr || p.counters == nullptr)) return hipErrorInvalidValue;
   if (p.in_dtype == DT_FP8) return launch_fp8(p, s);
   if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);

@@ -105,6 +105,7 @@ struct GemmArgs {
   // kernel left dirty in the XCD L2s (~B / 6 TB/s for B dirty bytes, MI355X_MICROARCH "boundary"),
   // and a GEMM that stores 64 MB of output leaves the L2s full of them
   int store_wt;
+  int prio;  // s_setprio(1) around the ping-pong MFMA blocks (set by the launcher, PZ_GEMM_PRIO)
 };
 
 // split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().

@@ -191,6 +191,7 @@ int main(int argc, char** argv) {
     }
     p.epi = e;
     p.store_wt = c.wt;
+    p.prio = 1;
     int bm = c.fn == (F)launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, R> ? 128 : 256, bn = bm;
     if (c.tile_m) bm = c.tile_m, bn = c.tile_n;
     const int tiles = ((c.M + bm - 1) / bm) * ((c.N + bn - 1) / bn);
