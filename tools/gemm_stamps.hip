@@ -121,12 +121,18 @@ int main(int argc, char** argv) {
   };
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  for (const Case& c : cases) {
-    if (argc > 1) {
-      bool want = false;
-      for (int i = 1; i < argc; ++i) want |= strcmp(argv[i], c.name) == 0;
-      if (!want) continue;
-    }
+  // cases run in command-line order (repeats allowed: interleave A/B pairs against clock drift);
+  // no arguments: the whole table
+  std::vector<const Case*> order;
+  if (argc > 1) {
+    for (int i = 1; i < argc; ++i)
+      for (const Case& c : cases)
+        if (strcmp(argv[i], c.name) == 0) order.push_back(&c);
+  } else {
+    for (const Case& c : cases) order.push_back(&c);
+  }
+  for (const Case* cp : order) {
+    const Case& c = *cp;
     const int64_t na = static_cast<int64_t>(c.M) * c.K, nb = static_cast<int64_t>(c.N) * c.K;
     const int64_t nc = static_cast<int64_t>(c.M) * c.N;
     uint16_t *A, *Bm, *C;
