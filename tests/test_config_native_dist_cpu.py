@@ -112,3 +112,60 @@ def test_relu_mask_tile_blocked_layout(m, n):
         i, j = (int(torch.randint(0, m, (1,), generator=g)), int(torch.randint(0, n, (1,), generator=g)))
         off = (i >> 8) * 256 * ld + (j >> 8) * 8192 + (i & 255) * 32 + ((j & 255) >> 3)
         assert bool((int(flat[off]) >> (j & 7)) & 1) == bool(pos[i, j])
+
+
+def test_collective_footprint_proxy_plumbing():
+    """PZ_COMM=proxy (parallel/dist.py _ProxyComm over csrc/comm_proxy.hip): its knobs reach the
+    proxy communicator, bucket all-reduces become tickets on it, shutdown closes it; and it refuses
+    anything but a forced world-1 GPU run. The proxy kernel itself runs in the GPU tier
+    (tests/test_dp_gpu.py forced[fp32-proxy])."""
+    code = textwrap.dedent("""
+        import os, torch
+        from penr_oz_neural_network_torch_amd.parallel import dist as D
+        log = {"init": None, "reduced": [], "closed": []}
+        class FakeOps:
+            @staticmethod
+            def rccl_proxy_init(world, wgs, gbps, cus, hp):
+                log["init"] = (world, wgs, gbps, cus, hp); return 3
+            @staticmethod
+            def rccl_all_reduce(h, t):
+                log["reduced"].append((h, t.numel())); return len(log["reduced"]) - 1
+            @staticmethod
+            def rccl_wait(h, ticket):
+                pass
+            @staticmethod
+            def rccl_destroy(h):
+                log["closed"].append(h)
+        class FakeTorch:
+            ops = type("ops", (), {"pz": FakeOps})
+            def __getattr__(self, name):
+                return getattr(torch, name)
+        os.environ.update(PZ_COMM_PROXY_WORLD="4", PZ_COMM_PROXY_WGS="8", PZ_COMM_PROXY_GBPS="200", PZ_COMM_CUS="8")
+        D.torch = FakeTorch()
+        comm = D._ProxyComm()
+        assert log["init"] == (4, 8, 200.0, 8, False)
+        tk = comm.all_reduce(torch.zeros(10))
+        assert isinstance(tk, D._Ticket) and log["reduced"] == [(3, 10)]
+        ctx = D.DataParallelContext()
+        ctx.native = comm
+        D.set_context(ctx)
+        D.shutdown()
+        assert log["closed"] == [3] and comm.handle is None
+        comm.close()  # idempotent
+        assert log["closed"] == [3]
+        D.torch = torch
+        # forced world 1 over gloo without a GPU: refused
+        os.environ.update(PZ_FORCE_COMM="1", PZ_DIST_BACKEND="gloo", PZ_COMM="proxy")
+        for k in ("RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT"):
+            os.environ.pop(k, None)
+        try:
+            D.init_from_env()
+            raise SystemExit("proxy accepted without a GPU")
+        except RuntimeError as e:
+            assert "ONE GPU" in str(e)
+        D.shutdown()
+        print("proxy ok")
+    """)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0 and "proxy ok" in r.stdout, r.stderr[-3000:]
