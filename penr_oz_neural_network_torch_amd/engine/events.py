@@ -29,6 +29,30 @@ class _Native:
             torch.ops.pz.event_wait(self.h, self.dev)
 
 
+class _Signal:
+    """Device-side ordering (csrc/stream_signal.hip): ``record`` launches a one-wave kernel that
+    bumps this entry's counter, ``wait`` a one-wave kernel that holds the stream until the counter
+    has reached that record's count. The compute stream pays ~1.5 us per record instead of the ~7 us
+    of an event with a cross-stream waiter (profiles/r4_packet_gap.txt). Two streams only: a
+    re-record of the entry on either stream is ordered after every wait on the previous record.
+    Off by default (PZ_DEV_SIG=1): the waiting wave holds a CU for as long as it waits, and the
+    256-CU-quantised GEMMs beside it need an extra round (mlp4 1.49 vs 1.09 ms, see
+    csrc/stream_signal.hip)."""
+    __slots__ = ("ctr", "slot", "n", "timeout_us")
+
+    def __init__(self, ctr: torch.Tensor, slot: int, timeout_us: float):
+        self.ctr, self.slot, self.n, self.timeout_us = ctr, slot, 0, timeout_us
+
+    def record(self, stream) -> None:
+        self.n += 1
+        with torch.cuda.stream(stream):
+            torch.ops.pz.signal_set(self.ctr, self.slot)
+
+    def wait(self, stream) -> None:
+        with torch.cuda.stream(stream):
+            torch.ops.pz.signal_wait(self.ctr, self.slot, self.n, self.timeout_us)
+
+
 class _Torch:
     __slots__ = ("ev",)
 
@@ -51,7 +75,15 @@ class StreamEvents:
         self.dev = device.index if device.index is not None else torch.cuda.current_device()
         # PZ_TORCH_EVENTS=1: the system-fenced events of before (A/B)
         self.fenced = os.environ.get("PZ_TORCH_EVENTS", "0") == "1"
-        self._ring = [_Native(torch.ops.pz.event_create(self.dev, 0), self.dev) for _ in range(ring)]
+        # PZ_DEV_SIG=1: device-side counters instead of events for the ordering ring (A/B)
+        self.signals = os.environ.get("PZ_DEV_SIG", "0") == "1" and not self.fenced
+        self._ctr = None
+        if self.signals:
+            self._ctr = torch.zeros(ring * 32, dtype=torch.int32, device=torch.device("cuda", self.dev))
+            # a waiter gives up after 5 s and records it (timeouts()): the grid always drains
+            self._ring = [_Signal(self._ctr, i, 5e6) for i in range(ring)]
+        else:
+            self._ring = [_Native(torch.ops.pz.event_create(self.dev, 0), self.dev) for _ in range(ring)]
         self._next = 0
         self._stamps: list[int] = []
 
@@ -82,10 +114,17 @@ class StreamEvents:
                 torch.ops.pz.event_destroy(h)
         self._stamps = [keep] if keep is not None else []
 
+    def timeouts(self) -> int:
+        """Signal waits that gave up (read after a synchronize; 0 with events)."""
+        if self._ctr is None:
+            return 0
+        return int(self._ctr.view(-1, 32)[:, 1].sum().item())
+
     def close(self) -> None:
         self.release()
         for ev in self._ring:
-            torch.ops.pz.event_destroy(ev.h)
+            if isinstance(ev, _Native):
+                torch.ops.pz.event_destroy(ev.h)
         self._ring = []
 
     def __del__(self):  # (a trainer dropped without close(); nothing to do at interpreter exit)

@@ -1648,6 +1648,9 @@ class FusedTrainer:
         if not self._pending:
             return []
         torch.cuda.synchronize(self.dev)
+        if self.events.signals and self.events.timeouts():
+            raise RuntimeError("fused trainer: a device-side stream wait timed out (PZ_DEV_SIG=1): "
+                               "the step's cross-stream ordering was not kept")
         costs = self.costs.cpu().tolist()
         ratios = self.ratios.cpu().view(-1, max(1, self.opt.nslots)).tolist()
         out = []
