@@ -496,4 +496,9 @@ def test_paired_dw_matches_separate_launches(monkeypatch, dtype):
     for a, b, nb in zip(c0, c1, cn):
         assert abs(a - b) <= 3 * abs(a - nb) + 1e-3 * max(1.0, abs(a)), (c0, c1, cn)
     d, dn = (p0 - p1).abs(), (p0 - pn).abs()
-    assert d.mean().item() <= 3 * dn.mean().item() + 2e-5, (d.mean().item(), dn.mean().item())
+    # the pair runs split-K 2 where the separate launches run split-K 4: dW rounds differently and
+    # Adam turns that into sign flips of near-zero gradients (each <= 2 * lr per step). The
+    # unpaired schedule is deterministic here (dn ~ 0), so the bound is absolute: fp8 measured
+    # 5.6e-5 on one r4 box (below 2e-5 on others); a wrong dW moves every weight by ~lr (3e-3)
+    assert d.mean().item() <= 3 * dn.mean().item() + 2e-4, (d.mean().item(), dn.mean().item())
+    assert d.max().item() <= 2 * 0.003 * steps + 1e-6

@@ -70,8 +70,8 @@ def _run(monkeypatch, sig: str, dtype: str):
 @pytest.mark.parametrize("dtype", ["bfloat16", "fp8"])
 def test_trainer_on_signals_matches_events(monkeypatch, dtype):
     """Same trajectory as the event ring, to the run-to-run noise of the trainer's atomic
-    reductions. fp8 runs are bit-identical either way (r4 GPU run: weights equal, costs within
-    1e-9); bf16 event-ring runs already differ from each other in the last bits of the cost, and
+    reductions. fp8 runs are nearly bit-identical either way (r4 GPU runs: weights equal or 4e-6
+    apart, costs within 1e-9); bf16 event-ring runs already differ from each other in the last bits of the cost, and
     Adam turns that into sign flips of near-zero gradients: weights apart by up to a few lr
     (5e-3 event vs event, 5.8e-3 signal vs event on the r4 box), bounded by 2 * lr * steps."""
     c0, w0 = _run(monkeypatch, "0", dtype)
@@ -85,7 +85,7 @@ def test_trainer_on_signals_matches_events(monkeypatch, dtype):
     dc_sig = max(abs(a - b) / abs(a) for a, b in zip(c0, c1))
     print(f"{dtype}: event vs event cost {dc_ev:.2e} weights {dw(w0, w0b):.2e}; "
           f"signal vs event cost {dc_sig:.2e} weights {dw(w0, w1):.2e}")
-    assert dc_sig <= 1e-4, (c0, c1)
-    if dtype == "fp8":
-        assert dw(w0, w1) == 0.0 or dw(w0, w1) <= 2 * dw(w0, w0b)
-    assert dw(w0, w1) <= 2 * 0.001 * 6
+    # (bf16: event vs event already 1.2e-4 apart on one r4 box, signal vs event 1.6e-4 on another)
+    assert dc_sig <= (1e-5 if dtype == "fp8" else 1e-3), (c0, c1)
+    # fp8: usually bit-identical, at most a rare last-bit difference (4e-6 seen once on r4 boxes)
+    assert dw(w0, w1) <= (1e-4 if dtype == "fp8" else 2 * 0.001 * 6)
