@@ -194,8 +194,10 @@ def compute_model_output(body: ActivationRequest = Body(..., openapi_examples={
     return {"output_vector": output, "cost": cost}
 
 
-# active training sessions by model id (one event loop, so a plain dict is safe)
+# active training sessions by model id (one event loop, so a plain dict is safe), and the ids
+# whose PUT /train/ is still loading the checkpoint (between the 409 check and the task start)
 model_locks: Dict[str, Lock] = {}
+_starting: set = set()
 
 
 def _log_task_failure(task) -> None:
@@ -208,9 +210,16 @@ async def train_model(body: TrainingRequest = Body(...)):
     model_id = body.model_id
     log.info(f"Requesting training for model {model_id}")
     lock = model_locks.setdefault(model_id, Lock())
-    if lock.locked():
+    if lock.locked() or model_id in _starting:
         raise HTTPException(status_code=409, detail=f"Training already in progress for model {model_id}.")
-    model = NeuralNetworkModel.deserialize(model_id)
+    # the checkpoint loads OFF the event loop (seconds for a 25 M-1 B parameter model; the
+    # reference parses it on the loop, main.py:270, and every /progress/ poll stalls meanwhile)
+    _starting.add(model_id)
+    try:
+        model = await run_in_threadpool(NeuralNetworkModel.deserialize, model_id)
+    except BaseException:
+        _starting.discard(model_id)
+        raise
     data = [(item.activation_vector, item.target_vector) for item in body.training_data]
 
     hp = dict(epochs=body.epochs, learning_rate=body.learning_rate, batch_size=body.batch_size,
@@ -218,9 +227,13 @@ async def train_model(body: TrainingRequest = Body(...)):
               beta1=body.adam_beta1, beta2=body.adam_beta2, epsilon=body.adam_epsilon)
 
     async def train():
-        async with lock:
-            # one thread trains; with a multi-GPU train group up, a GPU model trains on every rank
-            await run_in_threadpool(service.train, model, data, hp)
+        try:
+            async with lock:
+                _starting.discard(model_id)  # the lock now says "in progress"
+                # one thread trains; with a multi-GPU train group up, a GPU model trains on every rank
+                await run_in_threadpool(service.train, model, data, hp)
+        finally:
+            _starting.discard(model_id)
 
     create_task(train()).add_done_callback(_log_task_failure)
     return JSONResponse(content={"message": f"Training for model {model_id} started asynchronously."},

@@ -253,7 +253,22 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
                 "pz::gemm: store_c=False needs the MFMA path with a bf16 C and a side output");
     p.C = nullptr;
   }
-  at::Tensor ws;  // split-K slabs: from the caching allocator, stream-ordered reuse is safe
+  at::Tensor ws;  // split-K / stream-K slabs: from the caching allocator, stream-ordered reuse is safe
+  // flags bits 2-3: engine (0 default, 1 tiled gemm_mfma, 2 persistent stream-K); bits 16-31: the
+  // CU budget of the persistent engine (0 = every CU)
+  p.engine = static_cast<int>((flags >> 2) & 3);
+  p.cus = static_cast<int>((flags >> 16) & 0xFFFF);
+  if ((p.engine == 2 || (p.engine == 0 && pz::sk_default())) && pz::sk_eligible(p)) {
+    const int64_t sk_floats = pz::sk_ws_floats(&p, 1);
+    int* tickets = nullptr;
+    if (sk_floats > 0) {
+      ws = at::empty({sk_floats}, A.options().dtype(at::kFloat));
+      tickets = split_counters(pz::sk_tickets(&p, 1), A.device());
+    }
+    PZ_HIP_CHECK(pz::gemm_sk(&p, 1, sk_floats > 0 ? ws.data_ptr<float>() : nullptr, tickets, cur_stream(A)));
+    return;
+  }
+  TORCH_CHECK(p.engine != 2, "pz::gemm: the stream-K engine cannot run this GEMM (pz::sk_eligible)");
   // flags bit 0: no split-K (a GEMM that runs concurrently with others: its tile count need not
   // fill the CUs on its own, and it skips the in-launch reduction)
   const int64_t ws_floats = (flags & 1) ? 0 : pz::gemm_split_ws_floats(p);

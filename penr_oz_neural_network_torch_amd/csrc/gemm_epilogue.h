@@ -159,10 +159,10 @@ PZ_DEV void act_bwd_row(f32x4_t (&v)[L::COLS], const PZ_LDS char* img, int ml, i
 #undef PZ_ACTB_LOOP
 }
 
-// v *= relu'(.) from the stage's ReLU bitmask: `bits` = the 64 mask bits of the wave's 64
+// v *= relu'(.) from the stage's ReLU bitmask: `bits` = the mask bits of the wave's 64 or 128
 // columns of this row; group j element r is bit n_off(j) + n_lane + r (never straddles a word)
-template <class L>
-PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], u32x2_t bits, int nlane) {
+template <class L, int NWORD>
+PZ_DEV void act_bwd_mask_row(f32x4_t (&v)[L::COLS], const uint32_t (&bits)[NWORD], int nlane) {
 #pragma unroll
   for (int j = 0; j < L::COLS; ++j) {
     const uint32_t w = bits[L::n_off(j) >> 5] >> ((L::n_off(j) & 31) + nlane);
@@ -255,7 +255,8 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   constexpr int CHUNKS_PER_ROW = BN / 8;
   constexpr int ROWS_PER_PASS = NT / CHUNKS_PER_ROW;
   constexpr int PASSES = BM / ROWS_PER_PASS;
-  static_assert(WTN == 64, "the ReLU bitmask epilogue assumes 64-column wave tiles");
+  static_assert(WTN == 64 || WTN == 128, "the ReLU bitmask epilogue reads 64- or 128-column wave rows");
+  constexpr int MWORDS = WTN / 32;  // bitmask words per accumulator row
   const int tid = threadIdx.x;
   const int my_row = tid / CHUNKS_PER_ROW, my_chunk = tid % CHUNKS_PER_ROW;
   // FWD_ONLY: no colsum / backward code
@@ -267,16 +268,25 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
   const bool use_mask = EK == EK_BWD_MASK || (EK != EK_STORE && p.mask != nullptr);
   constexpr bool kColsum = !FWD_ONLY && (EK == EK_ANY || EK == EK_BWD_MASK);
 
-  // ReLU bitmask (EPI_BWD): 8 bytes per accumulator row, issued before the barrier so the
-  // loads fly while the slower waves finish their last MFMAs
-  u32x2_t mbits[ROWS];
+  // ReLU bitmask (EPI_BWD): 8 (16) bytes per accumulator row of a 64 (128)-column wave tile,
+  // issued before the barrier so the loads fly while the slower waves finish their last MFMAs
+  uint32_t mbits[ROWS][MWORDS];
   if (bwd && use_mask) {
-    // (the tile's rows lie in one 256-row block: 32-B row pitch, 64-column aligned 8-B reads)
+    // (the tile's rows lie in one 256-row block: 32-B row pitch, wave-column aligned reads)
     const uint8_t* mrow = p.mask + mask_off(m0, n0 + wn * WTN, p.ldmask);
 #pragma unroll
     for (int i = 0; i < ROWS; ++i) {
       const int m = m0 + ml0 + L::MSTEP * i;
-      mbits[i] = m < p.M ? *reinterpret_cast<const u32x2_t*>(mrow + (ml0 + L::MSTEP * i) * 32) : u32x2_t{0u, 0u};
+      const uint8_t* src = mrow + (ml0 + L::MSTEP * i) * 32;
+      if constexpr (MWORDS == 2) {
+        const u32x2_t b = m < p.M ? *reinterpret_cast<const u32x2_t*>(src) : u32x2_t{0u, 0u};
+        mbits[i][0] = b[0];
+        mbits[i][1] = b[1];
+      } else {
+        const u32x4_t b = m < p.M ? *reinterpret_cast<const u32x4_t*>(src) : u32x4_t{0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mbits[i][q] = b[q];
+      }
     }
   }
 
@@ -344,7 +354,7 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
     } else if (EK == EK_BWD_MASK || use_mask) {
       // ReLU stage: y > 0  <=>  kept by drop_post AND kept by drop_pre AND z > 0, so the whole
       // derivative chain is one bit times the dropout scales — no hashes in the backward
-      act_bwd_mask_row<L>(v, mbits[i], nlane);
+      act_bwd_mask_row<L, MWORDS>(v, mbits[i], nlane);
 #pragma unroll
       for (int j = 0; j < COLS; ++j) v[j] *= bwd_scale;
     } else if constexpr (EK == EK_ANY) {

@@ -1,0 +1,563 @@
+// N1b — persistent stream-K bf16 GEMM for gfx950: the step GEMMs' engine.
+//
+// Replaces the reference's per-layer matmuls (neural_net_model.py:117 forward `x @ W`, and the two
+// autograd `mm` of cost.backward(), :495) with the fused stage epilogues around them (bias :119,
+// activation :172-184, dropout :393-395, bias-gradient column sums).
+//
+// Design (MI355X-first; /opt/skills/guides/cdna_hip_programming.md §5, MI355X_MICROARCH.md):
+//  * 256x256 macro tile on FOUR waves, one per SIMD, each owning a 128x128 wave tile = 8x8
+//    v_mfma_f32_16x16x32_bf16 accumulators (the whole 256-register AGPR file). Per 32-deep K step
+//    a wave reads 16 fragments for 64 MFMAs: 0.25 LDS reads per MFMA (the 8-wave 128x64 wave
+//    tiles of gemm_mfma.hip read 0.375).
+//  * LDS ring of NS 32-deep slots (32 KiB: A [256 rows][32 k], B likewise), filled by buffer-
+//    addressed LDS-DMA (`buffer_load_dwordx4 ... lds`, swizzle on the per-lane SOURCE offset).
+//    Fragments are read one step AHEAD into a second VGPR set, so a slot is free again one step
+//    after it landed; its refill for step h+NS is issued in step h and has NS-1 steps (1.5 full
+//    64-deep K steps at NS = 4) to land — the 2-slot 64-deep ring gave the DMA one step.
+//  * One raw s_barrier per step: every wave's counted `vmcnt` for step h+2 and `lgkmcnt(0)` for
+//    its reads of step h+1 precede it (RAW for the next reads, WAR for the next refill).
+//  * MFMAs, next-step fragment reads and refill DMAs interleaved in 16 groups per step (4 MFMAs,
+//    one fragment, every other group one DMA), fenced by sched_barrier so hipcc keeps the mix.
+//  * PERSISTENT: the grid is the CU budget (GemmArgs::cus, at most the device's CUs, one
+//    workgroup per CU). Every workgroup walks a static schedule: a stream-K region — the tiles
+//    that do not fill whole rounds of workgroups, their K iterations split evenly over ALL
+//    workgroups ("two-tile" stream-K: the remainder plus one full round) — then whole data-
+//    parallel tiles. A CU budget below the device (RCCL channels resident beside the GEMMs)
+//    shrinks the grid instead of leaving a straggler round of tiles.
+//  * Stream-K partial tiles: each contributor stores its fp32 accumulators write-through (sc1)
+//    into a slab, drains, joins a barrier and takes a relaxed agent-scope ticket (MI355X_MICROARCH
+//    hand-off table, row 1); the LAST arriver folds the slabs in K order with sc1 loads and runs
+//    the epilogue. The sum order never depends on which workgroup arrives last: deterministic.
+//  * Epilogues: gemm_epilogue.h's LDS-staged kinds on 128-column wave tiles; fp32 outputs (weight
+//    gradients) store straight from the accumulators.
+//  * Two problems of one layout / epilogue kind / K may share a launch (the two skinny weight-
+//    gradient GEMMs of a 3-layer MLP): their tiles form one schedule.
+#include <algorithm>
+#include <cstdlib>
+#include <type_traits>
+
+#include "pz_common.h"
+#include "pz_launch.h"
+
+namespace pz {
+namespace {
+
+#include "gemm_common.h"
+#include "gemm_epilogue.h"
+
+constexpr int kSkB = 256;                    // macro tile BM = BN
+constexpr int kSkNT = 256;                   // four waves
+constexpr int kSkBK = 32;                    // K depth of a ring slot
+constexpr int kSkOp = kSkB * kSkBK * 2;      // one operand's slot image: 16 KiB
+constexpr int kSkSlot = 2 * kSkOp;           // A then B: 32 KiB
+constexpr int kSkPieces = kSkOp / 1024 / 4;  // LDS-DMA instructions per wave, operand and step (4)
+constexpr int kSkG = 2 * kSkPieces;          // per wave and step (8)
+constexpr int kSkNS = 4;                     // ring slots (128 KiB = the epilogue's C image)
+constexpr int kSkSlab = kSkB * kSkB;         // fp32 floats of one partial tile
+constexpr int kSkF32 = 100;                  // epilogue code of the fp32-output store path
+constexpr int kSkMaxCon = 8;                 // contributors per stream-K tile (sk_plan bounds it)
+
+struct SkSched {
+  int nprob;
+  int tiles0;           // tiles of problem 0 (problem 1's tiles follow)
+  int tiles;            // all tiles
+  int iters;            // 32-deep K steps per tile
+  int grid;             // workgroups
+  int sk_tiles;         // tiles [0, sk_tiles) are stream-K'd over every workgroup
+  long long sk_iters;   // sk_tiles * iters
+};
+
+struct SkArgs {
+  GemmArgs p[2];
+  SkSched s;
+  float* ws;      // [2 * grid][256 * 256] partial slabs: slab 2w = workgroup w's first unit, 2w+1 its last
+  int* counters;  // [sk_tiles] tickets, zero between launches (the last arriver resets its tile's)
+};
+
+// first stream-K iteration of workgroup w (w = grid: the end)
+PZ_DEV long long sk_start(const SkSched& s, int w) { return static_cast<long long>(w) * s.sk_iters / s.grid; }
+
+// the workgroup whose stream-K range holds iteration `it`
+PZ_DEV int sk_owner(const SkSched& s, long long it) {
+  int w = static_cast<int>(it * s.grid / s.sk_iters);
+  while (w + 1 < s.grid && sk_start(s, w + 1) <= it) ++w;
+  while (w > 0 && sk_start(s, w) > it) --w;
+  return w;
+}
+
+// One operand's LDS-DMA addressing for a unit. K-contiguous ([rows][K]): piece i of this wave =
+// 16 rows x 64 B; M/N-contiguous ([K][rows]): piece i = 2 k-rows x 512 B. The per-lane offsets
+// carry the read-side swizzle (rule 21: linear LDS destination, permuted source).
+struct SkOperand {
+  i32x4_t rs;          // raw buffer resource of the operand
+  uint32_t voff[2];    // per-lane byte offsets (M/N-contiguous: by piece parity)
+  uint32_t base;       // wave-uniform byte offset of this wave's piece 0 at the unit's first step
+  uint32_t pstep;      // bytes between the wave's consecutive pieces
+  uint32_t kstep;      // bytes per 32-deep K step
+};
+
+template <bool KC>
+PZ_DEV SkOperand sk_operand(const void* g, int64_t ld, int row0, int kb, int wave, int lane) {
+  SkOperand o;
+  o.rs = buf_rsrc(g);
+  const uint32_t l = static_cast<uint32_t>(ld);
+  if constexpr (KC) {
+    const int r = lane >> 2;  // row within the piece (16 rows x 4 chunks)
+    const int chunk = (lane & 3) ^ swz_kc<32>(r);
+    o.voff[0] = o.voff[1] = (static_cast<uint32_t>(r) * l + static_cast<uint32_t>(chunk) * 8u) * 2u;
+    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(row0 + wave * 4 * 16) * l + static_cast<uint32_t>(kb) * kSkBK) * 2u);
+    o.pstep = __builtin_amdgcn_readfirstlane(16u * l * 2u);
+    o.kstep = kSkBK * 2;
+  } else {
+#pragma unroll
+    for (int par = 0; par < 2; ++par) {
+      const int kr = wave * 8 + 2 * par + (lane >> 5);  // k-row in the slot (its swizzle only)
+      const int chunk = (lane & 31) ^ swz_mn(kr);
+      o.voff[par] = (static_cast<uint32_t>(lane >> 5) * l + static_cast<uint32_t>(chunk) * 8u) * 2u;
+    }
+    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(kb * kSkBK + wave * 8) * l + static_cast<uint32_t>(row0)) * 2u);
+    o.pstep = __builtin_amdgcn_readfirstlane(2u * l * 2u);
+    o.kstep = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(kSkBK) * l * 2u);
+  }
+  return o;
+}
+
+// piece i of K step ks (relative to the unit) into the wave's LDS range `lds` (+ i KiB)
+template <bool KC>
+PZ_DEV void sk_dma(const SkOperand& o, int i, int ks, uint32_t lds) {
+  const uint32_t voff = KC ? o.voff[0] : o.voff[i & 1];
+  blds16<0>(o.rs, voff, o.base + static_cast<uint32_t>(i) * o.pstep + static_cast<uint32_t>(ks) * o.kstep,
+            lds + static_cast<uint32_t>(i) * 1024u);
+}
+
+// fragment f (16 rows / columns x 32 k) of the wave's 128-row / -column half `wg` of a slot image
+template <bool KC>
+PZ_DEV i16x8_t sk_frag(const PZ_LDS char* img, int wg, int f, int lane, uint32_t kc_lane) {
+  if constexpr (KC) return *reinterpret_cast<const PZ_LDS i16x8_t*>(img + (wg * 128 + f * 16) * (kSkBK * 2) + kc_lane);
+  else return frag_mn<kSkB>(img, wg * 128 + f * 16, 8 * (lane >> 4), lane);
+}
+
+struct SkFrag {
+  i16x8_t a[8];
+  i16x8_t b[8];
+};
+
+PZ_DEV void sk_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// The main loop of one unit: n 32-deep K steps into acc (zeroed by the caller).
+template <bool A_KC, bool B_KC, int NS>
+PZ_DEV void sk_mainloop(f32x4_t (&acc)[8][8], PZ_LDS char* smem, const SkOperand& oa, const SkOperand& ob, int n,
+                        int wave, int wm, int wn, int lane) {
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t wpiece = static_cast<uint32_t>(wave) * kSkPieces * 1024u;
+  const uint32_t kc_lane = static_cast<uint32_t>((lane & 15) * (kSkBK * 2) + (((lane >> 4) ^ swz_kc<32>(lane & 15)) << 4));
+  auto dma_step = [&](int ks) __attribute__((always_inline)) {
+    const uint32_t sb = lds0 + static_cast<uint32_t>(ks % NS) * kSkSlot + wpiece;
+#pragma unroll
+    for (int i = 0; i < kSkPieces; ++i) sk_dma<A_KC>(oa, i, ks, sb);
+#pragma unroll
+    for (int i = 0; i < kSkPieces; ++i) sk_dma<B_KC>(ob, i, ks, sb + kSkOp);
+  };
+  auto read_all = [&](SkFrag& f, int ks) __attribute__((always_inline)) {
+    const PZ_LDS char* img = smem + (ks % NS) * kSkSlot;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.b[j] = sk_frag<B_KC>(img + kSkOp, wn, j, lane, kc_lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) f.a[i] = sk_frag<A_KC>(img, wm, i, lane, kc_lane);
+  };
+  // step h: 64 MFMAs on `cur`; rd: read step h+1 into `nxt`; dm: refill slot h % NS with step
+  // h+NS. ONE body with scalar guards: three specialised bodies made hipcc keep every fragment
+  // set live across all of them (spills)
+  auto step = [&](const SkFrag& cur, SkFrag& nxt, int h) __attribute__((always_inline)) {
+    const bool rd = h + 1 < n, dm = h + NS < n;
+    const PZ_LDS char* img = smem + ((h + 1) % NS) * kSkSlot;
+    const uint32_t sb = lds0 + static_cast<uint32_t>(h % NS) * kSkSlot + wpiece;
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<16>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      static_for<4>([&](auto qc) {
+        constexpr int idx = 4 * g + decltype(qc)::value, i = idx >> 3, j = idx & 7;
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, cur.b[j]),
+                                                            __builtin_bit_cast(bf16x8_t, cur.a[i]), acc[i][j], 0, 0, 0);
+      });
+      if (rd) {
+        if constexpr (g < 8) nxt.b[g] = sk_frag<B_KC>(img + kSkOp, wn, g, lane, kc_lane);
+        else nxt.a[g - 8] = sk_frag<A_KC>(img, wm, g - 8, lane, kc_lane);
+      }
+      if constexpr ((g & 1) == 0) {
+        constexpr int pc = g / 2;
+        if (dm) {
+          if constexpr (pc < kSkPieces) sk_dma<A_KC>(oa, pc, h + NS, sb);
+          else sk_dma<B_KC>(ob, pc - kSkPieces, h + NS, sb + kSkOp);
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    if (h + 2 < n) {  // step h+2 landed for every wave; every read of slot (h+1) % NS retired
+      wait_newer<kSkG, NS - 2>(min(h + NS, n - 1) - (h + 2));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      sk_barrier();
+    }
+  };
+
+  // the previous unit's epilogue stores share the VM counter with the DMAs counted below: retire
+  // them first; and every wave is done with the LDS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  sk_barrier();
+  const int pre = min(NS, n);
+  for (int s = 0; s < pre; ++s) dma_step(s);
+  wait_newer<kSkG, NS - 2>(max(pre - 2, 0));  // steps 0 and 1 landed
+  sk_barrier();
+  SkFrag f0, f1;
+  read_all(f0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  sk_barrier();  // every wave read slot 0 before step 0 refills it
+  for (int h = 0; h < n; h += 2) {
+    step(f0, f1, h);
+    if (h + 1 < n) step(f1, f0, h + 1);
+  }
+}
+
+// fp32-output epilogue (weight gradients): alpha, bias, accumulate, column sums; 16-B stores
+PZ_DEV void sk_store_f32(const GemmArgs& p, f32x4_t (&acc)[8][8], int m0, int n0, int wm, int wn, int lane) {
+  float* __restrict__ Cp = static_cast<float*>(p.C);
+  const int g4 = 4 * (lane >> 4);
+  static_for<8>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const int n = n0 + wn * 128 + j * 16 + g4;
+    const f32x4_t bias4 = p.bias != nullptr ? *reinterpret_cast<const f32x4_t*>(p.bias + n) : f32x4_t{0.f, 0.f, 0.f, 0.f};
+    f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
+    static_for<8>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      const int m = m0 + wm * 128 + i * 16 + (lane & 15);
+      f32x4_t v = acc[i][j] * p.alpha + bias4;
+      f32x4_t* dst = reinterpret_cast<f32x4_t*>(Cp + static_cast<int64_t>(m) * p.ldc + n);
+      if (p.accumulate) v += *dst;
+      *dst = v;
+      cs += v;
+    });
+    if (p.colsum != nullptr) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float s = group_sum<16>(cs[r]);
+        if ((lane & 15) == 0) atomicAdd(p.colsum + n + r, s);
+      }
+    }
+  });
+}
+
+template <bool A_KC, bool B_KC, typename OutT, int EK, int NS>
+__global__ void __launch_bounds__(kSkNT) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_sk_kernel(const SkArgs g) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+  const SkSched& s = g.s;
+  const int w = xcd_remap(blockIdx.x, gridDim.x);  // consecutive ids share an XCD's L2
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  const int tid = threadIdx.x;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // Work units in schedule order: the stream-K range [s0, s1) cut at tile boundaries, then the
+  // data-parallel tiles w, w + grid, ... ONE loop, so the unit body is inlined once.
+  const long long s0 = s.sk_iters > 0 ? sk_start(s, w) : 0, s1 = s.sk_iters > 0 ? sk_start(s, w + 1) : 0;
+  long long it = s0;
+  int dp_t = s.sk_tiles + w;
+  for (;;) {
+    // this unit: K steps [kb, ke) of tile t; slab >= 0: a stream-K partial tile
+    int t, kb, ke, slab;
+    if (it < s1) {
+      t = static_cast<int>(it / s.iters);
+      kb = static_cast<int>(it - static_cast<long long>(t) * s.iters);
+      const long long left = s1 - it;
+      ke = left < static_cast<long long>(s.iters - kb) ? kb + static_cast<int>(left) : s.iters;
+      slab = (kb == 0 && ke == s.iters) ? -1 : 2 * w + (it == s0 ? 0 : 1);
+      it += ke - kb;
+    } else if (dp_t < s.tiles) {
+      t = dp_t;
+      kb = 0;
+      ke = s.iters;
+      slab = -1;
+      dp_t += s.grid;
+    } else {
+      break;
+    }
+    // (64-bit divisions run on the VALU: pin the unit's scalars to SGPRs, or every buffer
+    // descriptor / soffset built from them becomes a waterfall loop)
+    t = __builtin_amdgcn_readfirstlane(t);
+    kb = __builtin_amdgcn_readfirstlane(kb);
+    ke = __builtin_amdgcn_readfirstlane(ke);
+    slab = __builtin_amdgcn_readfirstlane(slab);
+    const int prob = (s.nprob > 1 && t >= s.tiles0) ? 1 : 0;
+    const GemmArgs& p = g.p[prob];
+    const int tl = t - prob * s.tiles0;
+    int tm, tn, tile_, slice_;
+    tile_coords(tl, p.M / kSkB, p.N / kSkB, 1, tm, tn, tile_, slice_);
+    const int m0 = tm * kSkB, n0 = tn * kSkB;
+    const SkOperand oa = sk_operand<A_KC>(p.A, p.lda, m0, kb, wave, lane);
+    const SkOperand ob = sk_operand<B_KC>(p.B, p.ldb, n0, kb, wave, lane);
+    f32x4_t acc[8][8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    sk_mainloop<A_KC, B_KC, NS>(acc, smem, oa, ob, ke - kb, wave, wm, wn, lane);
+
+    if (slab >= 0) {
+      // ---- stream-K hand-off (write-through slabs, one ticket per contributor)
+      constexpr int kSc1 = 16;
+      const auto rs_own = __builtin_amdgcn_make_buffer_rsrc(g.ws + static_cast<int64_t>(slab) * kSkSlab, 0, kSkSlab * 4,
+                                                            0x00020000);
+      static_for<64>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[c / 8][c % 8]), rs_own,
+                                               tid * 16, c * kSkNT * 16, kSc1);
+      });
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      const long long t0 = static_cast<long long>(t) * s.iters;
+      const int wlo = __builtin_amdgcn_readfirstlane(sk_owner(s, t0));
+      const int whi = __builtin_amdgcn_readfirstlane(sk_owner(s, t0 + s.iters - 1));
+      PZ_LDS int* flag = (PZ_LDS int*)(smem);
+      if (tid == 0) {
+        const int prev = __hip_atomic_fetch_add(g.counters + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = prev == whi - wlo;
+        *flag = last;
+        if (last) g.counters[t] = 0;  // ready for the next launch
+      }
+      __syncthreads();
+      if (__builtin_amdgcn_readfirstlane(*flag) == 0) continue;  // (uniform) another contributor finishes it
+      auto slab_of = [&](int c) { return __builtin_amdgcn_readfirstlane(2 * c + (sk_start(s, c) < t0 ? 1 : 0)); };
+      auto rs_of = [&](int c) {
+        return __builtin_amdgcn_make_buffer_rsrc(g.ws + static_cast<int64_t>(slab_of(c)) * kSkSlab, 0, kSkSlab * 4,
+                                                 0x00020000);
+      };
+#ifndef PZ_SK_NOFOLD
+      // in groups of 16 chunks (64 VGPRs of loads in flight): an unbounded unrolled fold let
+      // hipcc hoist all 64 loads (256 VGPRs) and spill
+      auto fold = [&](const auto& rs, bool first) __attribute__((always_inline)) {
+        static_for<4>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          f32x4_t ld[16];
+          static_for<16>([&](auto cc) {
+            constexpr int c = 16 * q + decltype(cc)::value;
+            ld[c - 16 * q] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, c * kSkNT * 16, kSc1));
+          });
+          static_for<16>([&](auto cc) {
+            constexpr int c = 16 * q + decltype(cc)::value;
+            acc[c / 8][c % 8] = first ? ld[c - 16 * q] : acc[c / 8][c % 8] + ld[c - 16 * q];
+          });
+          __builtin_amdgcn_sched_barrier(0);
+        });
+      };
+      if (whi - wlo == 1) {  // two contributors: own + other == the K-ordered sum (addition commutes)
+        fold(rs_of(w == wlo ? whi : wlo), false);
+      } else {  // fold every slab (own included, it was stored above) in K order
+        // (unrolled over at most kSkMaxCon contributors, sk_plan's bound: a runtime loop carried
+        // the 256 accumulators through a loop phi that hipcc could only keep in VGPRs)
+        fold(rs_of(wlo), true);
+        static_for<kSkMaxCon - 1>([&](auto kc) {
+          constexpr int k = decltype(kc)::value + 1;
+          if (wlo + k <= whi) fold(rs_of(wlo + k), false);
+        });
+      }
+#endif
+    }
+
+    // ---- epilogue
+#ifdef PZ_SK_NOEPI
+    if constexpr (true) {
+      uint16_t* C = static_cast<uint16_t*>(p.C);
+      static_for<64>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        const int m = m0 + wm * 128 + (c / 8) * 16 + (lane & 15), n = n0 + wn * 128 + (c % 8) * 16 + 4 * (lane >> 4);
+        float v[4] = {acc[c / 8][c % 8][0], acc[c / 8][c % 8][1], acc[c / 8][c % 8][2], acc[c / 8][c % 8][3]};
+        store4<uint16_t>(C + static_cast<int64_t>(m) * p.ldc + n, v);
+      });
+    } else
+#endif
+    if constexpr (EK == kSkF32) {
+      sk_store_f32(p, acc, m0, n0, wm, wn, lane);
+    } else {
+      epilogue_lds<kSkB, kSkB, 2, 2, Lay16<8, 8>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
+    }
+  }
+}
+
+int device_cus() {
+  static const int n = [] {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return cus > 0 ? cus : 256;
+  }();
+  return n;
+}
+
+// which epilogue covers these arguments (-1: none on this engine)
+int sk_epi_kind(const GemmArgs& p) {
+  if (p.out_dtype == DT_F32) {
+    if (p.epi_mode != EPI_STORE || p.mask != nullptr || p.out8 != nullptr) return -1;
+    return kSkF32;
+  }
+  if (p.out_dtype != DT_BF16 || p.accumulate) return -1;
+  if (p.epi_mode == EPI_STORE) {
+    if (p.out8 != nullptr) return -1;
+    return (p.bias == nullptr && p.colsum == nullptr && p.mask == nullptr) ? EK_STORE : EK_ANY;
+  }
+  if (p.epi_mode == EPI_FWD) {
+    const EpiSpec& e = p.epi;
+    if ((e.act == ACT_NONE || e.act == ACT_RELU) && p.colsum == nullptr) {
+      const bool relu = e.act == ACT_RELU;
+      if (!e.drop_all) {
+        if (relu && !e.drop_pre && e.drop_post) return EK_F_RELU_POST;
+        if (relu && e.drop_pre && e.drop_post) return EK_F_RELU_PREPOST;
+        if (!relu && e.drop_pre && !e.drop_post) return EK_F_PRE;
+      }
+      return EK_RELU;
+    }
+    return EK_ANY;
+  }
+  if (p.epi_mode == EPI_BWD) {
+    if (p.mask != nullptr) return p.epi.act == ACT_RELU ? EK_BWD_MASK : -1;
+    if (p.aux == nullptr || p.aux_dtype != DT_BF16 || p.ldaux % 8 != 0 || (reinterpret_cast<uintptr_t>(p.aux) & 15))
+      return -1;
+    return EK_ANY;
+  }
+  return -1;
+}
+
+SkSched sk_plan(const GemmArgs* probs, int n) {
+  SkSched s{};
+  s.nprob = n;
+  s.tiles0 = (probs[0].M / kSkB) * (probs[0].N / kSkB);
+  s.tiles = s.tiles0 + (n > 1 ? (probs[1].M / kSkB) * (probs[1].N / kSkB) : 0);
+  s.iters = probs[0].K / kSkBK;
+  const int cus = device_cus();
+  int grid = probs[0].cus > 0 ? std::min(probs[0].cus, cus) : cus;
+  const int T = s.tiles;
+  int sk = 0;
+  if (T % grid != 0) sk = T < grid ? T : T % grid + grid;
+  // a stream-K share under 8 steps per workgroup: fewer workgroups (each takes >= 8 steps)
+  if (sk > 0 && static_cast<long long>(sk) * s.iters < 8LL * grid) {
+    grid = std::max(1, static_cast<int>(static_cast<long long>(sk) * s.iters / 8));
+    sk = (T % grid == 0) ? 0 : (T < grid ? T : T % grid + grid);
+  }
+  s.grid = grid;
+  s.sk_tiles = sk;
+  s.sk_iters = static_cast<long long>(sk) * s.iters;
+  return s;
+}
+
+template <bool AKC, bool BKC, typename OutT, int EK>
+hipError_t sk_launch(const SkArgs& a, hipStream_t st) {
+  constexpr int lds = kSkNS * kSkSlot;
+  auto kern = gemm_sk_kernel<AKC, BKC, OutT, EK, kSkNS>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3(a.s.grid), dim3(kSkNT), lds, st, a);
+  return hipGetLastError();
+}
+
+hipError_t sk_dispatch(const SkArgs& a, int ek, hipStream_t st) {
+  const GemmArgs& p = a.p[0];
+#ifdef PZ_SK_ONE  // register / ISA experiments: one instantiation
+  (void)p;
+  (void)ek;
+  return sk_launch<PZ_SK_ONE>(a, st);
+#else
+  if (p.a_kc && !p.b_kc) {  // forward X · W[in, out]
+    switch (ek) {
+      case EK_STORE: return sk_launch<true, false, uint16_t, EK_STORE>(a, st);
+      case EK_RELU: return sk_launch<true, false, uint16_t, EK_RELU>(a, st);
+      case EK_F_RELU_POST: return sk_launch<true, false, uint16_t, EK_F_RELU_POST>(a, st);
+      case EK_F_RELU_PREPOST: return sk_launch<true, false, uint16_t, EK_F_RELU_PREPOST>(a, st);
+      case EK_F_PRE: return sk_launch<true, false, uint16_t, EK_F_PRE>(a, st);
+      case EK_ANY: return sk_launch<true, false, uint16_t, EK_ANY>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (p.a_kc && p.b_kc) {  // dX = dZ · Wᵀ
+    switch (ek) {
+      case EK_STORE: return sk_launch<true, true, uint16_t, EK_STORE>(a, st);
+      case EK_BWD_MASK: return sk_launch<true, true, uint16_t, EK_BWD_MASK>(a, st);
+      case EK_ANY: return sk_launch<true, true, uint16_t, EK_ANY>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  if (!p.a_kc && !p.b_kc) {  // dW = Xᵀ · dZ
+    switch (ek) {
+      case EK_STORE: return sk_launch<false, false, uint16_t, EK_STORE>(a, st);
+      case kSkF32: return sk_launch<false, false, float, kSkF32>(a, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  return hipErrorInvalidValue;
+#endif
+}
+
+}  // namespace
+
+bool sk_default() {
+  static const bool on = [] {
+    const char* e = getenv("PZ_GEMM_SK");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return on;
+}
+
+bool sk_eligible(const GemmArgs& p) {
+  if (p.force_generic || p.in_dtype != DT_BF16 || (p.out_dtype != DT_BF16 && p.out_dtype != DT_F32)) return false;
+  if (p.bias64 != nullptr || p.colsum64 != nullptr) return false;
+  if (p.M <= 0 || p.N <= 0 || p.M % kSkB != 0 || p.N % kSkB != 0 || p.K % kSkBK != 0 || p.K < 2 * kSkBK) return false;
+  if (!p.a_kc && p.b_kc) return false;  // (no MLP GEMM has this layout)
+  auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  if (!al16(p.A) || !al16(p.B) || (p.C != nullptr && !al16(p.C))) return false;
+  if (p.lda % 8 != 0 || p.ldb % 8 != 0 || p.ldc % 8 != 0 || p.idx_ld % 2 != 0) return false;
+  if (p.bias != nullptr && !al16(p.bias)) return false;
+  constexpr int64_t kLim = int64_t(1) << 32;  // buffer-addressed staging: 32-bit byte offsets
+  if ((p.a_kc ? static_cast<int64_t>(p.M) : static_cast<int64_t>(p.K)) * p.lda * 2 >= kLim) return false;
+  if ((p.b_kc ? static_cast<int64_t>(p.N) : static_cast<int64_t>(p.K)) * p.ldb * 2 >= kLim) return false;
+  if (p.mask != nullptr && (p.ldmask % 32 != 0 || (reinterpret_cast<uintptr_t>(p.mask) & 15) != 0)) return false;
+  if (p.out8 != nullptr && (p.out8_fmt != (p.epi_mode == EPI_BWD ? 1 : 0) || p.ldout8 % 8 != 0 ||
+                            (reinterpret_cast<uintptr_t>(p.out8) & 7) != 0 || p.out8_qscale == nullptr))
+    return false;
+  return sk_epi_kind(p) >= 0;
+}
+
+int sk_tickets(const GemmArgs* probs, int n) { return sk_plan(probs, n).sk_tiles; }
+
+int64_t sk_ws_floats(const GemmArgs* probs, int n) {
+  const SkSched s = sk_plan(probs, n);
+  return s.sk_tiles > 0 ? static_cast<int64_t>(2) * s.grid * kSkSlab : 0;
+}
+
+hipError_t gemm_sk(const GemmArgs* probs, int n, float* ws, int* counters, hipStream_t st) {
+  if (n < 1 || n > 2) return hipErrorInvalidValue;
+  for (int i = 0; i < n; ++i)
+    if (!sk_eligible(probs[i])) return hipErrorInvalidValue;
+  const int ek = sk_epi_kind(probs[0]);
+  if (n == 2 && (probs[1].K != probs[0].K || probs[1].a_kc != probs[0].a_kc || probs[1].b_kc != probs[0].b_kc ||
+                 sk_epi_kind(probs[1]) != ek || probs[1].out_dtype != probs[0].out_dtype))
+    return hipErrorInvalidValue;
+  SkArgs a{};
+  for (int i = 0; i < n; ++i) {
+    a.p[i] = probs[i];
+    a.p[i].store_wt = 1;
+  }
+  a.s = sk_plan(probs, n);
+  if (a.s.sk_tiles > 0 && (ws == nullptr || counters == nullptr)) return hipErrorInvalidValue;
+  a.ws = ws;
+  a.counters = counters;
+  return sk_dispatch(a, ek, st);
+}
+
+}  // namespace pz

@@ -278,11 +278,4 @@ hipError_t quantize_rows(const void* x, int dtype, int64_t ldx, int rows, int co
 // 4 KiB chunk per `step_us` each (comm_proxy.hip: one-GPU model of a ring all-reduce's kernels)
 hipError_t comm_proxy(void* scratch, int wgs, int chunk_bytes, double us, double step_us, hipStream_t s);
 
-// Device-side cross-stream ordering (stream_signal.hip): signal_set bumps counter `slot` of
-// `ctr` (one 128-byte line each) once its stream reaches it; signal_wait holds its stream until
-// that counter reaches `target` (wrap-safe), for at most `timeout_us`, then records the timeout in
-// ctr[1] of the slot and lets the stream go on.
-hipError_t signal_set(unsigned* ctr, int slot, hipStream_t s);
-hipError_t signal_wait(unsigned* ctr, int slot, unsigned target, double timeout_us, hipStream_t s);
-
 }  // namespace pz

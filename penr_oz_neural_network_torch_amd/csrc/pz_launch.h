@@ -106,7 +106,21 @@ struct GemmArgs {
   // and a GEMM that stores 64 MB of output leaves the L2s full of them
   int store_wt;
   int prio;  // s_setprio(1) around the ping-pong MFMA blocks (set by the launcher, PZ_GEMM_PRIO)
+  // persistent stream-K engine (gemm_sk.hip): workgroups = CUs it may occupy (0 = every CU; the
+  // trainer lowers it while RCCL channels hold CUs), engine 0 = default choice, 1 = the tiled
+  // kernels of gemm_mfma.hip, 2 = stream-K
+  int cus;
+  int engine;
 };
+
+// persistent stream-K engine: eligibility, workspace (fp32 floats for the partial-tile slabs of a
+// `cus`-workgroup launch; 0 = none needed) and launch over one or two problems of one layout and
+// epilogue kind (the second one's tiles follow the first's; equal K)
+bool sk_eligible(const GemmArgs& p);
+int64_t sk_ws_floats(const GemmArgs* probs, int n);
+int sk_tickets(const GemmArgs* probs, int n);  // per-tile ticket counters needed
+hipError_t gemm_sk(const GemmArgs* probs, int n, float* ws, int* counters, hipStream_t stream);
+bool sk_default();  // PZ_GEMM_SK: the engine gemm() picks for eligible shapes
 
 // split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().
 int gemm_split(const GemmArgs& args);

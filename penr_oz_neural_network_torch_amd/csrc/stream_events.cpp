@@ -73,32 +73,9 @@ double event_elapsed_op(int64_t start, int64_t end) {
   return ms;
 }
 
-// device-side signals (stream_signal.hip): `ctr` holds one 32-word slot per signal
-unsigned* signal_slot(const at::Tensor& ctr, int64_t slot) {
-  TORCH_CHECK(ctr.is_cuda() && ctr.scalar_type() == at::kInt && ctr.is_contiguous(),
-              "pz signals: a contiguous int32 device tensor");
-  TORCH_CHECK(slot >= 0 && (slot + 1) * 32 <= ctr.numel(), "pz signals: slot ", slot, " out of range");
-  return reinterpret_cast<unsigned*>(ctr.data_ptr<int32_t>());
-}
-
-void signal_set_op(const at::Tensor& ctr, int64_t slot) {
-  unsigned* p = signal_slot(ctr, slot);
-  check(pz::signal_set(p, static_cast<int>(slot), current(ctr.device().index())), "signal_set");
-}
-
-void signal_wait_op(const at::Tensor& ctr, int64_t slot, int64_t target, double timeout_us) {
-  unsigned* p = signal_slot(ctr, slot);
-  TORCH_CHECK(timeout_us > 0.0, "pz signals: a positive timeout");
-  check(pz::signal_wait(p, static_cast<int>(slot), static_cast<unsigned>(target & 0xffffffffLL), timeout_us,
-                        current(ctr.device().index())),
-        "signal_wait");
-}
-
 }  // namespace
 
 TORCH_LIBRARY_FRAGMENT(pz, m) {
-  m.def("signal_set(Tensor ctr, int slot) -> ()");
-  m.def("signal_wait(Tensor ctr, int slot, int target, float timeout_us) -> ()");
   m.def("event_create(int device, int kind=0) -> int");
   m.def("event_record(int ev, int device) -> ()");
   m.def("event_wait(int ev, int device) -> ()");
@@ -114,6 +91,4 @@ TORCH_LIBRARY_IMPL(pz, CompositeExplicitAutograd, m) {
   m.impl("event_query", TORCH_FN(event_query_op));
   m.impl("event_destroy", TORCH_FN(event_destroy_op));
   m.impl("event_elapsed", TORCH_FN(event_elapsed_op));
-  m.impl("signal_set", TORCH_FN(signal_set_op));
-  m.impl("signal_wait", TORCH_FN(signal_wait_op));
 }

@@ -9,55 +9,34 @@ kept (capture records them as graph dependencies).
 """
 from __future__ import annotations
 
-import os
-
 import torch
 
 
 class _Native:
-    __slots__ = ("h", "dev")
+    """A device-scope ordering event. ``pending``: recorded, and no wait enqueued on that record
+    yet — the ring never re-records such an entry (its waiter would order against the wrong
+    stream)."""
+    __slots__ = ("h", "dev", "pending")
 
     def __init__(self, h: int, dev: int):
-        self.h, self.dev = h, dev
+        self.h, self.dev, self.pending = h, dev, False
 
     def record(self, stream) -> None:
         with torch.cuda.stream(stream):
             torch.ops.pz.event_record(self.h, self.dev)
+        self.pending = True
 
     def wait(self, stream) -> None:
         with torch.cuda.stream(stream):
             torch.ops.pz.event_wait(self.h, self.dev)
-
-
-class _Signal:
-    """Device-side ordering (csrc/stream_signal.hip): ``record`` launches a one-wave kernel that
-    bumps this entry's counter, ``wait`` a one-wave kernel that holds the stream until the counter
-    has reached that record's count. The compute stream pays ~1.5 us per record instead of the ~7 us
-    of an event with a cross-stream waiter (profiles/r4_packet_gap.txt). Two streams only: a
-    re-record of the entry on either stream is ordered after every wait on the previous record.
-    Off by default (PZ_DEV_SIG=1): the waiting wave holds a CU for as long as it waits, and the
-    256-CU-quantised GEMMs beside it need an extra round (mlp4 1.49 vs 1.09 ms, see
-    csrc/stream_signal.hip)."""
-    __slots__ = ("ctr", "slot", "n", "timeout_us")
-
-    def __init__(self, ctr: torch.Tensor, slot: int, timeout_us: float):
-        self.ctr, self.slot, self.n, self.timeout_us = ctr, slot, 0, timeout_us
-
-    def record(self, stream) -> None:
-        self.n += 1
-        with torch.cuda.stream(stream):
-            torch.ops.pz.signal_set(self.ctr, self.slot)
-
-    def wait(self, stream) -> None:
-        with torch.cuda.stream(stream):
-            torch.ops.pz.signal_wait(self.ctr, self.slot, self.n, self.timeout_us)
+        self.pending = False
 
 
 class _Torch:
     __slots__ = ("ev",)
 
-    def __init__(self, timing: bool = False):
-        self.ev = torch.cuda.Event(enable_timing=timing)
+    def __init__(self):
+        self.ev = torch.cuda.Event()
 
     def record(self, stream) -> None:
         self.ev.record(stream)
@@ -67,37 +46,33 @@ class _Torch:
 
 
 class StreamEvents:
-    """A ring of device-scope ordering events (re-recorded round robin: every wait on a record is
-    enqueued before the ring comes back to it — far fewer than ``ring`` events per step) and
-    fence-free timestamp events, one per step until :meth:`release`."""
+    """A ring of device-scope ordering events, re-recorded round robin, and fence-free timestamp
+    events, one per step until :meth:`release`. An entry whose record still has no waiter when the
+    ring comes back to it is replaced by a fresh event (the ring grows instead of silently
+    re-ordering a waiter against the other stream: a schedule with more records per step than the
+    ring, e.g. many GEMM layers, stays correct)."""
 
     def __init__(self, device: torch.device, ring: int = 64):
         self.dev = device.index if device.index is not None else torch.cuda.current_device()
-        # PZ_TORCH_EVENTS=1: the system-fenced events of before (A/B)
-        self.fenced = os.environ.get("PZ_TORCH_EVENTS", "0") == "1"
-        # PZ_DEV_SIG=1: device-side counters instead of events for the ordering ring (A/B)
-        self.signals = os.environ.get("PZ_DEV_SIG", "0") == "1" and not self.fenced
-        self._ctr = None
-        if self.signals:
-            self._ctr = torch.zeros(ring * 32, dtype=torch.int32, device=torch.device("cuda", self.dev))
-            # a waiter gives up after 5 s and records it (timeouts()): the grid always drains
-            self._ring = [_Signal(self._ctr, i, 5e6) for i in range(ring)]
-        else:
-            self._ring = [_Native(torch.ops.pz.event_create(self.dev, 0), self.dev) for _ in range(ring)]
+        self._ring = [_Native(torch.ops.pz.event_create(self.dev, 0), self.dev) for _ in range(ring)]
+        self._retired: list[int] = []  # replaced entries, destroyed by release() / close()
         self._next = 0
         self._stamps: list[int] = []
 
     def sync(self, capture: bool = False):
         """An ordering event: ``.record(stream)`` then ``.wait(other_stream)``."""
-        if capture or self.fenced:
+        if capture:
             return _Torch()
         ev = self._ring[self._next]
+        if ev.pending:  # still awaited: never re-record it
+            self._retired.append(ev.h)
+            ev = self._ring[self._next] = _Native(torch.ops.pz.event_create(self.dev, 0), self.dev)
         self._next = (self._next + 1) % len(self._ring)
         return ev
 
     def stamp(self, stream) -> int:
         """Record a timestamp on ``stream``; returns its handle for :meth:`elapsed`."""
-        h = torch.ops.pz.event_create(self.dev, 2 if self.fenced else 1)
+        h = torch.ops.pz.event_create(self.dev, 1)
         self._stamps.append(h)
         with torch.cuda.stream(stream):
             torch.ops.pz.event_record(h, self.dev)
@@ -108,29 +83,27 @@ class StreamEvents:
         return float(torch.ops.pz.event_elapsed(start, end))
 
     def release(self, keep: int | None = None) -> None:
-        """Destroy the timestamps recorded so far (after a synchronize), except ``keep``."""
+        """Destroy the timestamps recorded so far and the replaced ring entries (after a
+        synchronize), except ``keep``."""
         for h in self._stamps:
             if h != keep:
                 torch.ops.pz.event_destroy(h)
         self._stamps = [keep] if keep is not None else []
-
-    def timeouts(self) -> int:
-        """Signal waits that gave up (read after a synchronize; 0 with events)."""
-        if self._ctr is None:
-            return 0
-        return int(self._ctr.view(-1, 32)[:, 1].sum().item())
+        for h in self._retired:
+            torch.ops.pz.event_destroy(h)
+        self._retired = []
 
     def close(self) -> None:
+        """Destroy every event (after a synchronize: nothing may still be recorded or awaited)."""
         self.release()
         for ev in self._ring:
-            if isinstance(ev, _Native):
-                torch.ops.pz.event_destroy(ev.h)
+            torch.ops.pz.event_destroy(ev.h)
         self._ring = []
 
-    def __del__(self):  # (a trainer dropped without close(); nothing to do at interpreter exit)
-        try:
-            if self._ring or self._stamps:
-                torch.cuda.synchronize(self.dev)
-                self.close()
-        except Exception:
-            pass
+    def abandon(self) -> None:
+        """Drop the events WITHOUT synchronizing or destroying them (a failed run whose streams may
+        never drain: a device synchronize could hang on a stuck collective). The handles leak."""
+        self._ring, self._retired, self._stamps = [], [], []
+
+    # No __del__: a synchronize from the garbage collector could land inside another trainer's
+    # hipGraph capture and invalidate it. A trainer dropped without close() leaks its handles.

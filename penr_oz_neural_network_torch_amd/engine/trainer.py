@@ -226,14 +226,11 @@ class FusedTrainer:
         self.opt.init_stats()
         # fp8 policy: ONE e4m3 copy per GEMM weight in its natural [in, out] layout — the forward
         # reads it N-contiguous (transposing 8-bit LDS reads), the backward dX GEMM K-contiguous —
-        # + per-tensor {q, s} records. PZ_FP8_WT=1: the former [out, in] transposed forward copy
-        # (a transpose-quantise pass per update; A/B)
+        # + per-tensor {q, s} records. Widths that are not multiples of 256 (the natural-layout
+        # forward GEMM stages B as whole 256-byte rows) keep an [out, in] transposed forward copy.
         self.fp8 = model.precision.name == "fp8"
-        # (the natural-layout forward GEMM stages B as whole 256-byte rows: every width % 256)
-        self._w8_nat = os.environ.get("PZ_FP8_WT", "0") != "1" and all(
-            st.seg_w.shape[1] % 256 == 0 for st in self.stages if st.kind == "gemm")
+        self._w8_nat = all(st.seg_w.shape[1] % 256 == 0 for st in self.stages if st.kind == "gemm")
         self.w8_kc = not self._w8_nat  # the forward operand's layout (K-contiguous = transposed copy)
-        self._fp8_bwd_env = os.environ.get("PZ_FP8_BWD", "1") != "0"
         self.w8: dict[int, torch.Tensor] = {}
         self._w8_fused = False
         if self.fp8:
@@ -272,7 +269,7 @@ class FusedTrainer:
                     continue
                 self.w8[st.seg_w.offset] = torch.empty(st.seg_w.shape[1], st.seg_w.shape[0], device=self.dev,
                                                        dtype=torch.float8_e4m3fn)
-                if k > 0 and self._fp8_bwd_env:  # dX operand of layers 2..n
+                if k > 0:  # dX operand of layers 2..n
                     self.w8n[st.seg_w.offset] = torch.empty(st.seg_w.shape, device=self.dev,
                                                             dtype=torch.float8_e4m3fn)
             self._refresh_fp8_weights()
@@ -281,8 +278,8 @@ class FusedTrainer:
             # natural layout: the optimizer writes the e4m3 copy itself with DELAYED weight scaling
             # (q from the amax the previous update reduced; the first update falls back to the
             # initial copies' current scale) — no quantisation pass re-reading the fp32 weights
-            # behind every update. PZ_FP8_WFUSE=0: the separate current-scaled quantise launch.
-            if self._w8_nat and os.environ.get("PZ_FP8_WFUSE", "1") != "0":
+            # behind every update.
+            if self._w8_nat:
                 self._w8_fused = True
                 self.opt.set_w8([{st.seg_w.offset: (self.w8[st.seg_w.offset],
                                                     self.wamax2[1 - p % 2, st.w8_index:st.w8_index + 1],
@@ -291,29 +288,15 @@ class FusedTrainer:
         # Optimizer overlap: each GEMM weight is updated on a side stream as soon as its gradient
         # bucket is complete (its dW GEMM on one GPU, its all-reduce under DP), while the rest of
         # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
+        # PZ_OPT_OVERLAP=0: every update on the compute stream, after the backward.
         self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
-        # PZ_OPT_PRIO=-1: the side stream at high priority (its workgroups are dispatched ahead of
-        # a GEMM's pending ones); within noise of priority 0 (profiles/r2_ab_opt_sched.txt)
-        prio = int(os.environ.get("PZ_OPT_PRIO", "0"))
-        self.opt_stream = torch.cuda.Stream(device=self.dev, priority=prio) if self.overlap else None
-        # PZ_MAIN_PRIO=-1 (A/B): the step's compute stream at high priority, so the dispatcher hands
-        # CUs that free up to the GEMMs' pending workgroups before the side stream's updates
-        mp = int(os.environ.get("PZ_MAIN_PRIO", "0"))
-        self._main_stream = torch.cuda.Stream(device=self.dev, priority=mp) if (mp < 0 and self.overlap) else None
-        self._main_synced = False
-        # PZ_OPT_SERIAL=1 (one process): the overlap schedule's update launches (grouping, pairing,
-        # order) enqueued on the COMPUTE stream where they fall, with no cross-stream events: every
-        # record / wait costs the compute stream ~7 us of packet processing (r4 step timeline), and
-        # an update beside a one-tile-per-CU GEMM slows the GEMM by about its own duration anyway
-        self._serial = False
+        self.opt_stream = torch.cuda.Stream(device=self.dev) if self.overlap else None
         self._g8_done: dict = {}  # stage index -> the dZ tensor whose e5m2 copy is current this step
         self._g8_epi_ready: set = set()  # stages whose epilogue-written e5m2 dZ scale is calibrated
         self._y_dead_cache: dict = {}  # fp8 policy: which bf16 GEMM outputs go unwritten (_y_dead)
         self._grad_su_pending = False  # fp8: a gradient scale update waits for the next step's gather
         self._act_su = None            # fp8: this step's activation scale update (folded into the head)
         self._run_epoch = None
-        # PZ_FP8_DW=0: bf16 weight-gradient GEMMs under the fp8 policy
-        self._fp8_dw_on = os.environ.get("PZ_FP8_DW", "1") != "0"
         # one launch per GEMM weight except the first layer's, which comes last anyway and
         # shares the final launch with the small accumulated parameters (biases, BN, embedding)
         gemm_w = [st.seg_w.offset for st in self.stages if st.kind == "gemm"]
@@ -332,56 +315,11 @@ class FusedTrainer:
                          and not self.fp8)
         self._fuse_ok: dict = {}
         self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
-        self._after_dx = os.environ.get("PZ_OPT_AFTER_DX", "1") == "1"  # measured 0.6% faster on one GPU
-        # first-layer dW under DP in row chunks (chunk c's bucket travels while chunk c+1 runs).
-        # Off by default: the chunk GEMMs ([512, 4096] x K 8192 on mlp4) need split-K 8 and took
-        # 71 + 80 us against 76 us for the whole dW (r4 step profile at world 1), more than the
-        # half bucket they hide (8 MB bf16 over an 8-rank ring: ~25 us at 300 GB/s)
-        self._dw_chunks = max(1, int(os.environ.get("PZ_DW_CHUNKS", "1")))
         self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
-        # PZ_OPT_MERGE=1: the side-stream updates of all layers but the first are queued together
-        # behind the last of their gradients (one event instead of one per layer). Default on:
-        # same-box A/B x3 mlp4 1.311-1.320 vs 1.321-1.326 ms, fp8 mlp8192 0.867 vs 0.869 ms;
-        # deep16x8192 (SGD) within noise. PZ_OPT_MERGE=0 queues one update per layer.
-        self._merge_side = os.environ.get("PZ_OPT_MERGE", "1") == "1"
+        # the side-stream updates of all layers but the first are queued together behind the last
+        # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
-        # PZ_OPT_SIDE_GRID=G (> 0): the merged side-stream update runs on at most G workgroups, a
-        # smaller share of the HBM beside the step-boundary launches on the compute stream (A/B)
-        self._side_grid = int(os.environ.get("PZ_OPT_SIDE_GRID", "0"))
-        # PZ_OPT_TRICKLE=G (> 0): the LARGEST side-updated weight is updated right behind its dW
-        # GEMM by a G-workgroup launch that streams beside the remaining backward GEMMs (a few CUs'
-        # worth of HBM traffic) instead of joining the merged updates after the last dX GEMM
-        # (bf16 / fp32 policies: the update writes the other shadow parity)
-        self._trickle = int(os.environ.get("PZ_OPT_TRICKLE", "0"))
-        self._trickle_key = None
-        if self._trickle > 0 and len(gemm_w) > 1 and not self.fp8:
-            sizes = {st.seg_w.offset: st.seg_w.numel for st in self.stages if st.kind == "gemm"}
-            self._trickle_key = max(gemm_w[1:], key=lambda k: sizes[k])
         self._side_pending: list = []
-        # PZ_OPT_DEFER=1: the largest side-updated weight is updated only after the first-layer /
-        # bias launch, so that launch (on the critical path) gets the HBM to itself. Off: the next
-        # fwd_L1 then runs beside that update at ~175 instead of ~95 us (mlp4 1.251-1.254 vs
-        # 1.229-1.232 ms, profiles/r2_ab_opt_defer.txt)
-        self._defer = os.environ.get("PZ_OPT_DEFER", "0") == "1" and len(gemm_w) > 1
-        sizes = {st.seg_w.offset: st.seg_w.numel for st in self.stages if st.kind == "gemm"}
-        self._defer_key = max(gemm_w[1:], key=lambda k: sizes[k]) if self._defer else None
-        self._deferred: list = []
-        # Backward ORDER (one process, side-stream updates): the weight-gradient GEMM of the
-        # LARGEST GEMM weight after the first layer is issued LAST, behind the dX chain and the
-        # first layer's dW. Every other update — the first-layer weight and the biases included —
-        # then runs on the side stream beside that long GEMM instead of after it, and the largest
-        # update runs beside the next step's first forward GEMM (which does not read that weight).
-        # The step's tail shrinks to the launch that queues it. PZ_BWD_ORDER=0: the reference
-        # order (dW then dX per layer, first-layer + bias update on the critical path). Not under
-        # data parallelism: there the last bucket's all-reduce is exposed, so the backward ends
-        # on the smallest dW (the first layer's, chunked).
-        self._late_idx = None
-        if (os.environ.get("PZ_BWD_ORDER", "0") == "1" and not self.ctx.enabled and not self.fuse_opt
-                and self.overlap and len(gemm_w) > 1):
-            cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
-            if cands:
-                self._late_idx = max(cands, key=lambda st: (st.seg_w.numel, st.index)).index
-        self._late_dw = None       # (stage, x_in, dZ) of the deferred weight-gradient GEMM
         # PAIRED weight-gradient GEMMs (one process): the dW GEMM of the GEMM stage after the first
         # with the fewest output tiles is deferred to the end of the backward and launched
         # TOGETHER with the first layer's (pz::gemm_pair): two skinny GEMMs that alone each need a
@@ -391,16 +329,10 @@ class FusedTrainer:
         self._pair_idx = None
         if (os.environ.get("PZ_DW_PAIR", "1") == "1" and not self.ctx.enabled and not self.fuse_opt
                 and self.overlap and self.stages[0].kind == "gemm"):
-            cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0 and st.index != self._late_idx]
+            cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
             if cands:
                 self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
         self._pair_dw = None       # (stage, x_in, dZ) of the dW GEMM that waits for its partner
-        self._serial = (self.overlap and not self.ctx.enabled and self._late_idx is None
-                        and os.environ.get("PZ_OPT_SERIAL", "0") == "1")
-        self._fwd_waits: dict = {}  # stage index -> event the next step's forward waits for
-        self._pf_args = None       # (epoch, parity, batch) of the sample _prefetch gathers next
-        self._pf_ready = None      # ((epoch, parity, batch, data id), event) of a gathered sample
-        self.prefetched_steps = 0  # steps that consumed a prefetched sample
         self._opt_done = None
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
         self._ov = None
@@ -483,7 +415,6 @@ class FusedTrainer:
         softmax head, ``[N, out]`` regression targets otherwise.
         """
         self._validate(inputs, targets.reshape(-1) if self.head == "softmax" else None)
-        self._main_synced = False  # (PZ_MAIN_PRIO: the step stream waits for this upload)
         host = torch.float64 if self.master == torch.float64 and self.stages[0].kind != "embed" else torch.float32
         self.data = self._table(inputs.to(dtype=host))
         self.block = self.data.shape[1] if self.stages[0].kind == "embed" else 1
@@ -506,14 +437,11 @@ class FusedTrainer:
         self._invalidate_graphs()  # captured steps point at the old buffers
         dev, cd = self.dev, self.compute
         pos = self.block
-        # sampled inputs / labels / picks, one set per weight-shadow parity: the NEXT step's sample
-        # can be gathered into the other set while this step still reads its own (_prefetch)
-        self._sample_sets = [(torch.empty(rows_b, self.data.shape[1], device=dev, dtype=torch.float32 if
-                                          self.stages[0].kind == "embed" else cd),
-                              torch.empty(rows_b, device=dev, dtype=torch.int64) if self.head == "softmax" else None,
-                              torch.empty(rows_b, device=dev, dtype=torch.int64)) for _ in range(2)]
-        self.x_in, self.lab, self.picked = self._sample_sets[0]
-        self._pf_ready = None
+        # sampled inputs / labels / picks
+        self.x_in = torch.empty(rows_b, self.data.shape[1], device=dev,
+                                dtype=torch.float32 if self.stages[0].kind == "embed" else cd)
+        self.lab = torch.empty(rows_b, device=dev, dtype=torch.int64) if self.head == "softmax" else None
+        self.picked = torch.empty(rows_b, device=dev, dtype=torch.int64)
         self.tgt = torch.empty(rows_b, self.targets.shape[1], device=dev, dtype=cd) if self.targets is not None \
             else None
         for st in self.stages:
@@ -581,44 +509,22 @@ class FusedTrainer:
             if w8n is not None:  # [in, out] copy for the backward dX GEMM, same scale
                 ops.quantize_rows(w, w8n, self.wqs[k], None)
 
-    def _opt_async(self, items: list, max_grid: int = 0) -> None:
+    def _opt_async(self, items: list) -> None:
         """Queue the updates of optimizer groups ``[(key, handles, stages)]`` on the side stream
         behind their gradients: ONE event recorded on the compute stream for all of them (each
         record / cross-stream wait costs the compute stream a few microseconds of idle)."""
         main, l2, scale = self._ov
-        if self._serial:  # in stream order on the compute stream (no events)
-            for key, handles, stages in items:
-                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity, max_grid)
-                if self.fp8:
-                    for st in stages:
-                        self._refresh_fp8_weights(st, 1 - self.parity)
-            return
         ready = self.events.sync(self._capturing)
         ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             ready.wait(self.opt_stream)
-            if self._pf_args is not None:
-                self._prefetch()
             for key, handles, stages in items:
                 for h in handles:
                     self.ctx.wait_one(h)
-                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity, max_grid)
+                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
                 if self.fp8:
                     for st in stages:
                         self._refresh_fp8_weights(st, 1 - self.parity)
-
-    def _prefetch(self) -> None:
-        """Gather the next step's minibatch into the other sample set (current stream: the side
-        stream, after the event that orders it behind everything the previous step read)."""
-        epoch, sel, batch = self._pf_args
-        self._pf_args = None
-        x, lab, picked = self._sample_sets[sel]
-        seed = self._gather_seed(epoch)
-        torch.ops.pz.gather_rows(self.data, None, seed[0], seed[1], x, batch, self.labels, lab, picked, None, None,
-                                 None)
-        ev = self.events.sync(self._capturing)
-        ev.record(torch.cuda.current_stream(self.dev))
-        self._pf_ready = ((epoch, sel, batch, id(self.data)), ev)
 
     def _plan_fp8(self, rows_b: int) -> None:
         """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
@@ -662,7 +568,7 @@ class FusedTrainer:
             # (the [in, out] e4m3 copy is single-buffered: the update of W must not run before this
             # step's dX GEMM has read it — true with the updates queued after the dX GEMMs)
             if (st.kind != "gemm" or not st.fp8 or prev is None or prev.kind != "gemm" or not prev.has_epi
-                    or st.seg_w.offset not in self.w8n or not self._fp8_bwd_env or not self._after_dx):
+                    or st.seg_w.offset not in self.w8n):
                 continue
             if st.out_width % 64 or prev.out_width % 8 or rows_b < 64:
                 continue
@@ -674,7 +580,7 @@ class FusedTrainer:
         for i, st in enumerate(self.stages):
             st.g8_from_epi = False
             nxt = self.stages[i + 1] if i + 1 < len(self.stages) else None
-            if (not self._fp8_dw_on or st.kind != "gemm" or not st.fp8 or getattr(st, "fp8_bwd", False)
+            if (st.kind != "gemm" or not st.fp8 or getattr(st, "fp8_bwd", False)
                     or nxt is None or nxt.kind != "gemm" or not st.has_epi or st.out_width % 256
                     or st.in_width % 256 or rows_b % 64):
                 continue
@@ -754,7 +660,6 @@ class FusedTrainer:
         ``lr_schedule(epoch) -> lr`` (the learning rate :meth:`step` will be called with) enables
         hipGraph replay: the per-epoch optimizer hyper-parameters are tabulated on the device
         once, so a captured step needs nothing from the host but a replay."""
-        self._main_synced = False
         self._alloc_progress(epochs)
         self._invalidate_graphs()
         self._plan = None
@@ -787,16 +692,6 @@ class FusedTrainer:
         self._warm = set()
 
     def step(self, epoch: int, lr: float, sample_size: int, dropout: float, l2: float, want_ratios: bool,
-             record: bool, indices: torch.Tensor | None = None) -> None:
-        if self._main_stream is None:
-            return self._step(epoch, lr, sample_size, dropout, l2, want_ratios, record, indices)
-        if not self._main_synced:  # once: everything the caller enqueued so far (data, weights)
-            self._main_stream.wait_stream(torch.cuda.current_stream(self.dev))
-            self._main_synced = True
-        with torch.cuda.stream(self._main_stream):
-            return self._step(epoch, lr, sample_size, dropout, l2, want_ratios, record, indices)
-
-    def _step(self, epoch: int, lr: float, sample_size: int, dropout: float, l2: float, want_ratios: bool,
               record: bool, indices: torch.Tensor | None = None) -> None:
         """One training epoch. ``indices`` (int64, this rank's ``batch`` rows) overrides the
         on-device sampler — used by the data-parallel equivalence tests.
@@ -809,7 +704,8 @@ class FusedTrainer:
         if sample_size < world:
             raise ValueError(f"sample size {sample_size} is smaller than the {world} data-parallel ranks")
         # the global sample is split exactly (reference :441, 460 draw sample_size rows): rank r
-        # draws rows [r*S//W, (r+1)*S//W): S % W ranks (the LAST ones) draw one row more. Every rank scales its
+        # draws rows [r*S//W, (r+1)*S//W): the S % W extra rows are spread by the floor division
+        # (S=10, W=4: 2, 3, 2, 3 rows). Every rank scales its
         # loss and gradients by 1/S (the GLOBAL sample), so the all-reduced sum is the global mean
         # with no 1/world factor — unequal shards weigh exactly by their share
         batch = (rank + 1) * sample_size // world - rank * sample_size // world
@@ -846,9 +742,6 @@ class FusedTrainer:
         if self._opt_done is not None:
             self._opt_done.wait(main)
             self._opt_done = None
-        for ev in self._fwd_waits.values():
-            ev.wait(main)
-        self._fwd_waits = {}
         self._early_done = None
         if self._ctr_epoch != epoch:
             self.epoch_ctr.fill_(epoch)
@@ -903,33 +796,15 @@ class FusedTrainer:
             idx = indices.to(device=self.dev, dtype=torch.int64).contiguous()
             if idx.numel() < batch:
                 raise ValueError(f"need {batch} indices, got {idx.numel()}")
-        self.x_in, self.lab, self.picked = self._sample_sets[self.parity]
         if self.fp8:
             self.aqs = self._aqs_store[self.parity]
-        pf, self._pf_ready = self._pf_ready, None
-        if pf is not None and idx is None and not capture and pf[0] == (epoch, self.parity, batch, id(self.data)):
-            pf[1].wait(main)  # gathered by the previous step's side stream (_prefetch)
-            self.prefetched_steps += 1
-        else:
-            # the previous step's gradient amax -> this step's e5m2 scales rides on the gather
-            # (delayed scaling: nothing reads them before this step's backward)
-            su = (self.gamax, self.gqs, 2.0, 57344.0) if self._grad_su_pending else (None, None, 1.0, 448.0)
-            ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
-                            self.epoch_ctr if capture else None, self.data8,
-                            self.x8 if self.data8 is not None else None, *su)
-            self._grad_su_pending = False
-        if self._grad_su_pending:  # (prefetched sample: no gather launch to ride on)
-            ops.scale_update(self.gamax, self.gqs, 2.0, True, 57344.0)
-            self._grad_su_pending = False
-        # PZ_PREFETCH=1: the next step's sample rides on this step's side stream, beside the dW GEMM
-        # of the first layer, instead of opening the next step between HBM-bound updates. Off: the
-        # gather starves beside a one-tile-per-CU GEMM (82 us instead of 10) and slows it (dW_L1 90
-        # -> 105 us): mlp4 1.221-1.223 vs 1.210-1.212 ms (profiles/r2_ab_prefetch.txt)
-        self._pf_args = None
-        if (overlap and not capture and indices is None and self.data8 is None and self.tgt is None
-                and os.environ.get("PZ_PREFETCH", "0") == "1" and not self._launch_bound(batch)
-                and epoch + 1 < self.costs.numel()):
-            self._pf_args = (epoch + 1, 1 - self.parity, batch)
+        # the previous step's gradient amax -> this step's e5m2 scales rides on the gather
+        # (delayed scaling: nothing reads them before this step's backward)
+        su = (self.gamax, self.gqs, 2.0, 57344.0) if self._grad_su_pending else (None, None, 1.0, 448.0)
+        ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
+                        self.epoch_ctr if capture else None, self.data8,
+                        self.x8 if self.data8 is not None else None, *su)
+        self._grad_su_pending = False
         if self.tgt is not None:
             ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
@@ -944,9 +819,6 @@ class FusedTrainer:
             if self._early_done is not None and st.kind == "gemm" and st.seg_w.offset in self._early_keys:
                 self._early_done.wait(main)
                 self._early_done = self._opt_done = None
-            ev = self._fwd_waits.pop(st.index, None)
-            if ev is not None:  # reordered backward: this stage's weights were updated on the side stream
-                ev.wait(main)
             x = self._forward_stage(st, x, batch, dropout, keys, rec)
             prev = st
         last = prev
@@ -959,9 +831,6 @@ class FusedTrainer:
             self._aqs_store[1 - self.parity].copy_(self.aqs)
 
         # ---------------- head
-        for ev in self._fwd_waits.values():  # (stages skipped above: record mode, no GEMM)
-            ev.wait(main)
-        self._fwd_waits = {}
         if self._opt_done is not None:
             self._opt_done.wait(main)
             self._opt_done = None
@@ -973,18 +842,6 @@ class FusedTrainer:
             self._act_su[1].copy_(self.aqs)
             ops.scale_update(self._act_su[0], self._act_su[1], self._act_su[2], True)
             self._act_su = None
-        # PZ_PREFETCH_MAIN=1: the NEXT step's minibatch is gathered into the other sample set
-        # right here, on this stream between the head and the first backward GEMM, where it has the
-        # HBM to itself, instead of at the head of the next step (26 us there, behind the
-        # first-layer update and beside the side stream's largest one). Measured SLOWER in the step
-        # (mlp4 1.130-1.134 vs 1.115-1.119 ms, profiles/r3_ab_prefetch_main.txt): off by default.
-        # The other set was last read by the previous step's kernels, all earlier on this stream.
-        # Not for the fp8 policy (one e4m3 input copy) or regression targets.
-        if (overlap and not capture and indices is None and self.data8 is None and self.tgt is None
-                and self._pf_args is None and os.environ.get("PZ_PREFETCH_MAIN", "0") == "1"
-                and epoch + 1 < self.costs.numel()):
-            self._pf_args = (epoch + 1, 1 - self.parity, batch)
-            self._prefetch()
 
         # ---------------- backward
         self._phase("pz.backward")
@@ -1009,18 +866,13 @@ class FusedTrainer:
                    # fused e4m3 weight copies: this step's updates read the amax slot of the
                    # current parity; step_finalize clears it for the next step's updates
                    clear=self._wamax_store[self.parity] if self._w8_fused else None)
-        if overlap and self._late_dw is not None:
-            self._finish_reordered(main, l2, capture, epoch, row, fin, handles)
-            return
         if overlap:
             # the last update (first-layer weights, biases, batchnorm, embeddings) runs on THIS
             # stream right behind the last dW: the next step's first GEMM follows it in order (no
             # cross-stream wait), and it overlaps the side stream's still-running updates instead
             # of queueing behind them; step_finalize (side) waits for both
-            after_rest = self._side_after_rest()
-            late_side = sorted(self._side_pending, key=lambda it: it[2][0].index) if after_rest else []
-            if self._side_pending and not after_rest:  # (merged side updates not flushed by their last layer)
-                self._opt_async(self._side_pending, self._side_grid)
+            if self._side_pending:  # (merged side updates not flushed by their last layer)
+                self._opt_async(self._side_pending)
             self._side_pending = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
@@ -1029,47 +881,10 @@ class FusedTrainer:
                 for st in self._late_stages:
                     self._refresh_fp8_weights(st, 1 - self.parity)
             self._ov = None
-            if self._serial:
-                for key, hs, stages in late_side + self._deferred:
-                    self.opt.step_group(key, self.grads, l2, 1.0, 1 - self.parity)
-                    if self.fp8:
-                        for st in stages:
-                            self._refresh_fp8_weights(st, 1 - self.parity)
-                self._deferred = []
-                self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row,
-                                  **fin)
-                self._opt_done = self._early_done = None
-                self._fwd_waits = {}
-                if not capture:
-                    self._last_event = self.events.stamp(main)
-                self.parity = 1 - self.parity
-                self._phase(None)
-                return
             rest_ev = self.events.sync(capture)
             rest_ev.record(main)
-            fwd_waits = {}
             with torch.cuda.stream(self.opt_stream):
                 rest_ev.wait(self.opt_stream)
-                for key, hs, stages in late_side:  # paired backward: one event per updated weight
-                    for h in hs:
-                        self.ctx.wait_one(h)
-                    self.opt.step_group(key, self.grads, l2, 1.0, 1 - self.parity)
-                    if self.fp8:
-                        for st in stages:
-                            self._refresh_fp8_weights(st, 1 - self.parity)
-                    if not capture:
-                        wev = self.events.sync()
-                        wev.record(self.opt_stream)
-                        for st in stages:
-                            fwd_waits[st.index] = wev
-                for key, hs, stages in self._deferred:  # PZ_OPT_DEFER
-                    for h in hs:
-                        self.ctx.wait_one(h)
-                    self.opt.step_group(key, self.grads, l2, 1.0, 1 - self.parity)
-                    if self.fp8:
-                        for st in stages:
-                            self._refresh_fp8_weights(st, 1 - self.parity)
-                self._deferred = []
                 self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
                 ev = self.events.sync(capture)
@@ -1081,9 +896,7 @@ class FusedTrainer:
                 # side-stream-updated weight: step_finalize (behind this stream's first-layer
                 # update) finishes long before the next step's first GEMM does, and its loss-slot
                 # and statistics resets are then ordered before the head and the updates
-                self._opt_done = ev
-                self._early_done = None if after_rest else ev
-                self._fwd_waits = fwd_waits
+                self._opt_done = self._early_done = ev
                 self._last_event = self.events.stamp(self.opt_stream)
             self.parity = 1 - self.parity
             self._phase(None)
@@ -1286,69 +1099,38 @@ class FusedTrainer:
             out = self._backward_dx(st, before, g, batch, p, keys, rec)
             self._pair_dw = (st, x_in, g)
             return out
-        if st.index == self._late_idx and rec is None and self._ov is not None:
-            # reordered backward: this weight's gradient GEMM is issued after the whole dX chain
-            # (its operands — the stage input and dZ — stay untouched until then)
-            out = self._backward_dx(st, before, g, batch, p, keys, rec)
-            self._late_dw = (st, x_in, g)
-            return out
         w_grad = self._w_grad(st.seg_w)
-        # Data parallel: the first layer's gradient is the last bucket of the backward and nothing
-        # is left to hide its all-reduce behind; PZ_DW_CHUNKS=c runs its dW GEMM in c row chunks so
-        # chunk i's all-reduce travels while chunk i+1 is computed (off by default, see __init__)
-        chunks = self._dw_chunk_count(st)
-        mine = []
-        rows = w_grad.shape[0] // chunks
-        # fp8 policy: the chunks run on the e4m3 x e5m2 operands too (column slices of the stage
-        # input's e4m3 copy) — _fp8_dw_ready checked the chunk shapes, so when the bf16 dZ went
-        # unwritten (store_c=False) the e5m2 copy is always what the dW GEMM reads
+        # fp8 policy: e4m3 activations x e5m2 dZ — _fp8_dw_ready checked the shapes, so when the
+        # bf16 dZ went unwritten (store_c=False) the e5m2 copy is always what the dW GEMM reads
         f8 = self._fp8_dw(st, g, w_grad)
         # (measured, not kept: these dW GEMMs on a stream of their own beside the dX chain, without
         # split-K: the concurrent GEMMs stretch each other, mlp4 1.26 vs 1.23 ms —
         # profiles/r3_ab_dw_stream.txt)
-        paired = self._pair_dw if st.index == 0 and chunks == 1 else None
+        paired = self._pair_dw if st.index == 0 else None
         self._pair_dw = None if st.index == 0 else self._pair_dw
         if paired is not None:
-            mine.append(self._run_pair(paired, st, x_in, g, w_grad, f8, handles))
-        for c in range(chunks if paired is None else 0):
-            sl = slice(c * rows, (c + 1) * rows)
-            out = w_grad[sl] if chunks > 1 else w_grad
+            mine = [self._run_pair(paired, st, x_in, g, w_grad, f8, handles)]
+        else:
             if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
                 x8, sx, g8, sg = f8
-                PF.gemm(x8[:, sl] if chunks > 1 else x8, False, g8, False, out, scale_a=sx, scale_b=sg)
+                PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
             else:
-                PF.gemm(x_in[:, sl] if chunks > 1 else x_in, False, g, False, out)
-            mine.append(self.ctx.all_reduce_async(out))
+                PF.gemm(x_in, False, g, False, w_grad)
+            mine = [self.ctx.all_reduce_async(w_grad)]
         handles.extend(mine)
-        # the update writes the OTHER shadow set: it need not wait for this layer's dX GEMM —
-        # unless the GEMMs read the fp32 master itself (float32 policy)
+        # the update writes the OTHER shadow set, but it is queued after this layer's dX GEMM
+        # (the fp8 dX operand and the float32 policy's GEMMs read the weight itself)
         own = st.seg_w.offset in self._early_keys
-        early = st.seg_w.offset in self.shadow_sets[self.parity] and not self._after_dx
         if self._ov is not None and not own:  # updated by the final launch
             self._late_stages.append(st)
             self._late_handles.extend(mine)
-        trickle = (self._ov is not None and own and st.seg_w.offset == self._trickle_key
-                   and st.seg_w.offset in self.shadow_sets[self.parity])
-        if self._ov is not None and own and (early or trickle):
-            self._opt_async([(st.seg_w.offset, mine, [st])], self._trickle if trickle else 0)
         out = self._backward_dx(st, before, g, batch, p, keys, rec)
-        if self._ov is not None and own and not early and not trickle:
-            item = (st.seg_w.offset, mine, [st])
-            (self._deferred if st.seg_w.offset == self._defer_key else self._side_pending).append(item)
-            if ((not self._merge_side or st.seg_w.offset == self._flush_key) and self._side_pending
-                    and not self._side_after_rest()):
-                self._opt_async(self._side_pending, self._side_grid)
+        if self._ov is not None and own:
+            self._side_pending.append((st.seg_w.offset, mine, [st]))
+            if st.seg_w.offset == self._flush_key and self._side_pending:
+                self._opt_async(self._side_pending)
                 self._side_pending = []
         return out
-
-    def _side_after_rest(self) -> bool:
-        """Paired backward (PZ_DW_PAIR): the side-stream updates wait for the step's last launch
-        (the first-layer / bias update on the main stream, which then has the HBM to itself right
-        behind the pair) and run beside the NEXT step's first forward GEMMs, each forward stage
-        waiting only for its own weight's update. Off by default (PZ_PAIR_SIDE=1: on): r4, one box,
-        mlp4 1.1157 / 1.1181 ms on vs 1.1011 / 1.1002 off; fp8 mlp8192 0.5229 / 0.526 vs 0.5214 / 0.5192."""
-        return (self._pair_idx is not None and self._ov is not None
-                and os.environ.get("PZ_PAIR_SIDE", "0") == "1")
 
     def _run_pair(self, paired, st0: Stage, x0, g0, w0, f8_0, handles):
         """The first layer's dW GEMM together with the deferred partner's (``_pair_idx``) in one
@@ -1380,55 +1162,6 @@ class FusedTrainer:
         self._side_pending.append((sp.seg_w.offset, [hp], [sp]))
         return self.ctx.all_reduce_async(w0)
 
-    def _finish_reordered(self, main, l2, capture, epoch, row, fin, handles) -> None:
-        """End of a reordered step (``PZ_BWD_ORDER``, one process). Main stream: the deferred
-        weight-gradient GEMM of the largest weight. Side stream, in order: every other pending
-        update (the other side-updated weights, then the first-layer weight + biases / batchnorm /
-        embedding), all beside that GEMM; then the deferred weight's own update and
-        ``step_finalize``, beside the next step's first forward GEMMs. The next step waits for the
-        first group before its first GEMM stage and for the rest before the deferred weight's
-        forward stage (``_fwd_waits``)."""
-        st, x_in, g = self._late_dw
-        self._late_dw = None
-        if self._side_pending:
-            self._opt_async(self._side_pending)
-            self._side_pending = []
-        for h in list(self._late_handles) + [handles[-1]]:
-            self.ctx.wait_one(h)
-        ready = self.events.sync(capture)
-        ready.record(main)  # the dX chain (bias column sums) and the first layer's dW are done
-        with torch.cuda.stream(self.opt_stream):
-            ready.wait(self.opt_stream)
-            self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
-            if self.fp8:
-                for s0 in self._late_stages:
-                    self._refresh_fp8_weights(s0, 1 - self.parity)
-            rest_ev = self.events.sync(capture)
-            rest_ev.record(self.opt_stream)
-        w_grad = self._w_grad(st.seg_w)
-        f8 = self._fp8_dw(st, g, w_grad)
-        if f8 is not None:
-            x8, sx, g8, sg = f8
-            PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
-        else:
-            PF.gemm(x_in, False, g, False, w_grad)
-        self._opt_async([(st.seg_w.offset, [self.ctx.all_reduce_async(w_grad)], [st])])
-        self._ov = None
-        with torch.cuda.stream(self.opt_stream):
-            self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row, **fin)
-            ev = self.events.sync(capture)
-            ev.record(self.opt_stream)
-        if capture:  # join the side stream into the capture stream
-            ev.wait(main)
-        else:
-            # stage 0 reads first-layer / embedding / batchnorm parameters of the rest group
-            self._fwd_waits = {0: rest_ev, st.index: ev}
-            self._opt_done = ev  # (the head: loss-slot reset by step_finalize)
-            self._early_done = None
-            self._last_event = self.events.stamp(self.opt_stream)
-        self.parity = 1 - self.parity
-        self._phase(None)
-
     def _quantize_g8(self, st: Stage, g):
         """dZ of an fp8 stage -> its e5m2 copy (delayed scaling; the first step calibrates on its
         own amax), once per step: the dW GEMM and the dX GEMM of the stage both consume it."""
@@ -1457,7 +1190,7 @@ class FusedTrainer:
 
     def _fp8_dw_ready(self, st: Stage) -> bool:
         """This step's dW GEMM of ``st`` will run on fp8 operands (``_fp8_dw`` returns them)."""
-        if not (self.fp8 and st.fp8 and self._fp8_dw_on and st.kind == "gemm"):
+        if not (self.fp8 and st.fp8 and st.kind == "gemm"):
             return False
         if getattr(st, "g8_from_epi", False):
             if st.index not in self._g8_epi_ready:
@@ -1468,24 +1201,12 @@ class FusedTrainer:
         w_grad = self._w_grad(st.seg_w)
         return x8 is not None and w_grad.dtype == torch.bfloat16 and self._fp8_dw_shape_ok(st, x8, w_grad)
 
-    def _dw_chunk_count(self, st: Stage) -> int:
-        """Row chunks of the stage's dW GEMM: the first layer's under data parallelism (its
-        all-reduce then travels chunk by chunk), else 1."""
-        if st.index != 0 or not self.ctx.enabled or self._dw_chunks < 2 or st.kind != "gemm":
-            return 1
-        rows = st.seg_w.shape[0]
-        return 1 if rows % (8 * self._dw_chunks) else self._dw_chunks
-
     def _fp8_dw_shape_ok(self, st: Stage, x8, w_grad) -> bool:
-        """Every chunk of the fp8 dW GEMM (x8 column slice x e5m2 dZ) takes the MFMA path."""
+        """The fp8 dW GEMM (x8 x e5m2 dZ) takes the MFMA path."""
         key = ("dwshape", st.index)
         ok = self._y_dead_cache.get(key)
         if ok is None:
-            chunks = self._dw_chunk_count(st)
-            rows = w_grad.shape[0] // chunks
-            ok = self._y_dead_cache[key] = all(
-                PF.gemm_path(x8[:, c * rows:(c + 1) * rows], False, st.buffers["g8"], False,
-                             w_grad[c * rows:(c + 1) * rows]) == "mfma" for c in range(chunks))
+            ok = self._y_dead_cache[key] = PF.gemm_path(x8, False, st.buffers["g8"], False, w_grad) == "mfma"
         return ok
 
     def _fp8_dw_ready_cached(self, st: Stage) -> bool:
@@ -1506,7 +1227,7 @@ class FusedTrainer:
         """fp8 weight-gradient operands (BASELINE config 5): the stage input's e4m3 copy (written by
         the previous GEMM's epilogue, or the gathered e4m3 dataset rows) and dZ's e5m2 copy, both
         M/N-contiguous, with their dequantisation factors — or None (bf16 dW)."""
-        if not (self.fp8 and st.fp8 and self._fp8_dw_on):
+        if not (self.fp8 and st.fp8):
             return None
         if getattr(st, "g8_from_epi", False):  # dZ's e5m2 copy came from the dX epilogue this step
             if self._g8_done.get(st.index) is not g:
@@ -1648,9 +1369,6 @@ class FusedTrainer:
         if not self._pending:
             return []
         torch.cuda.synchronize(self.dev)
-        if self.events.signals and self.events.timeouts():
-            raise RuntimeError("fused trainer: a device-side stream wait timed out (PZ_DEV_SIG=1): "
-                               "the step's cross-stream ordering was not kept")
         costs = self.costs.cpu().tolist()
         ratios = self.ratios.cpu().view(-1, max(1, self.opt.nslots)).tolist()
         out = []
@@ -1672,10 +1390,15 @@ class FusedTrainer:
             raise RuntimeError("no record-mode step has run")
         return self._record
 
-    def close(self) -> None:
-        """Release the trainer's HIP events (after its last drain)."""
-        torch.cuda.synchronize(self.dev)
-        self.events.close()
+    def close(self, ok: bool = True) -> None:
+        """Release the trainer's HIP events (after its last drain). ``ok=False`` (the run failed):
+        no device synchronize — it could wait forever on a stuck collective or a faulted stream
+        and replace the original error — the events are dropped, not destroyed."""
+        if ok:
+            torch.cuda.synchronize(self.dev)
+            self.events.close()
+        else:
+            self.events.abandon()
 
     # convenience for benchmarks / tests --------------------------------------------------
     def synchronize(self) -> None:

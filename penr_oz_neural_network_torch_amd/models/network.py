@@ -321,8 +321,10 @@ class NeuralNetworkModel(MultiLayerPerceptron):
             if trainer is not None:
                 try:
                     self._train_fused(trainer, data, **hp)
-                finally:
-                    trainer.close()  # its HIP events (engine/events.py)
+                except BaseException:
+                    trainer.close(ok=False)  # no device sync on the failure path (engine/events.py)
+                    raise
+                trainer.close()
             else:
                 self._train_autograd(data, **hp)
         except Exception:
@@ -385,7 +387,8 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                 sampler = torch.Generator().manual_seed(int(seed.item()))
         if sample_size < world:
             raise ValueError(f"sample size {sample_size} is smaller than the {world} data-parallel ranks")
-        # contiguous shards of the global sample; sample_size % world ranks (the LAST ones) take one more
+        # contiguous shards of the global sample; the sample_size % world extra rows are spread by the
+        # floor division (S=10, W=4: shards 2, 3, 2, 3)
         lo, hi = rank * sample_size // world, (rank + 1) * sample_size // world
         weight = (hi - lo) / sample_size  # this rank's share of the global mean loss
         activations = None

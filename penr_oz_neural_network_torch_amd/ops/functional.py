@@ -100,7 +100,7 @@ def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Ten
          idx_ld: int = 0, force_generic: bool = False, mask: Tensor | None = None,
          scale_a: Tensor | None = None, scale_b: Tensor | None = None, out8: Tensor | None = None,
          out8_qscale: Tensor | None = None, amax: Tensor | None = None, no_split: bool = False,
-         store_c: bool = True) -> Tensor:
+         store_c: bool = True, engine: int = 0, cus: int = 0) -> Tensor:
     """``out[M,N] = op(a) @ op(b)`` with a fused epilogue.
 
     ``a_kc``: ``a`` is stored ``[M,K]`` (else ``[K,M]``); ``b_kc``: ``b`` is stored ``[N,K]`` (else ``[K,N]``).
@@ -112,12 +112,15 @@ def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Ten
     split-K plan of a skinny shape off (a GEMM running beside others on its own stream).
     ``store_c=False`` (MFMA path, bf16 ``out``): only the side outputs — ``out8``, ``mask``,
     ``colsum`` — are written, ``out`` is not (the fp8 policy's bf16 tensors nobody reads).
+    ``engine``: 0 = the default choice, 1 = the tiled kernels (gemm_mfma.hip), 2 = the persistent
+    stream-K engine (gemm_sk.hip; raises if the shape is not eligible); ``cus`` = the CU budget of
+    the persistent engine (0 = every CU).
     """
     M, N = out.shape
     K = a.shape[1] if a_kc else a.shape[0]
     _ops().gemm(a, a_kc, b, b_kc, out, bias, aux, colsum, mode, epi[0], epi[1], alpha, accumulate,
                 M, N, K, idx_ld, force_generic, mask, scale_a, scale_b, out8, out8_qscale, amax,
-                (1 if no_split else 0) | (0 if store_c else 2))
+                (1 if no_split else 0) | (0 if store_c else 2) | ((engine & 3) << 2) | ((cus & 0xFFFF) << 16))
     return out
 
 

@@ -191,16 +191,19 @@ class TrainGroup:
     def wait_ready(self, timeout: float | None = None) -> bool:
         return self._ready.wait(timeout) and self._error is None
 
-    def _collect(self, timeout: float | None, straggler_s: float | None = None) -> list:
+    def _collect(self, timeout: float | None, straggler_s: float | None = None, rank0_grace_s: float = 0.0) -> list:
         """One reply per rank; ``None`` for a rank that did not answer (closed, or ``timeout`` s
         passed). Stops early once the watchdog marks the group lost. ``straggler_s``: once ANY
         rank has answered, the others must answer within that many seconds — a training may run
         for hours, but its ranks finish together (every step ends in a collective), so a rank
         still silent long after a peer reported is hung (a kernel that never returns, a deadlock
-        outside a collective) and must not hold the group lock forever."""
+        outside a collective) and must not hold the group lock forever. Rank 0 gets
+        ``rank0_grace_s`` more: after the last collective it still drains progress and writes the
+        final checkpoint (seconds to minutes for a large model), which no peer waits for."""
         out: list = [None] * len(self.conns)
         waiting = set(range(len(self.conns)))
         deadline = None if timeout is None else time.monotonic() + timeout
+        first = None  # when the first reply arrived (arms the straggler windows)
         while waiting and self._lost is None:
             for r in sorted(waiting):
                 c = self.conns[r]
@@ -210,12 +213,16 @@ class TrainGroup:
                         waiting.discard(r)
                 except (EOFError, OSError):
                     waiting.discard(r)
-                if straggler_s is not None and len(waiting) < len(self.conns):
-                    late = time.monotonic() + straggler_s
-                    deadline = late if deadline is None else min(deadline, late)
-                    straggler_s = None  # armed once, at the first reply
-            if deadline is not None and time.monotonic() > deadline:
+            now = time.monotonic()
+            if straggler_s is not None and first is None and len(waiting) < len(self.conns):
+                first = now
+            if deadline is not None and now > deadline:
                 break
+            if first is not None:
+                if any(r != 0 for r in waiting) and now > first + straggler_s:
+                    break
+                if 0 in waiting and now > first + straggler_s + rank0_grace_s:
+                    break
         return out
 
     def _lose(self, why: str, model_id: str | None = None, rank0_done: bool = False) -> None:
@@ -259,8 +266,10 @@ class TrainGroup:
             self._in_flight = True
             try:
                 # until every rank reported, or the group is lost; once one rank reported, the
-                # rest get the process-group timeout plus a margin
-                results = self._collect(None, straggler_s=self.timeout_s + 60.0)
+                # rest get the process-group timeout plus a margin, rank 0 also the time of its
+                # final checkpoint write (~2 us per parameter, generously)
+                grace = 120.0 + 2e-6 * float(getattr(model, "num_params", 0) or 0)
+                results = self._collect(None, straggler_s=self.timeout_s + 60.0, rank0_grace_s=grace)
             finally:
                 self._in_flight = False
             if self._lost is not None or any(m is None for m in results):

@@ -136,8 +136,6 @@ def _forced_main(rank, comm, out_path, impl="native"):
                       MASTER_PORT=str(_free_port()))
     if impl == "proxy":
         os.environ.update(PZ_COMM_CUS="16", PZ_COMM_PROXY_WGS="16")
-    if comm == "fp32":  # unchunked first-layer dW (chunks change the split-K choice = rounding)
-        os.environ["PZ_DW_CHUNKS"] = "1"
     os.environ.pop("WORLD_SIZE", None)
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown

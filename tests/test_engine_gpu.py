@@ -387,41 +387,6 @@ def test_fused_dw_update_matches_separate_launches(monkeypatch, optimizer):
         assert d.max().item() < 1e-3 and mean < 1e-6, (d.max(), mean)
 
 
-def test_prefetched_sample_matches_in_step_gather(monkeypatch):
-    """The next step's minibatch gathered ahead of time — on the main stream between this step's
-    head and backward (PZ_PREFETCH_MAIN=1) or on the side stream during the backward
-    (PZ_PREFETCH=1); both OFF by default, they measured slower in the step — is the sample the
-    step would have drawn itself: same picks, same costs."""
-    sizes = [1024, 2048, 1024, 256]  # ~110 GFLOP per step: not launch-bound, so no graph replay
-    n, S, steps = 8192, 4096, 5
-    g = torch.Generator().manual_seed(6)
-    inputs = torch.randn(n, sizes[0], generator=g)
-    labels = torch.randint(0, sizes[-1], (n,), generator=g)
-    runs = {}
-    for mode, (side, main) in {"in_step": ("0", "0"), "side": ("1", "0"), "main": ("0", "1")}.items():
-        monkeypatch.setenv("PZ_PREFETCH", side)
-        monkeypatch.setenv("PZ_PREFETCH_MAIN", main)
-        gpu, _ = _pair(sizes, ["relu", "relu", "softmax"], "adam", "bfloat16")
-        tr = FusedTrainer(gpu)
-        tr.load_tensors(inputs, labels, seed=4)
-        tr.begin(steps)
-        picks = []
-        for e in range(steps):
-            tr.step(e, 0.005, S, 0.1, 1e-3, want_ratios=False, record=e == steps - 1)
-            picks.append(tr.picked[:S].clone())
-        out = tr.drain()
-        runs[mode] = ([c for _, c, _, _ in out], torch.stack(picks).cpu(), tr.prefetched_steps)
-    c0, p0, n0 = runs["in_step"]
-    assert n0 == 0
-    assert len(set(p0[:, 0].tolist())) > 1  # the steps drew different samples
-    for mode in ("side", "main"):
-        c1, p1, n1 = runs[mode]
-        assert n1 == steps - 1, (mode, n1)  # every step after the first used the prefetch
-        assert torch.equal(p0, p1), mode
-        for a, b in zip(c0, c1):
-            assert abs(a - b) < 1e-3 * max(1.0, abs(a)), (mode, c0, c1)
-
-
 @pytest.mark.parametrize("optimizer", ["adam", "stochastic"])
 def test_graph_replay_matches_eager_steps(optimizer):
     """hipGraph-replayed steps (epoch-dependent dropout keys, sampler seeds and optimizer

@@ -43,13 +43,9 @@ def _close_fp8(got: torch.Tensor, ref: torch.Tensor) -> None:
     assert torch.all((g - r).abs() <= r.abs() * 0.125 + 2 ** -9)
 
 
-@pytest.mark.parametrize("fp8_bwd,wfuse", [("1", "1"), ("0", "1"), ("1", "0")])
-def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd, wfuse):
-    """BASELINE config 5 shape family at reduced size: [1024, 2048, 1024], batch 1024. wfuse: the
-    optimizer writes the e4m3 weight copies itself (delayed weight scaling, the default) or a
-    separate current-scaled quantisation launch follows each update (PZ_FP8_WFUSE=0)."""
-    monkeypatch.setenv("PZ_FP8_BWD", fp8_bwd)
-    monkeypatch.setenv("PZ_FP8_WFUSE", wfuse)
+def test_fp8_natural_layout_engine_path():
+    """BASELINE config 5 shape family at reduced size: [1024, 2048, 1024], batch 1024: the
+    optimizer writes the e4m3 weight copies itself (delayed weight scaling)."""
     sizes = [1024, 2048, 1024]
     algos = ["relu", "softmax"]
     n, S, steps = 8192, 1024, 12
@@ -73,15 +69,15 @@ def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd, wfuse):
         if dtype != "fp8":
             continue
         # the natural-layout path really ran: one [in, out] e4m3 copy per weight, fp8 forward on
-        # every stage, the dX GEMM of layer 2 on e5m2 x e4m3 (unless PZ_FP8_BWD=0), the first
+        # every stage, the dX GEMM of layer 2 on e5m2 x e4m3, the first
         # layer's dZ quantised by the dX epilogue and its dW GEMM on e4m3 x e5m2
         assert tr._w8_nat and not tr.w8_kc
         assert [st.fp8 for st in tr.stages] == [True, True]
-        assert [st.fp8_bwd for st in tr.stages] == [False, fp8_bwd == "1"]
+        assert [st.fp8_bwd for st in tr.stages] == [False, True]
         assert tr.stages[0].g8_from_epi and 0 in tr._g8_epi_ready
         assert tr._fp8_dw_ready_cached(tr.stages[0])
         torch.cuda.synchronize()
-        assert tr._w8_fused == (wfuse == "1")
+        assert tr._w8_fused
         gemms = [st for st in tr.stages if st.kind == "gemm"]
         amax = torch.stack([tr.store.view(st.seg_w).abs().max() for st in gemms]).cpu()
         rows = tr.wamax2.cpu()  # the last update's amax slot holds max|w|, the other was cleared
@@ -90,9 +86,8 @@ def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd, wfuse):
         for st in gemms:
             w = tr.store.view(st.seg_w)
             q = tr.wqs[st.w8_index, 0].item()
-            # current scaling: q from this amax; delayed: from the previous update's (a step of
-            # Adam moves max|w| by ~lr)
-            assert math.isclose(q, 448.0 / w.abs().max().item(), rel_tol=1e-6 if wfuse == "0" else 0.05)
+            # delayed scaling: q from the previous update's amax (a step of Adam moves max|w| by ~lr)
+            assert math.isclose(q, 448.0 / w.abs().max().item(), rel_tol=0.05)
             assert math.isclose(tr.wqs[st.w8_index, 1].item(), 1.0 / q, rel_tol=1e-6)
             w8 = tr.w8[st.seg_w.offset]
             assert w8.shape == w.shape and w8 is tr.w8n[st.seg_w.offset]  # natural [in, out], one copy
@@ -103,8 +98,7 @@ def test_fp8_natural_layout_engine_path(monkeypatch, fp8_bwd, wfuse):
         _close_fp8(tr.data8, _e4m3_ref(tr.data, xq))
         picked = tr.picked[:S]
         assert torch.equal(tr.x8[:S].view(torch.uint8), tr.data8[picked].view(torch.uint8))
-        # delayed e5m2 gradient scaling keeps moving after calibration (also when no
-        # stage runs an fp8 dX GEMM, PZ_FP8_BWD=0)
+        # delayed e5m2 gradient scaling keeps moving after calibration
         assert all(math.isfinite(v) and v > 0 for v in gqs_hist)
         assert len(set(gqs_hist[2:])) > 1, gqs_hist
         assert gqs_hist[-1] != 1.0
@@ -375,8 +369,7 @@ def _model8():
 
 
 def _rank8(rank, world, store, out_path):
-    # (chunking is off by default since r4 — it cost more GEMM time than it hid — so it is asked for)
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), PZ_DW_CHUNKS="2")
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world))
     torch.set_num_threads(2)
     dist.init_process_group("gloo", init_method=f"file://{store}", rank=rank, world_size=world)
     from penr_oz_neural_network_torch_amd.parallel.dist import DataParallelContext
@@ -390,20 +383,20 @@ def _rank8(rank, world, store, out_path):
                 indices=idx[e, rank * B8:(rank + 1) * B8])
     costs = [c for _, c, _, _ in tr.drain()]
     st0 = tr.stages[0]
-    info = {"chunks": tr._dw_chunk_count(st0), "fp8_dw": tr._fp8_dw_ready_cached(st0),
+    info = {"fp8_dw": tr._fp8_dw_ready_cached(st0),
             "calibrated": 0 in tr._g8_epi_ready}
     torch.save({"flat": model._param_store.flat.cpu(), "costs": costs, "info": info}, out_path + f".{rank}")
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_fp8_data_parallel_chunked_dw_matches_single_rank(tmp_path):
+def test_fp8_data_parallel_dw_matches_single_rank(tmp_path):
     world = 2
     out = str(tmp_path / "dp8.pt")
     mp.start_processes(_rank8, args=(world, str(tmp_path / "rdv"), out), nprocs=world, start_method="spawn")
     ranks = [torch.load(out + f".{r}", weights_only=True) for r in range(world)]
     info = ranks[0]["info"]
-    assert info == {"chunks": 2, "fp8_dw": True, "calibrated": True}, info
+    assert info == {"fp8_dw": True, "calibrated": True}, info
     model = _model8()
     w0 = model.params[0].detach().float().cpu().clone()
     tr = FusedTrainer(model)

@@ -48,3 +48,38 @@ def test_uvicorn_log_config_routes_through_the_service_format():
     assert cfg["formatters"]["default"]["format"] == main.LOG_FORMAT
     assert set(cfg["loggers"]) == {"uvicorn", "uvicorn.error", "uvicorn.access"}
     assert all(not v["propagate"] for v in cfg["loggers"].values())
+
+
+def test_progress_answers_while_train_loads_a_large_checkpoint(models_tmpdir, monkeypatch):
+    """PUT /train/ parses the checkpoint off the event loop — a /progress/ poll is
+    answered while a (slow, large) checkpoint loads, and a second PUT /train/ for the same model in
+    that window is a 409, not a second training."""
+    import threading
+    import time
+
+    with TestClient(main.app) as client:
+        assert client.post("/model/", json={"model_id": "big", "layer_sizes": [2, 4, 2],
+                                            "activation_algos": ["tanh", "softmax"]}).status_code == 200
+        real = NeuralNetworkModel.deserialize.__func__
+        loading = threading.Event()
+
+        def slow(cls, model_id, meta_only=False):
+            if not meta_only:  # the full parse of a large checkpoint
+                loading.set()
+                time.sleep(1.5)
+            return real(cls, model_id, meta_only=meta_only)
+
+        monkeypatch.setattr(NeuralNetworkModel, "deserialize", classmethod(slow))
+        data = [{"activation_vector": [i % 2, 1 - i % 2], "target_vector": [i % 2]} for i in range(40)]
+        body = {"model_id": "big", "training_data": data, "epochs": 2, "batch_size": 4}
+        res = {}
+        t = threading.Thread(target=lambda: res.setdefault("train", client.put("/train/", json=body)))
+        t.start()
+        assert loading.wait(10)
+        t0 = time.perf_counter()
+        r = client.get("/progress/", params={"model_id": "big"})
+        dt = time.perf_counter() - t0
+        assert r.status_code == 200 and dt < 0.5, dt  # (the loop is not parsing: well under the 1.5 s load)
+        assert client.put("/train/", json=body).status_code == 409  # still loading: in progress
+        t.join(30)
+        assert res["train"].status_code == 202

@@ -1,6 +1,7 @@
 """The REST service's multi-rank train group (parallel/service.py) on the CPU: ``PUT /train/``
 drives a 2-rank gloo data-parallel training (two rank processes started by the app's lifespan;
 the server process never joins the group) — the code path an 8-GPU node runs over RCCL."""
+import threading
 import time
 
 import pytest
@@ -151,6 +152,19 @@ def test_collect_straggler_deadline_and_lose_keeps_a_finished_model(models_tmpdi
     g2 = TrainGroup.__new__(TrainGroup)
     g2.conns, g2._lost = [a1], None
     assert g2._collect(None, straggler_s=0.5) == ["done"]  # nobody late: no deadline hit
+
+    # rank 0 answers last (its final checkpoint write) -- within its grace window it is
+    # not a straggler; past it, it is
+    (c0, d0), (c1, d1) = Pipe(), Pipe()
+    g3 = TrainGroup.__new__(TrainGroup)
+    g3.conns, g3._lost = [c0, c1], None
+    d1.send("done")
+    threading.Timer(0.8, lambda: d0.send("done")).start()  # after the 0.3 s peer window
+    assert g3._collect(None, straggler_s=0.3, rank0_grace_s=5.0) == ["done", "done"]
+    d1.send("done")
+    t0 = time.time()
+    assert g3._collect(None, straggler_s=0.2, rank0_grace_s=0.3) == [None, "done"]
+    assert time.time() - t0 < 10
 
     for status, rank0_done, want in (("Trained", False, "Trained"), ("Training", True, "Training"),
                                      ("Training", False, "Failed")):

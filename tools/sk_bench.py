@@ -1,0 +1,139 @@
+"""Persistent stream-K GEMM engine (csrc/gemm_sk.hip) vs the tiled kernels (csrc/gemm_mfma.hip) vs
+hipBLASLt (torch.matmul) on the flagship step's shapes.
+
+For every case: correctness of the stream-K engine against an fp32 torch reference (plain store)
+and against the tiled engine (fused epilogue), at CU budgets 256 / 240 / 200; then TFLOP/s in
+interleaved rounds (guide §5.4 rule 24), best and median, plain and fused.
+
+    python tools/sk_bench.py [case ...] [--rounds R] [--cus 256,240]
+"""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from penr_oz_neural_network_torch_amd.ops import functional as PF  # noqa: E402
+
+B = 8192
+CASES = {  # name: M, N, K, a_kc, b_kc, out dtype, fused mode
+    "fwd_L1": (B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask"),
+    "fwd_L2": (B, 4096, 4096, True, False, torch.bfloat16, "fwd_mask"),
+    "fwd_L3": (B, 1024, 4096, True, False, torch.bfloat16, "fwd_pre"),
+    "dX_L3": (B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask"),
+    "dX_L2": (B, 4096, 4096, True, True, torch.bfloat16, "bwd_mask"),
+    "dW_L3": (4096, 1024, B, False, False, torch.bfloat16, "store"),
+    "dW_L2": (4096, 4096, B, False, False, torch.bfloat16, "store"),
+    "dW_L1": (1024, 4096, B, False, False, torch.bfloat16, "store"),
+    "dW_L2f32": (4096, 4096, B, False, False, torch.float32, "store"),
+    "dX_L2aux": (B, 4096, 4096, True, True, torch.bfloat16, "bwd_aux"),
+}
+
+
+def timeit(fn, n=20, w=3):
+    for _ in range(w):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n * 1e-3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("cases", nargs="*")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--cus", default="256,240,200")
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+    dev = "cuda"
+    cus_list = [int(c) for c in args.cus.split(",")]
+    out = {}
+    torch.manual_seed(0)
+    for name, (M, N, K, akc, bkc, odt, mode) in CASES.items():
+        if args.cases and name not in args.cases:
+            continue
+        a = (torch.rand((M, K) if akc else (K, M), device=dev) * 2 - 1).to(torch.bfloat16)
+        b = (torch.rand((N, K) if bkc else (K, N), device=dev) * 2 - 1).to(torch.bfloat16)
+        c1 = torch.empty(M, N, device=dev, dtype=odt)
+        c2 = torch.empty(M, N, device=dev, dtype=odt)
+        bias = torch.randn(N, device=dev)
+        cs1 = torch.zeros(N, device=dev)
+        cs2 = torch.zeros(N, device=dev)
+        aux = torch.randn(M, N, device=dev).to(torch.bfloat16)
+        mask_w = torch.zeros(PF.relu_mask_shape(M, N), device=dev, dtype=torch.uint8)
+        mask_r = torch.randint(0, 256, PF.relu_mask_shape(M, N), device=dev, dtype=torch.uint8)
+        epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=0.2, seed=(1, 2))
+
+        def fused(c, eng, cus=0, cs=None, mk=None):
+            kw = dict(engine=eng, cus=cus)
+            if mode == "fwd_mask":
+                return lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD, epi=epi, mask=mk, **kw)
+            if mode == "fwd_pre":
+                return lambda: PF.gemm(a, akc, b, bkc, c, bias=bias, mode=PF.EPI_FWD,
+                                       epi=PF.epi_spec(drop_pre=3, p=0.2, seed=(1, 2)), **kw)
+            if mode == "bwd_mask":
+                return lambda: PF.gemm(a, akc, b, bkc, c, colsum=cs, mode=PF.EPI_BWD, epi=epi, mask=mask_r, **kw)
+            if mode == "bwd_aux":
+                return lambda: PF.gemm(a, akc, b, bkc, c, aux=aux, colsum=cs, mode=PF.EPI_BWD, epi=epi, **kw)
+            return lambda: PF.gemm(a, akc, b, bkc, c, **kw)
+
+        res = {}
+        if not args.no_check:
+            A = (a if akc else a.t()).float()
+            Bm = (b.t() if bkc else b).float()
+            ref = A @ Bm
+            scale = ref.abs().max().item()
+            for cus in cus_list:
+                PF.gemm(a, akc, b, bkc, c2, engine=2, cus=cus)
+                err = (c2.float() - ref).abs().max().item() / scale
+                # fused epilogue vs the tiled engine (same stage math; split sums may round differently)
+                m1 = torch.zeros_like(mask_w)
+                m2 = torch.zeros_like(mask_w)
+                cs1.zero_()
+                cs2.zero_()
+                fused(c1, 1, 0, cs1, m1)()
+                fused(c2, 2, cus, cs2, m2)()
+                d = (c1.float() - c2.float()).abs().max().item() / max(c1.float().abs().max().item(), 1e-30)
+                mdiff = (m1 != m2).float().mean().item()
+                csd = ((cs1 - cs2).abs().max() / cs1.abs().max().clamp_min(1e-30)).item()
+                ok = err < 1e-2 and d < 2e-2 and mdiff < 1e-3 and csd < 1e-2
+                res[f"check_cus{cus}"] = {"plain_rel_err": round(err, 6), "fused_vs_tiled": round(d, 6),
+                                          "mask_mismatch": mdiff, "colsum_rel": round(csd, 6), "ok": ok}
+                print(name, "cus", cus, res[f"check_cus{cus}"], flush=True)
+            # determinism: two stream-K runs bit-identical
+            PF.gemm(a, akc, b, bkc, c1, engine=2, cus=cus_list[-1])
+            PF.gemm(a, akc, b, bkc, c2, engine=2, cus=cus_list[-1])
+            res["deterministic"] = bool(torch.equal(c1, c2))
+        fl = 2.0 * M * N * K
+        variants = {
+            "tiled_plain": lambda: PF.gemm(a, akc, b, bkc, c1, engine=1),
+            "sk_plain": lambda: PF.gemm(a, akc, b, bkc, c2, engine=2),
+            "tiled_fused": fused(c1, 1, 0, cs1, mask_w),
+            "sk_fused": fused(c2, 2, 0, cs2, mask_w),
+        }
+        for cus in cus_list[1:]:
+            variants[f"sk_plain_cus{cus}"] = (lambda cc: (lambda: PF.gemm(a, akc, b, bkc, c2, engine=2, cus=cc)))(cus)
+        if odt == torch.bfloat16:
+            A_ = a if akc else a.t()
+            B_ = b.t() if bkc else b
+            variants["hipblaslt"] = lambda: torch.matmul(A_, B_)
+        tf = {k: [] for k in variants}
+        for _ in range(args.rounds):
+            for k, fn in variants.items():
+                tf[k].append(fl / timeit(fn) / 1e12)
+        for k, v in tf.items():
+            v.sort()
+            res[k] = {"best": round(v[-1], 1), "median": round(v[len(v) // 2], 1)}
+        out[name] = res
+        print(name, json.dumps({k: res[k] for k in variants}), flush=True)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
