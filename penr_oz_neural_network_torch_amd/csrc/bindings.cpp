@@ -253,12 +253,19 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
                 "pz::gemm: store_c=False needs the MFMA path with a bf16 C and a side output");
     p.C = nullptr;
   }
+  at::Tensor cs_ws;  // deterministic bias-gradient sums: per-tile partial rows (BM >= 128) + group rows
+  if (p.colsum != nullptr && p.out_dtype == pz::DT_BF16 && pz::deterministic()) {
+    const int parts = (p.M + 127) / 128, groups = (parts + 63) / 64;
+    cs_ws = at::empty({static_cast<int64_t>(parts + groups) * p.N}, A.options().dtype(at::kFloat));
+    p.cs_ws = cs_ws.data_ptr<float>();
+    p.cs_tickets = split_counters(((p.N + 127) / 128) * (groups + 1), A.device());
+  }
   at::Tensor ws;  // split-K / stream-K slabs: from the caching allocator, stream-ordered reuse is safe
-  // flags bits 2-3: engine (0 default, 1 tiled gemm_mfma, 2 persistent stream-K); bits 16-31: the
-  // CU budget of the persistent engine (0 = every CU)
+  // flags bits 2-3: engine (0 default, 1 tiled gemm_mfma, 2 persistent stream-K, 3 its 4-wave lab
+  // loop); bits 16-31: the CU budget of the persistent engine (0 = every CU)
   p.engine = static_cast<int>((flags >> 2) & 3);
   p.cus = static_cast<int>((flags >> 16) & 0xFFFF);
-  if ((p.engine == 2 || (p.engine == 0 && pz::sk_default())) && pz::sk_eligible(p)) {
+  if ((p.engine >= 2 || (p.engine == 0 && pz::sk_default())) && pz::sk_eligible(p)) {
     const int64_t sk_floats = pz::sk_ws_floats(&p, 1);
     int* tickets = nullptr;
     if (sk_floats > 0) {
@@ -268,7 +275,7 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
     PZ_HIP_CHECK(pz::gemm_sk(&p, 1, sk_floats > 0 ? ws.data_ptr<float>() : nullptr, tickets, cur_stream(A)));
     return;
   }
-  TORCH_CHECK(p.engine != 2, "pz::gemm: the stream-K engine cannot run this GEMM (pz::sk_eligible)");
+  TORCH_CHECK(p.engine < 2, "pz::gemm: the stream-K engine cannot run this GEMM (pz::sk_eligible)");
   // flags bit 0: no split-K (a GEMM that runs concurrently with others: its tile count need not
   // fill the CUs on its own, and it skips the in-launch reduction)
   const int64_t ws_floats = (flags & 1) ? 0 : pz::gemm_split_ws_floats(p);
@@ -435,6 +442,13 @@ void xent_head_op(const Tensor& logits, const Tensor& labels, int64_t rows_valid
   a.cols = static_cast<int>(logits.size(1));
   a.dtype = dt_of(logits);
   head_accumulators(a, loss, colsum, a.dtype == pz::DT_F64, "pz::xent_head");
+  at::Tensor cs_ws;  // deterministic bias-gradient sums: 32-row blocks' partial rows + group rows
+  if (a.colsum != nullptr && a.dtype == pz::DT_BF16 && pz::deterministic()) {
+    const int blocks = (a.rows + 31) / 32, groups = (blocks + 15) / 16;
+    cs_ws = at::empty({static_cast<int64_t>(blocks + groups) * a.cols}, logits.options().dtype(at::kFloat));
+    a.cs_ws = cs_ws.data_ptr<float>();
+    a.cs_tickets = split_counters(groups + 1, logits.device());
+  }
   a.loss_scale = loss_scale;
   if (dh.has_value() && dh->defined()) {
     TORCH_CHECK(dh->scalar_type() == logits.scalar_type() && dh->stride(1) == 1, "pz::xent_head: dh");

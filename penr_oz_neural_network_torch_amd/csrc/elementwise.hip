@@ -83,6 +83,24 @@ PZ_DEV void block_colsum_flush(A* colsum, const A* cs, int cols) {
     if (cs[c] != A(0)) atomicAdd(colsum + c, cs[c]);
 }
 
+// the bf16 heads' bias-gradient column sums: the block's wave partials (LDS [WAVES][cols]) summed in
+// wave order, then float atomics, or (a.cs_ws: deterministic) the block's partial row and the
+// ordered folds of pz_common.h det_colsum over groups of 16 blocks
+template <int WAVES>
+PZ_DEV void head_colsum_flush(const XentArgs& a, const float* cs_lds) {
+  __shared__ int det_flag;
+  for (int c = threadIdx.x; c < a.cols; c += WAVES * 64) {
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) t += cs_lds[w * a.cols + c];
+    if (a.cs_ws != nullptr) st_wt(a.cs_ws + static_cast<int64_t>(blockIdx.x) * a.cols + c, t);
+    else if (t != 0.f) atomicAdd(a.colsum + c, t);
+  }
+  if (a.cs_ws != nullptr)
+    det_colsum<WAVES * 64>(a.cs_ws, a.cs_tickets, gridDim.x, 16, blockIdx.x, a.cols, a.cols, a.colsum,
+                           (PZ_LDS int*)(&det_flag));
+}
+
 // accumulator pointers of a head: double for fp64 logits (loss64 / colsum64), float otherwise
 template <typename F> PZ_DEV F* head_loss(void* f32, void* f64);
 template <> PZ_DEV float* head_loss<float>(void* f32, void*) { return static_cast<float*>(f32); }
@@ -307,12 +325,7 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_bf16_kernel(XentArgs a) 
 #pragma unroll
         for (int e = 0; e < 8; ++e) mine[(lane + 64 * j) * 8 + e] = cs[j][e];
     __syncthreads();
-    for (int c = threadIdx.x; c < a.cols; c += WAVES * 64) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < WAVES; ++w) t += cs_lds[w * a.cols + c];
-      if (t != 0.f) atomicAdd(a.colsum + c, t);
-    }
+    head_colsum_flush<WAVES>(a, cs_lds);
   }
 }
 
@@ -554,12 +567,7 @@ __global__ void __launch_bounds__(WAVES * 64) xent_head_lean_kernel(XentArgs a) 
 #pragma unroll
       for (int q = 0; q < 8; ++q) mine[(lane + 64 * j) * 8 + q] = cs[j][q];
     __syncthreads();
-    for (int c = threadIdx.x; c < a.cols; c += WAVES * 64) {
-      float t = 0.f;
-#pragma unroll
-      for (int w = 0; w < WAVES; ++w) t += cs_lds[w * a.cols + c];
-      atomicAdd(a.colsum + c, t);
-    }
+    head_colsum_flush<WAVES>(a, cs_lds);
   }
 }
 
@@ -753,28 +761,18 @@ hipError_t xent_head(const XentArgs& in, hipStream_t s) {
   constexpr int kW = 16;         // waves per bf16 block: one row each
   const size_t ldsw = kW * lds;  // the bf16 kernel keeps one partial row per wave (up to 128 KiB)
   hipError_t le = hipSuccess;
+  if (!vec || a.cols > 2048) a.cs_ws = nullptr;  // (the general kernel: float atomics)
   // the lean kernel: the trainer's logits stage (no probabilities, dZ stored, at most the logits'
-  // pre-head dropout), row width a multiple of 512 (PZ_HEAD_LEAN=0: the general kernel, A/B)
-  static const bool lean_off = [] {
-    const char* e = getenv("PZ_HEAD_LEAN");
-    return e != nullptr && atoi(e) == 0;
-  }();
+  // pre-head dropout), row width a multiple of 512
   const EpiSpec& ep = a.epi;
   const int nch = a.cols / 512;
-  if (!lean_off && vec && a.probs == nullptr && a.dh != nullptr && a.cols % 512 == 0 && nch >= 1 && nch <= 4 &&
+  if (vec && a.probs == nullptr && a.dh != nullptr && a.cols % 512 == 0 && nch >= 1 && nch <= 4 &&
       nch != 3 && ep.act == ACT_NONE && !ep.drop_post && !ep.drop_all && a.labels != nullptr &&
       (a.out8 == nullptr || xent_head_out8_ok(a))) {
     const bool cs = a.colsum != nullptr, o8 = a.out8 != nullptr, dr = ep.drop_pre != 0;
     return launch_xent_lean(a, nch, cs, o8, dr, grid16, cs ? ldsw : 0, s);
   }
-  // PZ_HEAD_RPB=16 (A/B): 16-row blocks, one row per wave (twice the blocks and resident waves)
-  static const int rpb = [] {
-    const char* e = getenv("PZ_HEAD_RPB");
-    return e != nullptr ? atoi(e) : kBf16HeadRows;
-  }();
   if (vec && a.cols <= 512) le = launch_xent_bf16<1, kW>(a, grid16, ldsw, s);
-  else if (vec && a.cols <= 1024 && rpb == 16)
-    le = launch_xent_bf16<2, kW, 16>(a, dim3((a.rows + 15) / 16), ldsw, s);
   else if (vec && a.cols <= 1024) le = launch_xent_bf16<2, kW>(a, grid16, ldsw, s);
   else if (vec && a.cols <= 2048) le = launch_xent_bf16<4, kW>(a, grid16, ldsw, s);
   else {

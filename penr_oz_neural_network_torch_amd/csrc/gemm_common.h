@@ -152,6 +152,68 @@ PZ_DEV i16x8_t frag_mn(const PZ_LDS char* tile, int col16, int kbase, int lane) 
   return i16x8_t{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
 }
 
+// K-contiguous operand rows [row0, row0+R) x k [k0, k0+BK) -> slot [R][BK]; NW waves share it
+// FULL (buffer path, dispatcher-guaranteed full row tiles): no row clamp, so the piece's row
+// offset is wave-uniform and rides in soffset — one (BK 32) or two (BK 64: the swizzle flips
+// with the piece's parity) per-lane offsets stay live instead of one per piece (the 16 of a
+// BK 64 K-contiguous pair of operands spilled to scratch inside the loop)
+template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0, bool FULL = false>
+PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
+                     PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
+  constexpr int CPR = BK / 8;             // 16-B chunks per row
+  constexpr int RPI = 64 / CPR;           // rows per 1-KiB instruction
+  constexpr int INSTR = R / (RPI * NW);
+  static_assert(INSTR >= 1 && INSTR * RPI * NW == R, "K-contiguous stage split");
+#pragma unroll
+  for (int i = 0; i < INSTR; ++i) {
+    const int rbase = (wave * INSTR + i) * RPI;
+    const int r = rbase + lane / CPR;
+    const int chunk = (lane % CPR) ^ swz_kc<BK>(r);
+    if constexpr (BUF && FULL) {
+      const uint32_t voff = (static_cast<uint32_t>(lane / CPR) * static_cast<uint32_t>(ld) + chunk * 8) * 2u;
+      const uint32_t soff = (static_cast<uint32_t>(row0 + rbase) * static_cast<uint32_t>(ld) + static_cast<uint32_t>(k0)) * 2u;
+      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(soff), lds_addr(tile + rbase * BK * 2));
+      continue;
+    }
+    int gr = row0 + r;
+    gr = gr < rows_valid ? gr : rows_valid - 1;
+    if constexpr (BUF) {
+      const uint32_t voff = (static_cast<uint32_t>(gr) * static_cast<uint32_t>(ld) + chunk * 8) * 2u;
+      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * 2u), lds_addr(tile + rbase * BK * 2));
+    } else {
+      const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
+      glds16(src, lds_addr(tile + rbase * BK * 2));
+    }
+  }
+}
+
+// M/N-contiguous operand: k rows [k0, k0+BK) x cols [col0, col0+R) -> slot [BK][R]
+template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0>
+PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int cols_valid, int k0,
+                     PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
+  constexpr int ROW_BYTES = R * 2;
+  constexpr int CHUNKS = R / 8;
+  constexpr int ROWS_PER = 1024 / ROW_BYTES;
+  constexpr int INSTR = (BK * ROW_BYTES) / (1024 * NW);
+  static_assert(INSTR >= 1 && INSTR * 1024 * NW == BK * ROW_BYTES, "M/N-contiguous stage split");
+#pragma unroll
+  for (int i = 0; i < INSTR; ++i) {
+    const int kbase = (wave * INSTR + i) * ROWS_PER;
+    const int kr = kbase + lane / CHUNKS;
+    const int chunk = (lane % CHUNKS) ^ swz_mn(kr);
+    int gc = col0 + chunk * 8;
+    gc = gc < cols_valid ? gc : cols_valid - 8;
+    if constexpr (BUF) {
+      const uint32_t voff = (static_cast<uint32_t>(kr) * static_cast<uint32_t>(ld) + gc) * 2u;
+      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * static_cast<uint32_t>(ld) * 2u),
+             lds_addr(tile + kbase * ROW_BYTES));
+    } else {
+      const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
+      glds16(src, lds_addr(tile + kbase * ROW_BYTES));
+    }
+  }
+}
+
 template <int N>
 PZ_DEV void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");

@@ -528,11 +528,25 @@ PZ_DEV void epilogue_lds(const GemmArgs& p, Acc& acc, PZ_LDS char* smem, int m0,
         for (int r = 0; r < 4; ++r) part[wm * BN + nl0 + L::n_off(j) + r] = cs[j][r];
     }
     __syncthreads();
-    for (int c = tid; c < BN; c += NT) {  // fire-and-forget: nothing waits for them in this kernel
-      float s = 0.f;
+    if (p.cs_ws != nullptr) {  // deterministic: this tile's partial row, then the ordered folds
+      const int tiles_m = (p.M + BM - 1) / BM, tm = m0 / BM;
+      const int cols = min(BN, p.N - n0);
+      for (int c = tid; c < cols; c += NT) {
+        float s = 0.f;
 #pragma unroll
-      for (int w = 0; w < WM; ++w) s += part[w * BN + c];
-      if (n0 + c < p.N) atomicAdd(p.colsum + n0 + c, s);
+        for (int w = 0; w < WM; ++w) s += part[w * BN + c];
+        st_wt(p.cs_ws + static_cast<int64_t>(tm) * p.N + n0 + c, s);
+      }
+      constexpr int kGroup = 64;
+      det_colsum<NT>(p.cs_ws + n0, p.cs_tickets + (n0 / BN) * ((tiles_m + kGroup - 1) / kGroup + 1), tiles_m, kGroup, tm,
+                     cols, p.N, p.colsum + n0, reinterpret_cast<PZ_LDS int*>(smem + WM * BN * 4));
+    } else {
+      for (int c = tid; c < BN; c += NT) {  // fire-and-forget: nothing waits for them in this kernel
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < WM; ++w) s += part[w * BN + c];
+        if (n0 + c < p.N) atomicAdd(p.colsum + n0 + c, s);
+      }
     }
   }
 }

@@ -90,68 +90,6 @@ struct Cfg {
 };
 
 
-// K-contiguous operand rows [row0, row0+R) x k [k0, k0+BK) -> slot [R][BK]; NW waves share it
-// FULL (buffer path, dispatcher-guaranteed full row tiles): no row clamp, so the piece's row
-// offset is wave-uniform and rides in soffset — one (BK 32) or two (BK 64: the swizzle flips
-// with the piece's parity) per-lane offsets stay live instead of one per piece (the 16 of a
-// BK 64 K-contiguous pair of operands spilled to scratch inside the loop)
-template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0, bool FULL = false>
-PZ_DEV void stage_kc(const uint16_t* __restrict__ g, int64_t ld, int row0, int rows_valid, int k0,
-                     PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
-  constexpr int CPR = BK / 8;             // 16-B chunks per row
-  constexpr int RPI = 64 / CPR;           // rows per 1-KiB instruction
-  constexpr int INSTR = R / (RPI * NW);
-  static_assert(INSTR >= 1 && INSTR * RPI * NW == R, "K-contiguous stage split");
-#pragma unroll
-  for (int i = 0; i < INSTR; ++i) {
-    const int rbase = (wave * INSTR + i) * RPI;
-    const int r = rbase + lane / CPR;
-    const int chunk = (lane % CPR) ^ swz_kc<BK>(r);
-    if constexpr (BUF && FULL) {
-      const uint32_t voff = (static_cast<uint32_t>(lane / CPR) * static_cast<uint32_t>(ld) + chunk * 8) * 2u;
-      const uint32_t soff = (static_cast<uint32_t>(row0 + rbase) * static_cast<uint32_t>(ld) + static_cast<uint32_t>(k0)) * 2u;
-      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(soff), lds_addr(tile + rbase * BK * 2));
-      continue;
-    }
-    int gr = row0 + r;
-    gr = gr < rows_valid ? gr : rows_valid - 1;
-    if constexpr (BUF) {
-      const uint32_t voff = (static_cast<uint32_t>(gr) * static_cast<uint32_t>(ld) + chunk * 8) * 2u;
-      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * 2u), lds_addr(tile + rbase * BK * 2));
-    } else {
-      const uint16_t* src = g + static_cast<int64_t>(gr) * ld + k0 + chunk * 8;
-      glds16(src, lds_addr(tile + rbase * BK * 2));
-    }
-  }
-}
-
-// M/N-contiguous operand: k rows [k0, k0+BK) x cols [col0, col0+R) -> slot [BK][R]
-template <int R, int NW, int BK = 32, bool BUF = false, int POL = 0>
-PZ_DEV void stage_mn(const uint16_t* __restrict__ g, int64_t ld, int col0, int cols_valid, int k0,
-                     PZ_LDS char* tile, int wave, int lane, i32x4_t rs = {}) {
-  constexpr int ROW_BYTES = R * 2;
-  constexpr int CHUNKS = R / 8;
-  constexpr int ROWS_PER = 1024 / ROW_BYTES;
-  constexpr int INSTR = (BK * ROW_BYTES) / (1024 * NW);
-  static_assert(INSTR >= 1 && INSTR * 1024 * NW == BK * ROW_BYTES, "M/N-contiguous stage split");
-#pragma unroll
-  for (int i = 0; i < INSTR; ++i) {
-    const int kbase = (wave * INSTR + i) * ROWS_PER;
-    const int kr = kbase + lane / CHUNKS;
-    const int chunk = (lane % CHUNKS) ^ swz_mn(kr);
-    int gc = col0 + chunk * 8;
-    gc = gc < cols_valid ? gc : cols_valid - 8;
-    if constexpr (BUF) {
-      const uint32_t voff = (static_cast<uint32_t>(kr) * static_cast<uint32_t>(ld) + gc) * 2u;
-      blds16<POL>(rs, voff, __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(k0) * static_cast<uint32_t>(ld) * 2u),
-             lds_addr(tile + kbase * ROW_BYTES));
-    } else {
-      const uint16_t* src = g + static_cast<int64_t>(k0 + kr) * ld + gc;
-      glds16(src, lds_addr(tile + kbase * ROW_BYTES));
-    }
-  }
-}
-
 template <int RB, int NW, int KROWS>
 PZ_DEV void stage_mn8(int64_t ld16, int col0, int k0, PZ_LDS char* tile, int wave, int lane, i32x4_t rs) {
   constexpr int CHUNKS = RB / 16;
@@ -686,8 +624,22 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
     }
     __syncthreads();
     if (*flag == 0) return;  // block-uniform: another slice finishes this tile
-    for (int sl = 0; sl < split; ++sl) {
-      if (sl == slice) continue;
+    // the sum order must not depend on which slice arrived last (deterministic results): two
+    // slices = own + other (addition commutes); more = every slab in slice order, own included
+    if (split > 2) {
+      static_for<CH>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        const f32x4_t v = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (c * C::NT + tid) * 16, 0, kSc1));
+        if constexpr (ACC32) {
+          constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
+          acc[i][j][q] = v[0]; acc[i][j][q + 1] = v[1]; acc[i][j][q + 2] = v[2]; acc[i][j][q + 3] = v[3];
+        } else {
+          acc[c / C::TN][c % C::TN] = v;
+        }
+      });
+    }
+    for (int sl = split > 2 ? 1 : 0; sl < split; ++sl) {
+      if (split <= 2 && sl == slice) continue;
       static_for<CH>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
         add_chunk(cc, __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(

@@ -46,22 +46,28 @@ namespace {
 #include "gemm_epilogue.h"
 
 constexpr int kSkB = 256;                    // macro tile BM = BN
-constexpr int kSkNT = 256;                   // four waves
-constexpr int kSkBK = 32;                    // K depth of a ring slot
-constexpr int kSkOp = kSkB * kSkBK * 2;      // one operand's slot image: 16 KiB
-constexpr int kSkSlot = 2 * kSkOp;           // A then B: 32 KiB
-constexpr int kSkPieces = kSkOp / 1024 / 4;  // LDS-DMA instructions per wave, operand and step (4)
-constexpr int kSkG = 2 * kSkPieces;          // per wave and step (8)
-constexpr int kSkNS = 4;                     // ring slots (128 KiB = the epilogue's C image)
 constexpr int kSkSlab = kSkB * kSkB;         // fp32 floats of one partial tile
 constexpr int kSkF32 = 100;                  // epilogue code of the fp32-output store path
 constexpr int kSkMaxCon = 8;                 // contributors per stream-K tile (sk_plan bounds it)
+constexpr int kSkLds = 128 * 1024;           // both main loops' rings = the epilogue's C image
+
+// Main-loop geometry per wave count. W = 8 (the default): two waves per SIMD, 128x64 wave tiles,
+// the ping-pong over a 2-slot 64-deep ring of the tiled kernels (gemm_mfma.hip VAR 30). W = 4
+// (engine 3, lab): one wave per SIMD, 128x128 wave tiles, a 4-slot 32-deep ring.
+template <int W> struct SkGeo {
+  static constexpr int NT = W * 64;
+  static constexpr int WN = W / 2;           // wave grid 2 x WN
+  static constexpr int TN = 16 / WN;         // 16x16 accumulator tiles across a wave tile
+  static constexpr int WTN = kSkB / WN;
+  static constexpr int BK = W == 8 ? 64 : 32;  // K depth of one schedule step
+  static constexpr int CH = 8 * TN;          // f32x4 accumulator chunks per lane
+};
 
 struct SkSched {
   int nprob;
   int tiles0;           // tiles of problem 0 (problem 1's tiles follow)
   int tiles;            // all tiles
-  int iters;            // 32-deep K steps per tile
+  int iters;            // K steps per tile
   int grid;             // workgroups
   int sk_tiles;         // tiles [0, sk_tiles) are stream-K'd over every workgroup
   long long sk_iters;   // sk_tiles * iters
@@ -85,11 +91,102 @@ PZ_DEV int sk_owner(const SkSched& s, long long it) {
   return w;
 }
 
+PZ_DEV void sk_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// ------------------------------------------------------------------ W = 8: the ping-pong loop
+// Waves 0-3 (group 0) and 4-7 (group 1) share the four SIMDs and run one barrier interval apart:
+// while one wave of a SIMD issues its 64-MFMA block (setprio 1), its partner issues the next
+// step's LDS-DMA and fragment reads into the gaps (hazard argument: gemm_mfma.hip gemm_body, BK 64
+// branch). Group 0 stages step t+1 in its read interval of step t; every wave waits for it
+// (vmcnt(0)) before the barrier that opens the next read interval.
+template <bool A_KC, bool B_KC>
+PZ_DEV void pp_mainloop(f32x4_t (&acc)[8][4], PZ_LDS char* smem, const GemmArgs& p, i32x4_t rs_a, i32x4_t rs_b,
+                        int m0, int n0, int kt0, int nk, int wave, int lane) {
+  constexpr int BK = 64, A_BYTES = kSkB * BK * 2, SLOT = 2 * A_BYTES;
+  const int grp = wave >> 2, tw = wave & 3;
+  const int wm = wave >> 2, wn = wave & 3;
+  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
+  const uint16_t* __restrict__ B = static_cast<const uint16_t*>(p.B);
+  auto stage = [&](int kt, auto team, int tw_) __attribute__((always_inline)) {
+    constexpr int TEAM = decltype(team)::value;
+    PZ_LDS char* base = smem + (kt & 1) * SLOT;
+    const int k0 = (kt0 + kt) * BK;
+    if constexpr (A_KC) stage_kc<kSkB, TEAM, BK, true, 0, true>(A, p.lda, m0, p.M, k0, base, tw_, lane, rs_a);
+    else stage_mn<kSkB, TEAM, BK, true, 0>(A, p.lda, m0, p.M, k0, base, tw_, lane, rs_a);
+    if constexpr (B_KC) stage_kc<kSkB, TEAM, BK, true, 0, true>(B, p.ldb, n0, p.N, k0, base + A_BYTES, tw_, lane, rs_b);
+    else stage_mn<kSkB, TEAM, BK, true, 0>(B, p.ldb, n0, p.N, k0, base + A_BYTES, tw_, lane, rs_b);
+  };
+  struct Frags { i16x8_t a[2][8]; i16x8_t b[2][4]; };
+  auto read = [&](int slot, Frags& f) __attribute__((always_inline)) {
+    const PZ_LDS char* ta = smem + slot * SLOT;
+    const PZ_LDS char* tb = ta + A_BYTES;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (B_KC) f.b[kb][j] = frag_kc<BK>(tb, wn * 64 + j * 16 + (lane & 15), (lane >> 4) + 4 * kb);
+        else f.b[kb][j] = frag_mn<kSkB>(tb, wn * 64 + j * 16, 8 * (lane >> 4) + 32 * kb, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (A_KC) f.a[kb][i] = frag_kc<BK>(ta, wm * 128 + i * 16 + (lane & 15), (lane >> 4) + 4 * kb);
+        else f.a[kb][i] = frag_mn<kSkB>(ta, wm * 128 + i * 16, 8 * (lane >> 4) + 32 * kb, lane);
+      }
+    }
+  };
+  using T4 = std::integral_constant<int, 4>;
+  using T8 = std::integral_constant<int, 8>;
+  // the previous unit's epilogue stores share the VM counter with the DMAs; and every wave is done
+  // with the LDS image before slot 0 is refilled
+  wait_vm<0>();
+  sk_barrier();
+  stage(0, T8{}, wave);
+  wait_vm<0>();
+  sk_barrier();
+  if (grp == 1) sk_barrier();
+  for (int t = 0; t < nk; ++t) {
+    if (grp == 0 && t + 1 < nk) stage(t + 1, T4{}, tw);
+    Frags f;
+    read(t & 1, f);
+    if (grp == 1) wait_vm<0>();  // step t+1 (issued by group 0 one interval ago) landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    sk_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, f.b[kb][j]),
+                                                              __builtin_bit_cast(bf16x8_t, f.a[kb][i]), acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (grp == 0) wait_vm<0>();
+    sk_barrier();
+  }
+  if (grp == 0) sk_barrier();
+}
+
+// ------------------------------------------------------------------ W = 4: the lab loop
+// 256x256 macro tile on FOUR waves (128x128 wave tiles = the whole AGPR file): 0.25 LDS reads per
+// MFMA. LDS ring of 4 32-deep slots filled by buffer-addressed LDS-DMA; fragments read one step
+// ahead into a second VGPR set; MFMAs, fragment reads and refill DMAs interleaved in 16 groups per
+// step. Correct and deterministic, but measured 0.70-0.75x the ping-pong on the step's shapes
+// (profiles/r5_gemm_bench_vs_hipblaslt.txt): one wave per SIMD has no partner to run while it
+// waits at the per-step barrier (SQ_WAIT_ANY 0.30-0.40 of its cycles, profiles/r5_pmc_sk.txt).
+constexpr int kSkW4BK = 32, kSkW4Op = kSkB * kSkW4BK * 2, kSkW4Slot = 2 * kSkW4Op, kSkW4NS = 4;
+constexpr int kSkW4Pieces = kSkW4Op / 1024 / 4;  // LDS-DMA instructions per wave, operand and step
+constexpr int kSkW4G = 2 * kSkW4Pieces;
+
 // One operand's LDS-DMA addressing for a unit. K-contiguous ([rows][K]): piece i of this wave =
 // 16 rows x 64 B; M/N-contiguous ([K][rows]): piece i = 2 k-rows x 512 B. The per-lane offsets
-// carry the read-side swizzle (rule 21: linear LDS destination, permuted source).
+// carry the read-side swizzle (linear LDS destination, permuted source).
 struct SkOperand {
-  i32x4_t rs;          // raw buffer resource of the operand
+  i32x4_t rs;
   uint32_t voff[2];    // per-lane byte offsets (M/N-contiguous: by piece parity)
   uint32_t base;       // wave-uniform byte offset of this wave's piece 0 at the unit's first step
   uint32_t pstep;      // bytes between the wave's consecutive pieces
@@ -97,32 +194,31 @@ struct SkOperand {
 };
 
 template <bool KC>
-PZ_DEV SkOperand sk_operand(const void* g, int64_t ld, int row0, int kb, int wave, int lane) {
+PZ_DEV SkOperand sk_operand(i32x4_t rs, int64_t ld, int row0, int kb, int wave, int lane) {
   SkOperand o;
-  o.rs = buf_rsrc(g);
+  o.rs = rs;
   const uint32_t l = static_cast<uint32_t>(ld);
   if constexpr (KC) {
-    const int r = lane >> 2;  // row within the piece (16 rows x 4 chunks)
+    const int r = lane >> 2;
     const int chunk = (lane & 3) ^ swz_kc<32>(r);
     o.voff[0] = o.voff[1] = (static_cast<uint32_t>(r) * l + static_cast<uint32_t>(chunk) * 8u) * 2u;
-    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(row0 + wave * 4 * 16) * l + static_cast<uint32_t>(kb) * kSkBK) * 2u);
+    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(row0 + wave * 4 * 16) * l + static_cast<uint32_t>(kb) * kSkW4BK) * 2u);
     o.pstep = __builtin_amdgcn_readfirstlane(16u * l * 2u);
-    o.kstep = kSkBK * 2;
+    o.kstep = kSkW4BK * 2;
   } else {
 #pragma unroll
     for (int par = 0; par < 2; ++par) {
-      const int kr = wave * 8 + 2 * par + (lane >> 5);  // k-row in the slot (its swizzle only)
+      const int kr = wave * 8 + 2 * par + (lane >> 5);
       const int chunk = (lane & 31) ^ swz_mn(kr);
       o.voff[par] = (static_cast<uint32_t>(lane >> 5) * l + static_cast<uint32_t>(chunk) * 8u) * 2u;
     }
-    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(kb * kSkBK + wave * 8) * l + static_cast<uint32_t>(row0)) * 2u);
+    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(kb * kSkW4BK + wave * 8) * l + static_cast<uint32_t>(row0)) * 2u);
     o.pstep = __builtin_amdgcn_readfirstlane(2u * l * 2u);
-    o.kstep = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(kSkBK) * l * 2u);
+    o.kstep = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(kSkW4BK) * l * 2u);
   }
   return o;
 }
 
-// piece i of K step ks (relative to the unit) into the wave's LDS range `lds` (+ i KiB)
 template <bool KC>
 PZ_DEV void sk_dma(const SkOperand& o, int i, int ks, uint32_t lds) {
   const uint32_t voff = KC ? o.voff[0] : o.voff[i & 1];
@@ -130,10 +226,9 @@ PZ_DEV void sk_dma(const SkOperand& o, int i, int ks, uint32_t lds) {
             lds + static_cast<uint32_t>(i) * 1024u);
 }
 
-// fragment f (16 rows / columns x 32 k) of the wave's 128-row / -column half `wg` of a slot image
 template <bool KC>
 PZ_DEV i16x8_t sk_frag(const PZ_LDS char* img, int wg, int f, int lane, uint32_t kc_lane) {
-  if constexpr (KC) return *reinterpret_cast<const PZ_LDS i16x8_t*>(img + (wg * 128 + f * 16) * (kSkBK * 2) + kc_lane);
+  if constexpr (KC) return *reinterpret_cast<const PZ_LDS i16x8_t*>(img + (wg * 128 + f * 16) * (kSkW4BK * 2) + kc_lane);
   else return frag_mn<kSkB>(img, wg * 128 + f * 16, 8 * (lane >> 4), lane);
 }
 
@@ -142,40 +237,36 @@ struct SkFrag {
   i16x8_t b[8];
 };
 
-PZ_DEV void sk_barrier() {
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-}
-
-// The main loop of one unit: n 32-deep K steps into acc (zeroed by the caller).
-template <bool A_KC, bool B_KC, int NS>
-PZ_DEV void sk_mainloop(f32x4_t (&acc)[8][8], PZ_LDS char* smem, const SkOperand& oa, const SkOperand& ob, int n,
-                        int wave, int wm, int wn, int lane) {
+template <bool A_KC, bool B_KC>
+PZ_DEV void w4_mainloop(f32x4_t (&acc)[8][8], PZ_LDS char* smem, const GemmArgs& p, i32x4_t rs_a, i32x4_t rs_b,
+                        int m0, int n0, int kt0, int n, int wave, int lane) {
+  constexpr int NS = kSkW4NS;
+  const int wm = wave >> 1, wn = wave & 1;
+  const SkOperand oa = sk_operand<A_KC>(rs_a, p.lda, m0, kt0, wave, lane);
+  const SkOperand ob = sk_operand<B_KC>(rs_b, p.ldb, n0, kt0, wave, lane);
   const uint32_t lds0 = lds_addr(smem);
-  const uint32_t wpiece = static_cast<uint32_t>(wave) * kSkPieces * 1024u;
-  const uint32_t kc_lane = static_cast<uint32_t>((lane & 15) * (kSkBK * 2) + (((lane >> 4) ^ swz_kc<32>(lane & 15)) << 4));
+  const uint32_t wpiece = static_cast<uint32_t>(wave) * kSkW4Pieces * 1024u;
+  const uint32_t kc_lane = static_cast<uint32_t>((lane & 15) * (kSkW4BK * 2) + (((lane >> 4) ^ swz_kc<32>(lane & 15)) << 4));
   auto dma_step = [&](int ks) __attribute__((always_inline)) {
-    const uint32_t sb = lds0 + static_cast<uint32_t>(ks % NS) * kSkSlot + wpiece;
+    const uint32_t sb = lds0 + static_cast<uint32_t>(ks % NS) * kSkW4Slot + wpiece;
 #pragma unroll
-    for (int i = 0; i < kSkPieces; ++i) sk_dma<A_KC>(oa, i, ks, sb);
+    for (int i = 0; i < kSkW4Pieces; ++i) sk_dma<A_KC>(oa, i, ks, sb);
 #pragma unroll
-    for (int i = 0; i < kSkPieces; ++i) sk_dma<B_KC>(ob, i, ks, sb + kSkOp);
+    for (int i = 0; i < kSkW4Pieces; ++i) sk_dma<B_KC>(ob, i, ks, sb + kSkW4Op);
   };
   auto read_all = [&](SkFrag& f, int ks) __attribute__((always_inline)) {
-    const PZ_LDS char* img = smem + (ks % NS) * kSkSlot;
+    const PZ_LDS char* img = smem + (ks % NS) * kSkW4Slot;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f.b[j] = sk_frag<B_KC>(img + kSkOp, wn, j, lane, kc_lane);
+    for (int j = 0; j < 8; ++j) f.b[j] = sk_frag<B_KC>(img + kSkW4Op, wn, j, lane, kc_lane);
 #pragma unroll
     for (int i = 0; i < 8; ++i) f.a[i] = sk_frag<A_KC>(img, wm, i, lane, kc_lane);
   };
   // step h: 64 MFMAs on `cur`; rd: read step h+1 into `nxt`; dm: refill slot h % NS with step
-  // h+NS. ONE body with scalar guards: three specialised bodies made hipcc keep every fragment
-  // set live across all of them (spills)
+  // h+NS. ONE body with scalar guards (three specialised bodies kept every fragment set live)
   auto step = [&](const SkFrag& cur, SkFrag& nxt, int h) __attribute__((always_inline)) {
     const bool rd = h + 1 < n, dm = h + NS < n;
-    const PZ_LDS char* img = smem + ((h + 1) % NS) * kSkSlot;
-    const uint32_t sb = lds0 + static_cast<uint32_t>(h % NS) * kSkSlot + wpiece;
+    const PZ_LDS char* img = smem + ((h + 1) % NS) * kSkW4Slot;
+    const uint32_t sb = lds0 + static_cast<uint32_t>(h % NS) * kSkW4Slot + wpiece;
     __builtin_amdgcn_sched_barrier(0);
     static_for<16>([&](auto gc) {
       constexpr int g = decltype(gc)::value;
@@ -185,32 +276,29 @@ PZ_DEV void sk_mainloop(f32x4_t (&acc)[8][8], PZ_LDS char* smem, const SkOperand
                                                             __builtin_bit_cast(bf16x8_t, cur.a[i]), acc[i][j], 0, 0, 0);
       });
       if (rd) {
-        if constexpr (g < 8) nxt.b[g] = sk_frag<B_KC>(img + kSkOp, wn, g, lane, kc_lane);
+        if constexpr (g < 8) nxt.b[g] = sk_frag<B_KC>(img + kSkW4Op, wn, g, lane, kc_lane);
         else nxt.a[g - 8] = sk_frag<A_KC>(img, wm, g - 8, lane, kc_lane);
       }
       if constexpr ((g & 1) == 0) {
         constexpr int pc = g / 2;
         if (dm) {
-          if constexpr (pc < kSkPieces) sk_dma<A_KC>(oa, pc, h + NS, sb);
-          else sk_dma<B_KC>(ob, pc - kSkPieces, h + NS, sb + kSkOp);
+          if constexpr (pc < kSkW4Pieces) sk_dma<A_KC>(oa, pc, h + NS, sb);
+          else sk_dma<B_KC>(ob, pc - kSkW4Pieces, h + NS, sb + kSkW4Op);
         }
       }
       __builtin_amdgcn_sched_barrier(0);
     });
     if (h + 2 < n) {  // step h+2 landed for every wave; every read of slot (h+1) % NS retired
-      wait_newer<kSkG, NS - 2>(min(h + NS, n - 1) - (h + 2));
+      wait_newer<kSkW4G, NS - 2>(min(h + NS, n - 1) - (h + 2));
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       sk_barrier();
     }
   };
-
-  // the previous unit's epilogue stores share the VM counter with the DMAs counted below: retire
-  // them first; and every wave is done with the LDS
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  wait_vm<0>();
   sk_barrier();
   const int pre = min(NS, n);
   for (int s = 0; s < pre; ++s) dma_step(s);
-  wait_newer<kSkG, NS - 2>(max(pre - 2, 0));  // steps 0 and 1 landed
+  wait_newer<kSkW4G, NS - 2>(max(pre - 2, 0));  // steps 0 and 1 landed
   sk_barrier();
   SkFrag f0, f1;
   read_all(f0, 0);
@@ -222,15 +310,16 @@ PZ_DEV void sk_mainloop(f32x4_t (&acc)[8][8], PZ_LDS char* smem, const SkOperand
   }
 }
 
-// fp32-output epilogue (weight gradients): alpha, bias, accumulate, column sums; 16-B stores
-PZ_DEV void sk_store_f32(const GemmArgs& p, f32x4_t (&acc)[8][8], int m0, int n0, int wm, int wn, int lane) {
+// fp32-output epilogue (weight gradients): alpha, bias, accumulate; 16-B stores
+template <int W>
+PZ_DEV void sk_store_f32(const GemmArgs& p, f32x4_t (&acc)[8][SkGeo<W>::TN], int m0, int n0, int wm, int wn, int lane) {
+  using G = SkGeo<W>;
   float* __restrict__ Cp = static_cast<float*>(p.C);
   const int g4 = 4 * (lane >> 4);
-  static_for<8>([&](auto jc) {
+  static_for<G::TN>([&](auto jc) {
     constexpr int j = decltype(jc)::value;
-    const int n = n0 + wn * 128 + j * 16 + g4;
+    const int n = n0 + wn * G::WTN + j * 16 + g4;
     const f32x4_t bias4 = p.bias != nullptr ? *reinterpret_cast<const f32x4_t*>(p.bias + n) : f32x4_t{0.f, 0.f, 0.f, 0.f};
-    f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
     static_for<8>([&](auto ic) {
       constexpr int i = decltype(ic)::value;
       const int m = m0 + wm * 128 + i * 16 + (lane & 15);
@@ -238,21 +327,15 @@ PZ_DEV void sk_store_f32(const GemmArgs& p, f32x4_t (&acc)[8][8], int m0, int n0
       f32x4_t* dst = reinterpret_cast<f32x4_t*>(Cp + static_cast<int64_t>(m) * p.ldc + n);
       if (p.accumulate) v += *dst;
       *dst = v;
-      cs += v;
     });
-    if (p.colsum != nullptr) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float s = group_sum<16>(cs[r]);
-        if ((lane & 15) == 0) atomicAdd(p.colsum + n + r, s);
-      }
-    }
   });
 }
 
-template <bool A_KC, bool B_KC, typename OutT, int EK, int NS>
-__global__ void __launch_bounds__(kSkNT) __attribute__((amdgpu_waves_per_eu(1, 1)))
+template <bool A_KC, bool B_KC, typename OutT, int EK, int W>
+__global__ void __launch_bounds__(SkGeo<W>::NT) __attribute__((amdgpu_waves_per_eu(W / 4, W / 4)))
 gemm_sk_kernel(const SkArgs g) {
+  using G = SkGeo<W>;
+  constexpr int NT = G::NT, CH = G::CH;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
   const SkSched& s = g.s;
@@ -260,7 +343,7 @@ gemm_sk_kernel(const SkArgs g) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
   const int tid = threadIdx.x;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / G::WN, wn = wave % G::WN;
 
   // Work units in schedule order: the stream-K range [s0, s1) cut at tile boundaries, then the
   // data-parallel tiles w, w + grid, ... ONE loop, so the unit body is inlined once.
@@ -298,24 +381,24 @@ gemm_sk_kernel(const SkArgs g) {
     int tm, tn, tile_, slice_;
     tile_coords(tl, p.M / kSkB, p.N / kSkB, 1, tm, tn, tile_, slice_);
     const int m0 = tm * kSkB, n0 = tn * kSkB;
-    const SkOperand oa = sk_operand<A_KC>(p.A, p.lda, m0, kb, wave, lane);
-    const SkOperand ob = sk_operand<B_KC>(p.B, p.ldb, n0, kb, wave, lane);
-    f32x4_t acc[8][8];
+    f32x4_t acc[8][G::TN];
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    sk_mainloop<A_KC, B_KC, NS>(acc, smem, oa, ob, ke - kb, wave, wm, wn, lane);
+      for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    if constexpr (W == 8) pp_mainloop<A_KC, B_KC>(acc, smem, p, buf_rsrc(p.A), buf_rsrc(p.B), m0, n0, kb, ke - kb, wave, lane);
+    else w4_mainloop<A_KC, B_KC>(acc, smem, p, buf_rsrc(p.A), buf_rsrc(p.B), m0, n0, kb, ke - kb, wave, lane);
 
     if (slab >= 0) {
-      // ---- stream-K hand-off (write-through slabs, one ticket per contributor)
+      // ---- stream-K hand-off (write-through slabs, one ticket per contributor: MI355X_MICROARCH
+      // hand-off table, row 1)
       constexpr int kSc1 = 16;
       const auto rs_own = __builtin_amdgcn_make_buffer_rsrc(g.ws + static_cast<int64_t>(slab) * kSkSlab, 0, kSkSlab * 4,
                                                             0x00020000);
-      static_for<64>([&](auto cc) {
+      static_for<CH>([&](auto cc) {
         constexpr int c = decltype(cc)::value;
-        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[c / 8][c % 8]), rs_own,
-                                               tid * 16, c * kSkNT * 16, kSc1);
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4_t, acc[c / G::TN][c % G::TN]), rs_own,
+                                               tid * 16, c * NT * 16, kSc1);
       });
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -336,20 +419,19 @@ gemm_sk_kernel(const SkArgs g) {
         return __builtin_amdgcn_make_buffer_rsrc(g.ws + static_cast<int64_t>(slab_of(c)) * kSkSlab, 0, kSkSlab * 4,
                                                  0x00020000);
       };
-#ifndef PZ_SK_NOFOLD
       // in groups of 16 chunks (64 VGPRs of loads in flight): an unbounded unrolled fold let
-      // hipcc hoist all 64 loads (256 VGPRs) and spill
+      // hipcc hoist every load and spill
       auto fold = [&](const auto& rs, bool first) __attribute__((always_inline)) {
-        static_for<4>([&](auto qc) {
+        static_for<CH / 16>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
           f32x4_t ld[16];
           static_for<16>([&](auto cc) {
             constexpr int c = 16 * q + decltype(cc)::value;
-            ld[c - 16 * q] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, c * kSkNT * 16, kSc1));
+            ld[c - 16 * q] = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, c * NT * 16, kSc1));
           });
           static_for<16>([&](auto cc) {
             constexpr int c = 16 * q + decltype(cc)::value;
-            acc[c / 8][c % 8] = first ? ld[c - 16 * q] : acc[c / 8][c % 8] + ld[c - 16 * q];
+            acc[c / G::TN][c % G::TN] = first ? ld[c - 16 * q] : acc[c / G::TN][c % G::TN] + ld[c - 16 * q];
           });
           __builtin_amdgcn_sched_barrier(0);
         });
@@ -358,32 +440,20 @@ gemm_sk_kernel(const SkArgs g) {
         fold(rs_of(w == wlo ? whi : wlo), false);
       } else {  // fold every slab (own included, it was stored above) in K order
         // (unrolled over at most kSkMaxCon contributors, sk_plan's bound: a runtime loop carried
-        // the 256 accumulators through a loop phi that hipcc could only keep in VGPRs)
+        // the accumulators through a loop phi that hipcc could only keep in VGPRs)
         fold(rs_of(wlo), true);
         static_for<kSkMaxCon - 1>([&](auto kc) {
           constexpr int k = decltype(kc)::value + 1;
           if (wlo + k <= whi) fold(rs_of(wlo + k), false);
         });
       }
-#endif
     }
 
     // ---- epilogue
-#ifdef PZ_SK_NOEPI
-    if constexpr (true) {
-      uint16_t* C = static_cast<uint16_t*>(p.C);
-      static_for<64>([&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        const int m = m0 + wm * 128 + (c / 8) * 16 + (lane & 15), n = n0 + wn * 128 + (c % 8) * 16 + 4 * (lane >> 4);
-        float v[4] = {acc[c / 8][c % 8][0], acc[c / 8][c % 8][1], acc[c / 8][c % 8][2], acc[c / 8][c % 8][3]};
-        store4<uint16_t>(C + static_cast<int64_t>(m) * p.ldc + n, v);
-      });
-    } else
-#endif
     if constexpr (EK == kSkF32) {
-      sk_store_f32(p, acc, m0, n0, wm, wn, lane);
+      sk_store_f32<W>(p, acc, m0, n0, wm, wn, lane);
     } else {
-      epilogue_lds<kSkB, kSkB, 2, 2, Lay16<8, 8>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
+      epilogue_lds<kSkB, kSkB, 2, G::WN, Lay16<8, G::TN>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
     }
   }
 }
@@ -401,7 +471,7 @@ int device_cus() {
 // which epilogue covers these arguments (-1: none on this engine)
 int sk_epi_kind(const GemmArgs& p) {
   if (p.out_dtype == DT_F32) {
-    if (p.epi_mode != EPI_STORE || p.mask != nullptr || p.out8 != nullptr) return -1;
+    if (p.epi_mode != EPI_STORE || p.mask != nullptr || p.out8 != nullptr || p.colsum != nullptr) return -1;
     return kSkF32;
   }
   if (p.out_dtype != DT_BF16 || p.accumulate) return -1;
@@ -431,20 +501,27 @@ int sk_epi_kind(const GemmArgs& p) {
   return -1;
 }
 
+// wave count of the engine a GEMM runs on: 8 (ping-pong) unless engine 3 asks for the 4-wave lab
+int sk_waves(const GemmArgs& p) { return p.engine == 3 ? 4 : 8; }
+
 SkSched sk_plan(const GemmArgs* probs, int n) {
   SkSched s{};
   s.nprob = n;
   s.tiles0 = (probs[0].M / kSkB) * (probs[0].N / kSkB);
   s.tiles = s.tiles0 + (n > 1 ? (probs[1].M / kSkB) * (probs[1].N / kSkB) : 0);
-  s.iters = probs[0].K / kSkBK;
+  const int bk = sk_waves(probs[0]) == 8 ? SkGeo<8>::BK : SkGeo<4>::BK;
+  s.iters = probs[0].K / bk;
   const int cus = device_cus();
   int grid = probs[0].cus > 0 ? std::min(probs[0].cus, cus) : cus;
   const int T = s.tiles;
+  // fewer tiles than workgroups: at most kSkMaxCon contributors per tile (the fold's unroll)
+  if (T < grid) grid = std::min(grid, T * (kSkMaxCon - 1));
   int sk = 0;
   if (T % grid != 0) sk = T < grid ? T : T % grid + grid;
-  // a stream-K share under 8 steps per workgroup: fewer workgroups (each takes >= 8 steps)
-  if (sk > 0 && static_cast<long long>(sk) * s.iters < 8LL * grid) {
-    grid = std::max(1, static_cast<int>(static_cast<long long>(sk) * s.iters / 8));
+  // a stream-K share under 256 K per workgroup: fewer workgroups (each takes at least that)
+  const long long min_steps = 256 / bk;
+  if (sk > 0 && static_cast<long long>(sk) * s.iters < min_steps * grid) {
+    grid = std::max(1, static_cast<int>(static_cast<long long>(sk) * s.iters / min_steps));
     sk = (T % grid == 0) ? 0 : (T < grid ? T : T % grid + grid);
   }
   s.grid = grid;
@@ -453,55 +530,54 @@ SkSched sk_plan(const GemmArgs* probs, int n) {
   return s;
 }
 
-template <bool AKC, bool BKC, typename OutT, int EK>
+template <bool AKC, bool BKC, typename OutT, int EK, int W>
 hipError_t sk_launch(const SkArgs& a, hipStream_t st) {
-  constexpr int lds = kSkNS * kSkSlot;
-  auto kern = gemm_sk_kernel<AKC, BKC, OutT, EK, kSkNS>;
+  auto kern = gemm_sk_kernel<AKC, BKC, OutT, EK, W>;
   static bool attr_set = false;
   if (!attr_set) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize, kSkLds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3(a.s.grid), dim3(kSkNT), lds, st, a);
+  hipLaunchKernelGGL(kern, dim3(a.s.grid), dim3(SkGeo<W>::NT), kSkLds, st, a);
   return hipGetLastError();
 }
 
 hipError_t sk_dispatch(const SkArgs& a, int ek, hipStream_t st) {
   const GemmArgs& p = a.p[0];
-#ifdef PZ_SK_ONE  // register / ISA experiments: one instantiation
-  (void)p;
-  (void)ek;
-  return sk_launch<PZ_SK_ONE>(a, st);
-#else
+  if (sk_waves(p) == 4) {  // lab engine: plain stores only
+    if (ek != EK_STORE) return hipErrorInvalidValue;
+    if (p.a_kc && !p.b_kc) return sk_launch<true, false, uint16_t, EK_STORE, 4>(a, st);
+    if (p.a_kc && p.b_kc) return sk_launch<true, true, uint16_t, EK_STORE, 4>(a, st);
+    return sk_launch<false, false, uint16_t, EK_STORE, 4>(a, st);
+  }
   if (p.a_kc && !p.b_kc) {  // forward X · W[in, out]
     switch (ek) {
-      case EK_STORE: return sk_launch<true, false, uint16_t, EK_STORE>(a, st);
-      case EK_RELU: return sk_launch<true, false, uint16_t, EK_RELU>(a, st);
-      case EK_F_RELU_POST: return sk_launch<true, false, uint16_t, EK_F_RELU_POST>(a, st);
-      case EK_F_RELU_PREPOST: return sk_launch<true, false, uint16_t, EK_F_RELU_PREPOST>(a, st);
-      case EK_F_PRE: return sk_launch<true, false, uint16_t, EK_F_PRE>(a, st);
-      case EK_ANY: return sk_launch<true, false, uint16_t, EK_ANY>(a, st);
+      case EK_STORE: return sk_launch<true, false, uint16_t, EK_STORE, 8>(a, st);
+      case EK_RELU: return sk_launch<true, false, uint16_t, EK_RELU, 8>(a, st);
+      case EK_F_RELU_POST: return sk_launch<true, false, uint16_t, EK_F_RELU_POST, 8>(a, st);
+      case EK_F_RELU_PREPOST: return sk_launch<true, false, uint16_t, EK_F_RELU_PREPOST, 8>(a, st);
+      case EK_F_PRE: return sk_launch<true, false, uint16_t, EK_F_PRE, 8>(a, st);
+      case EK_ANY: return sk_launch<true, false, uint16_t, EK_ANY, 8>(a, st);
       default: return hipErrorInvalidValue;
     }
   }
   if (p.a_kc && p.b_kc) {  // dX = dZ · Wᵀ
     switch (ek) {
-      case EK_STORE: return sk_launch<true, true, uint16_t, EK_STORE>(a, st);
-      case EK_BWD_MASK: return sk_launch<true, true, uint16_t, EK_BWD_MASK>(a, st);
-      case EK_ANY: return sk_launch<true, true, uint16_t, EK_ANY>(a, st);
+      case EK_STORE: return sk_launch<true, true, uint16_t, EK_STORE, 8>(a, st);
+      case EK_BWD_MASK: return sk_launch<true, true, uint16_t, EK_BWD_MASK, 8>(a, st);
+      case EK_ANY: return sk_launch<true, true, uint16_t, EK_ANY, 8>(a, st);
       default: return hipErrorInvalidValue;
     }
   }
   if (!p.a_kc && !p.b_kc) {  // dW = Xᵀ · dZ
     switch (ek) {
-      case EK_STORE: return sk_launch<false, false, uint16_t, EK_STORE>(a, st);
-      case kSkF32: return sk_launch<false, false, float, kSkF32>(a, st);
+      case EK_STORE: return sk_launch<false, false, uint16_t, EK_STORE, 8>(a, st);
+      case kSkF32: return sk_launch<false, false, float, kSkF32, 8>(a, st);
       default: return hipErrorInvalidValue;
     }
   }
   return hipErrorInvalidValue;
-#endif
 }
 
 }  // namespace
@@ -514,10 +590,19 @@ bool sk_default() {
   return on;
 }
 
+bool deterministic() {
+  static const bool on = [] {
+    const char* e = getenv("PZ_DETERMINISTIC");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 bool sk_eligible(const GemmArgs& p) {
   if (p.force_generic || p.in_dtype != DT_BF16 || (p.out_dtype != DT_BF16 && p.out_dtype != DT_F32)) return false;
   if (p.bias64 != nullptr || p.colsum64 != nullptr) return false;
-  if (p.M <= 0 || p.N <= 0 || p.M % kSkB != 0 || p.N % kSkB != 0 || p.K % kSkBK != 0 || p.K < 2 * kSkBK) return false;
+  const int bk = sk_waves(p) == 8 ? SkGeo<8>::BK : SkGeo<4>::BK;
+  if (p.M <= 0 || p.N <= 0 || p.M % kSkB != 0 || p.N % kSkB != 0 || p.K % bk != 0 || p.K < 2 * bk) return false;
   if (!p.a_kc && p.b_kc) return false;  // (no MLP GEMM has this layout)
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
   if (!al16(p.A) || !al16(p.B) || (p.C != nullptr && !al16(p.C))) return false;
@@ -530,7 +615,8 @@ bool sk_eligible(const GemmArgs& p) {
   if (p.out8 != nullptr && (p.out8_fmt != (p.epi_mode == EPI_BWD ? 1 : 0) || p.ldout8 % 8 != 0 ||
                             (reinterpret_cast<uintptr_t>(p.out8) & 7) != 0 || p.out8_qscale == nullptr))
     return false;
-  return sk_epi_kind(p) >= 0;
+  const int ek = sk_epi_kind(p);
+  return ek >= 0 && (sk_waves(p) == 8 || ek == EK_STORE);
 }
 
 int sk_tickets(const GemmArgs* probs, int n) { return sk_plan(probs, n).sk_tiles; }

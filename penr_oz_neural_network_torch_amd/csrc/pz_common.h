@@ -296,6 +296,63 @@ PZ_DEV double wave_sum_d(double v) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Deterministic column sums across workgroups (bias gradients): instead of one float atomic per
+// column and workgroup (a sum whose order is the arrival order), producer `idx` stores its partial
+// row [nparts][ld] write-through (4-B sc1 stores), then the last arriver of its group of `group`
+// producers folds that group's rows IN ROW ORDER into a group row (written after the partials, at
+// row nparts + g), and the last group folder folds the group rows in order into colsum[c] (+=).
+// Hand-off: MI355X_MICROARCH table row 1 (sc1 stores, every wave's vmcnt(0), barrier, one relaxed
+// agent-scope ticket per producer; sc1 loads). Tickets: [ceil(nparts / group) + 1], zero between
+// launches (each last arriver resets the one it completed).
+PZ_DEV void st_wt(float* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+PZ_DEV float ld_wt(const float* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// every wave's stores drained, then one ticket: true (block-uniform) in the expect-th arriver
+PZ_DEV bool det_ticket(int* ticket, int expect, PZ_LDS int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = prev == expect - 1;
+    if (last) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  return __builtin_amdgcn_readfirstlane(*flag) != 0;
+}
+
+// rows [r0, r1) of column c, summed in row order (loads issued 8 at a time)
+PZ_DEV float det_fold(const float* ws, int64_t ld, int r0, int r1, int c) {
+  float s = 0.f;
+  int r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = ld_wt(ws + static_cast<int64_t>(r + k) * ld + c);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += v[k];
+  }
+  for (; r < r1; ++r) s += ld_wt(ws + static_cast<int64_t>(r) * ld + c);
+  return s;
+}
+
+// after this block stored its row idx (columns [0, cols) of ws + idx * ld): the fold levels
+template <int NT>
+PZ_DEV void det_colsum(float* ws, int* tickets, int nparts, int group, int idx, int cols, int64_t ld, float* colsum,
+                       PZ_LDS int* flag) {
+  const int ngroups = (nparts + group - 1) / group;
+  const int g = idx / group, gr0 = g * group, gr1 = min(nparts, gr0 + group);
+  if (!det_ticket(tickets + g, gr1 - gr0, flag)) return;
+  if (ngroups == 1) {
+    for (int c = threadIdx.x; c < cols; c += NT) colsum[c] += det_fold(ws, ld, 0, nparts, c);
+    return;
+  }
+  for (int c = threadIdx.x; c < cols; c += NT) st_wt(ws + static_cast<int64_t>(nparts + g) * ld + c, det_fold(ws, ld, gr0, gr1, c));
+  if (!det_ticket(tickets + ngroups, ngroups, flag)) return;
+  for (int c = threadIdx.x; c < cols; c += NT) colsum[c] += det_fold(ws, ld, nparts, nparts + ngroups, c);
+}
+
+// ------------------------------------------------------------------------------------------
 // one parameter's optimizer update, shared by optimizer_step (optim.hip) and the dW-GEMM-fused
 // update (EPI_OPT, gemm_mfma.hip) so both round identically. Adam = torch.optim.Adam's single-
 // tensor step (lerp_, mul_/addcmul_, sqrt/div/add_, addcdiv_); SGD = the reference's

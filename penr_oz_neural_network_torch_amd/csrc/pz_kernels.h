@@ -35,6 +35,10 @@ struct XentArgs {
   double grad_scale;    // usually 1/global_batch
   float* colsum;        // += column sums of dh (bias gradient), may be null
   double* colsum64;     // fp64 logits: column sums in double instead
+  // bf16 heads, deterministic column sums (pz_common.h det_colsum): [blocks + groups][cols] partial
+  // rows and tickets; null = float atomics
+  float* cs_ws;
+  int* cs_tickets;
   void* probs;          // optional softmax output [rows][ld_probs]
   int64_t ld_probs;
   EpiSpec epi;          // logits' dropout (drop_pre); act must be NONE

@@ -65,6 +65,10 @@ struct GemmArgs {
   // (used instead of bias / colsum when set) — the fp64 fused engine stays exact to fp64 rounding
   const double* bias64;
   double* colsum64;
+  // deterministic column sums (pz_common.h det_colsum; bf16 LDS-staged epilogues): per-tile partial
+  // rows [ceil(M / BM) + groups][N] and per-column-strip tickets; null = float atomics
+  float* cs_ws;
+  int* cs_tickets;
   int epi_mode;
   EpiSpec epi;
   int64_t idx_ld;     // logical row stride used for dropout element indices (usually N)
@@ -108,7 +112,7 @@ struct GemmArgs {
   int prio;  // s_setprio(1) around the ping-pong MFMA blocks (set by the launcher, PZ_GEMM_PRIO)
   // persistent stream-K engine (gemm_sk.hip): workgroups = CUs it may occupy (0 = every CU; the
   // trainer lowers it while RCCL channels hold CUs), engine 0 = default choice, 1 = the tiled
-  // kernels of gemm_mfma.hip, 2 = stream-K
+  // kernels of gemm_mfma.hip, 2 = stream-K (8-wave ping-pong loop), 3 = stream-K on the 4-wave lab loop
   int cus;
   int engine;
 };
@@ -121,6 +125,9 @@ int64_t sk_ws_floats(const GemmArgs* probs, int n);
 int sk_tickets(const GemmArgs* probs, int n);  // per-tile ticket counters needed
 hipError_t gemm_sk(const GemmArgs* probs, int n, float* ws, int* counters, hipStream_t stream);
 bool sk_default();  // PZ_GEMM_SK: the engine gemm() picks for eligible shapes
+// PZ_DETERMINISTIC (default 1): bias-gradient column sums of the bf16 GEMM epilogues and heads are
+// folded in a fixed order (pz_common.h det_colsum) instead of float atomics
+bool deterministic();
 
 // split-K plan for the MFMA path: 1 = none. Workspace floats needed: gemm_split_ws_floats().
 int gemm_split(const GemmArgs& args);

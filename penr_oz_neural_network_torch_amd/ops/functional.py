@@ -113,7 +113,8 @@ def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Ten
     ``store_c=False`` (MFMA path, bf16 ``out``): only the side outputs — ``out8``, ``mask``,
     ``colsum`` — are written, ``out`` is not (the fp8 policy's bf16 tensors nobody reads).
     ``engine``: 0 = the default choice, 1 = the tiled kernels (gemm_mfma.hip), 2 = the persistent
-    stream-K engine (gemm_sk.hip; raises if the shape is not eligible); ``cus`` = the CU budget of
+    stream-K engine (gemm_sk.hip; raises if the shape is not eligible), 3 = that engine on its
+    4-wave lab main loop (plain stores only); ``cus`` = the CU budget of
     the persistent engine (0 = every CU).
     """
     M, N = out.shape

@@ -127,3 +127,55 @@ def test_sk_matches_tiled_engine_bitwise_on_whole_tiles(native_lib):
     PF.gemm(a, True, b, False, o1, engine=1)
     PF.gemm(a, True, b, False, o2, engine=2, cus=256)
     assert torch.equal(o1, o2)
+
+
+@pytest.mark.parametrize("engine,cus", [(1, 0), (2, 256), (2, 200)])
+def test_bias_gradient_colsums_are_deterministic(native_lib, engine, cus):
+    """PZ_DETERMINISTIC (default): the backward epilogue's bias-gradient column sums are folded in
+    tile-row order (pz_common.h det_colsum), not in atomic arrival order — bit-identical across runs,
+    on the tiled and the stream-K engines, and equal to the fp64 column sums of the stored dX."""
+    M, N, K = 8192, 4096, 1024
+    g, w, _ = _ops(M, N, K, True, True, 21)
+    mask = PF.relu_mask_empty(M, N, device=DEV)
+    mask.random_(0, 256)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=0.1, seed=(3, 4))
+    outs = []
+    for _ in range(3):
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        colsum = torch.zeros(N, device=DEV)
+        PF.gemm(g, True, w, True, out, colsum=colsum, mode=PF.EPI_BWD, epi=epi, mask=mask, engine=engine, cus=cus)
+        outs.append((out, colsum))
+    assert all(torch.equal(outs[0][1], o[1]) and torch.equal(outs[0][0], o[0]) for o in outs[1:])
+    ref = outs[0][0].double().sum(0)
+    assert (outs[0][1].double() - ref).abs().max().item() <= 1e-4 * ref.abs().max().item() + 1e-3
+
+
+@pytest.mark.parametrize("B,C", [(8192, 1024), (4096, 2048)])
+def test_head_colsums_are_deterministic(native_lib, B, C):
+    """The lean bf16 cross-entropy head's bias-gradient sums: partial rows of 32-row blocks folded
+    in block order over two ticketed levels — bit-identical across runs, close to fp64."""
+    logits = (torch.randn(B, C, device=DEV) * 2).to(torch.bfloat16)
+    labels = torch.randint(0, C, (B,), device=DEV)
+    ei, ef = PF.epi_spec(drop_pre=4, p=0.1, seed=(1, 9))
+    sums = []
+    for _ in range(3):
+        loss, colsum = torch.zeros(1, device=DEV), torch.zeros(C, device=DEV)
+        dh = torch.empty(B, C, device=DEV, dtype=torch.bfloat16)
+        torch.ops.pz.xent_head(logits, labels, B, loss, 1.0 / B, dh, 1.0 / B, colsum, None, ei, ef, C)
+        sums.append((colsum, dh))
+    assert all(torch.equal(sums[0][0], s[0]) for s in sums[1:])
+    ref = (torch.softmax(logits.double(), 1) - torch.nn.functional.one_hot(labels, C)) / B
+    ref = ref * torch.from_numpy(keep_mask(B * C, 1, 9, 4, 0.1).reshape(B, C)).to(DEV) / 0.9
+    assert (sums[0][0].double() - ref.sum(0)).abs().max().item() <= 1e-3 * ref.abs().max().item() * math.sqrt(B)
+
+
+@pytest.mark.parametrize("layout", ["fwd", "dx", "dw"])
+def test_sk_four_wave_lab_loop(native_lib, layout):
+    """engine 3: the stream-K engine on its 4-wave 128x128-wave-tile lab loop (plain stores)."""
+    a_kc, b_kc = {"fwd": (True, False), "dx": (True, True), "dw": (False, False)}[layout]
+    M, N, K = 2048, 2048, 1024
+    a, b, ref = _ops(M, N, K, a_kc, b_kc, 5)
+    for cus in (256, 200):
+        out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+        PF.gemm(a, a_kc, b, b_kc, out, engine=3, cus=cus)
+        _close(out, ref, K)

@@ -2,7 +2,7 @@
 # Hardware-counter passes over tools/gemm_bench.py cases (one rocprofv3 run per counter group,
 # kernel-trace only: never combined with sys/runtime traces). Summarise with
 # `python tools/pmc_summary.py gpurun_out/pmc_<tag>`.
-# usage: PMC_SET=core|mem tools/pmc_gemm.sh <tag> <gemm_bench case>...
+# usage: PMC_SET=core|mem [PMC_PROG=tools/sk_bench.py] tools/pmc_gemm.sh <tag> <bench args>...
 set -e
 tag=$1; shift
 out=$(pwd)/gpurun_out/pmc_$tag
@@ -24,5 +24,5 @@ i=0
 for g in "${groups[@]}"; do
   i=$((i + 1))
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 180 rocprofv3 --kernel-trace --pmc $g -d "$out/g$i" -o run \
-      -- python3 "$repo/tools/gemm_bench.py" "$@") > "$out/g$i.log" 2>&1
+      -- python3 "$repo/${PMC_PROG:-tools/gemm_bench.py}" "$@") > "$out/g$i.log" 2>&1
 done

@@ -13,6 +13,8 @@ import sys
 def short(name: str) -> str:
     if "gemm_mfma_kernel" in name:
         return "pz_gemm<" + name.split("gemm_mfma_kernel<", 1)[1].split(">(", 1)[0] + ">"
+    if "gemm_sk_kernel" in name:
+        return "pz_sk<" + name.split("gemm_sk_kernel<", 1)[1].split(">(", 1)[0] + ">"
     if name.startswith("Cijk_"):
         return name[:60]
     return name.split("(", 1)[0][:60]
@@ -20,7 +22,7 @@ def short(name: str) -> str:
 
 def main():
     root = sys.argv[1]
-    keep = sys.argv[2:] or ["gemm_mfma", "Cijk_"]
+    keep = sys.argv[2:] or ["gemm_mfma", "gemm_sk", "Cijk_"]
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
 
     def add(kernel, counter, value):
