@@ -789,67 +789,35 @@ hipError_t launch_layout(const GemmArgs& p, hipStream_t s) {
 #ifndef PZ_GEMM_LAB  // tools/gemm_lab.hip instantiates only the variants it measures
 // buffer-addressed DMA (VAR 6) needs every staged byte within 4 GiB of the operand's base
 bool buffer_ok(const GemmArgs& p) {
-  static const bool off = [] {  // PZ_GEMM_BUF=0: flat-addressed DMA everywhere (A/B experiments)
-    const char* e = getenv("PZ_GEMM_BUF");
-    return e != nullptr && atoi(e) == 0;
-  }();
-  if (off) return false;
   constexpr int64_t kLim = int64_t(1) << 32;
   const int64_t ea = (p.a_kc ? static_cast<int64_t>(p.M) : static_cast<int64_t>(p.K)) * p.lda * 2;
   const int64_t eb = (p.b_kc ? static_cast<int64_t>(p.N) : static_cast<int64_t>(p.K)) * p.ldb * 2;
   return ea < kLim && eb < kLim;
 }
 
-// PZ_GEMM_P128=1: 128x128 tiles (two workgroups per CU) instead of split-K 256x256 when the
-// shape has at least two such tiles per CU. In isolation fwd [8192,1024] K=4096 runs 950 vs 855
-// TFLOP/s (tools/gemm_lab), but the mlp4 step is 0.9% SLOWER with it (same-box A/B x3), so off.
-bool prefer_128(const GemmArgs& p) {
-  static const int on = [] {  // 1: every eligible shape, 2: bf16-output (forward / dX) shapes only
-    const char* e = getenv("PZ_GEMM_P128");
-    return e != nullptr ? atoi(e) : 0;
-  }();
-  if (on == 0 || (on == 2 && p.out_dtype != DT_BF16)) return false;
-  constexpr int kFill = 240;
-  const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  const int t128 = ((p.M + 127) / 128) * ((p.N + 127) / 128);
-  return t256 < kFill && t128 >= 2 * kFill;
-}
-
+// (measured, not kept: 128x128 tiles, two workgroups per CU, instead of split-K 256x256 for
+// skinny shapes — fwd [8192,1024] K=4096 950 vs 855 TFLOP/s alone, the mlp4 step 0.9% slower)
 // 64-deep ring steps (VAR 30: 2 x 64 KiB slots, one MFMA interval = 64 MFMAs per wave, the
 // staging waves fetch whole 128-B lines of K-contiguous rows) for layouts with an M/N-contiguous
 // operand: fwd [8192,4096]x[4096,4096] +6%, dW +4%, fwd K=1024 +4% (tools/gemm_lab, same box).
 // Both operands K-contiguous (dX) stay on the 32-deep ring: the BK64 form spills there (-11%).
 bool use_bk64(const GemmArgs& p, bool buf) {
-  // PZ_GEMM_BK64=0: 32-deep ring everywhere; =2: not for K-contiguous x K-contiguous (A/B)
-  static const int mode = [] {
-    const char* e = getenv("PZ_GEMM_BK64");
-    return e != nullptr ? atoi(e) : 1;
-  }();
-  const bool off = mode == 0 || (mode == 2 && p.a_kc && p.b_kc);
   const int split = p.split_k > 1 ? p.split_k : 1;
   // VAR 30 stages K-contiguous operands without a row clamp: full 256-row tiles only (which
   // also frees the K-contiguous x K-contiguous dX GEMMs from a scratch spill: +5..6%, lab)
   const bool full = (!p.a_kc || p.M % 256 == 0) && (!p.b_kc || p.N % 256 == 0);
-  return !off && buf && full && p.K % 64 == 0 && (p.K / 64) % split == 0;
+  return buf && full && p.K % 64 == 0 && (p.K / 64) % split == 0;
 }
 
 // which specialised epilogue (gemm_epilogue.h: EK_*) covers these arguments
 int epi_kind(const GemmArgs& p) {
-  static const bool off = [] {  // PZ_GEMM_EK=0: the generic epilogue everywhere (A/B)
-    const char* e = getenv("PZ_GEMM_EK");
-    return e != nullptr && atoi(e) == 0;
-  }();
-  if (off || p.out_dtype != DT_BF16 || p.accumulate) return EK_ANY;
+  if (p.out_dtype != DT_BF16 || p.accumulate) return EK_ANY;
   if (p.epi_mode == EPI_STORE && p.bias == nullptr && p.colsum == nullptr && p.mask == nullptr && p.out8 == nullptr)
     return EK_STORE;
   if (p.epi_mode == EPI_FWD && (p.epi.act == ACT_NONE || p.epi.act == ACT_RELU) && p.colsum == nullptr) {
-    static const bool fixed_off = [] {  // PZ_GEMM_EKF=0: EK_RELU for every forward stage (A/B)
-      const char* e = getenv("PZ_GEMM_EKF");
-      return e != nullptr && atoi(e) == 0;
-    }();
     const EpiSpec& e = p.epi;
     const bool relu = e.act == ACT_RELU;
-    if (!fixed_off && !e.drop_all) {
+    if (!e.drop_all) {
       if (relu && !e.drop_pre && e.drop_post) return EK_F_RELU_POST;
       if (relu && e.drop_pre && e.drop_post) return EK_F_RELU_PREPOST;
       if (!relu && e.drop_pre && !e.drop_post) return EK_F_PRE;
@@ -887,46 +855,28 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   const bool buf = buffer_ok(p);
   const bool bk64 = use_bk64(p, buf);
   constexpr int kFill = 240;  // ~ CU count: a config below this leaves CUs idle
-  // experiments (probe variants live in tools/gemm_lab.hip): PZ_GEMM_TILE=1 (256x256 flat DMA)
-  // 2 (256x128) 3 (128x128) 16 (256x256 buffer DMA)
-  static const int forced = [] {
-    const char* e = getenv("PZ_GEMM_TILE");
-    return e ? atoi(e) : 0;
-  }();
   if (p.split_k > 1) {  // slabs sized for 256x256
     if (bk64) return launch_bk64_256<OutT, AuxT, 30>(p, s);
     if (buf) return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
     return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
-  }
-  switch (forced) {
-    case 16: return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
-    case 1: return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
-    case 2: return launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
-    case 3: return launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
-    default: break;
   }
   // buffer-addressed LDS-DMA (VAR 6; +2..12% on the step's shapes, tools/gemm_lab)
   if (tiles(256, 256) >= kFill) {
     if (bk64) return launch_bk64_256<OutT, AuxT, 30>(p, s);
     return buf ? launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s) : launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
   }
-  if (!prefer_128(p) && tiles(256, 128) >= kFill) {
+  if (tiles(256, 128) >= kFill) {
     if (bk64) return launch_layout<256, 128, 4, 2, OutT, AuxT, 30>(p, s);
     return buf ? launch_layout<256, 128, 4, 2, OutT, AuxT, 6>(p, s) : launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
   }
   return buf ? launch_layout<128, 128, 2, 2, OutT, AuxT, 6>(p, s) : launch_layout<128, 128, 2, 2, OutT, AuxT>(p, s);
 }
 
-// PZ_F8_2WG (default 1): fp8 GEMMs with at least two 256x256 tiles per CU and no split-K run as
-// 256x128 tiles on 4-wave workgroups, two per CU (VAR 16 / 17): one workgroup's epilogue beside
-// the other's main loop. 0: the 8-wave ping-pong 256x256 kernels (VAR 15 / 9)
+// fp8 GEMMs with at least two 256x256 tiles per CU and no split-K run as 256x128 tiles on 4-wave
+// workgroups, two per CU (VAR 16 / 17): one workgroup's epilogue beside the other's main loop
 bool f8_two_wg(const GemmArgs& p) {
-  static const bool on = [] {
-    const char* e = getenv("PZ_F8_2WG");
-    return e == nullptr || atoi(e) != 0;
-  }();
   const int t256 = ((p.M + 255) / 256) * ((p.N + 255) / 256);
-  return on && p.split_k <= 1 && t256 >= 480 && p.N % 128 == 0;
+  return p.split_k <= 1 && t256 >= 480 && p.N % 128 == 0;
 }
 
 hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
@@ -959,44 +909,21 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
     if (ek == EK_F_PRE) return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15, EK_F_PRE>(p, s);
     return launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 15>(p, s);
   }
-  // PZ_GEMM_F8BUF=1: buffer-addressed staging DMA (VAR 10 / 11), A/B
-  static const bool f8buf = [] {
-    const char* e = getenv("PZ_GEMM_F8BUF");
-    return e != nullptr && atoi(e) == 1;
-  }();
-  const bool buf = f8buf && buffer_ok(p);
-  // PZ_GEMM_F8BK64=1: the 64-deep ring (VAR 12 / 13: 256x256 tiles, full rows of both
-  // K-contiguous operands, K a multiple of 128 bytes per slice). Within noise of the 32-deep ring
-  // (f8 GEMMs -1..+3%, mlp8192 step 0.822-0.832 vs 0.819-0.827 ms, profiles/r2_ab_fp8_bk64.txt): off
-  static const bool bk64_on = [] {
-    const char* e = getenv("PZ_GEMM_F8BK64");
-    return e != nullptr && atoi(e) == 1;
-  }();
-  if (ek_fixed(ek)) ek = EK_RELU;  // (VAR 8 / 10 / 12 forms: the generic ReLU-stage kind)
-  const int split = p.split_k > 1 ? p.split_k : 1;
-  const bool bk64 = bk64_on && buffer_ok(p) && p.M % 256 == 0 && p.N % 256 == 0 && p.K % 128 == 0 &&
-                    (p.K / 128) % split == 0 && (tiles >= 240 || p.split_k > 1);
-  if (bk64)
-    return p.a_fmt == 1 ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 13>(p, s)
-                        : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 12>(p, s);
+  // (measured, not kept: buffer-addressed staging, VAR 10 / 11; the 64-deep ring, VAR 12 / 13,
+  // within noise of the 32-deep one, profiles/r2_ab_fp8_bk64.txt)
+  if (ek_fixed(ek)) ek = EK_RELU;  // (VAR 8 forms: the generic ReLU-stage kind)
   const bool big = tiles >= 240 || p.split_k > 1;
   if (p.a_fmt == 1) {  // e5m2 x e4m3 (backward dX)
-    if (!buf && ek == EK_BWD_MASK)
+    if (ek == EK_BWD_MASK)
       return big ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9, EK_BWD_MASK>(p, s)
                  : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 9, EK_BWD_MASK>(p, s);
-    if (big)
-      return buf ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 11>(p, s)
-                 : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>(p, s);
-    return buf ? launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 11>(p, s)
+    return big ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 9>(p, s)
                : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 9>(p, s);
   }
-  if (!buf && ek == EK_RELU)
+  if (ek == EK_RELU)
     return big ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8, EK_RELU>(p, s)
                : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8, EK_RELU>(p, s);
-  if (big)
-    return buf ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 10>(p, s)
-               : launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s);
-  return buf ? launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 10>(p, s)
+  return big ? launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 8>(p, s)
              : launch_cfg<128, 128, 2, 2, true, true, uint16_t, uint16_t, 8>(p, s);
 }
 
@@ -1102,29 +1029,16 @@ bool mfma_eligible(const GemmArgs& p) {
 }
 
 int gemm_split(const GemmArgs& p) {
-  static const int mode = [] {  // PZ_SPLITK=0 disables split-K (experiments)
-    const char* e = getenv("PZ_SPLITK");
-    return e ? atoi(e) : 1;
-  }();
-  static const bool forced_tile = getenv("PZ_GEMM_TILE") != nullptr;
   // fp8 skinny shapes run better as 128x128 tiles (measured: split-K 256x256 -4%); the fp8
   // weight-gradient GEMM (both operands M/N-contiguous, 256-tiles only) splits like bf16
   // (and the N-contiguous-weight fp8 forward, VAR 15: 256x256 tiles only)
   const bool f8_dw = p.in_dtype == DT_FP8 && !p.b_kc;
-  if (mode == 0 || forced_tile || (p.in_dtype == DT_FP8 && !f8_dw) || !mfma_eligible(p)) return 1;
+  if ((p.in_dtype == DT_FP8 && !f8_dw) || !mfma_eligible(p)) return 1;
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   constexpr int kFill = 240;
-  if (tiles >= kFill || prefer_128(p)) return 1;
-  // PZ_GEMM_W128=1: bf16 outputs (forward / dX) on 256x128 tiles (64-deep ring) instead of a
-  // split. Isolated fwd [8192,1024] K=4096 runs 1008 vs 881 TF/s (tools/gemm_lab,
-  // profiles/r2_lab_skinny_fwd.txt) but the steps are SLOWER with it (mlp4 1.260-1.272 vs
-  // 1.243 ms, mlp8192 bf16 0.918 vs 0.878 ms, same box): off
-  static const bool w128 = [] {
-    const char* e = getenv("PZ_GEMM_W128");
-    return e != nullptr && atoi(e) == 1;
-  }();
-  const int t256x128 = ((p.M + 255) / 256) * ((p.N + 127) / 128);
-  if (w128 && p.out_dtype == DT_BF16 && t256x128 >= kFill) return 1;
+  if (tiles >= kFill) return 1;
+  // (measured, not kept: bf16 outputs on 256x128 tiles instead of a split — fwd [8192,1024]
+  // K=4096 1008 vs 881 TF/s alone, the mlp4 step slower, profiles/r2_lab_skinny_fwd.txt)
   const int nk = p.K / (p.in_dtype == DT_FP8 ? 64 : kBK);
   for (int sp : {2, 4, 8})
     if (tiles * sp >= kFill && nk % sp == 0 && nk / sp >= 16) return sp;
@@ -1140,14 +1054,6 @@ int64_t gemm_split_ws_floats(const GemmArgs& p) {
 // whole-tile epilogue stores write through (sc1) instead of leaving dirty L2 lines for the kernel
 // boundary's write-back (GemmArgs::store_wt); on by default, PZ_GEMM_WT=0 turns it off. r4 A/B,
 // mlp4 step: 1.1112 ms off, 1.1081 on; with PZ_OPT_NT on 1.1023 -> 1.0975
-int prio_default() {  // PZ_GEMM_PRIO=0: no s_setprio bracket around the ping-pong MFMA blocks (A/B)
-  static const int on = [] {
-    const char* e = getenv("PZ_GEMM_PRIO");
-    return e != nullptr ? atoi(e) : 1;
-  }();
-  return on;
-}
-
 int store_wt_default() {
   static const int on = [] {
     const char* e = getenv("PZ_GEMM_WT");
@@ -1161,14 +1067,15 @@ int store_wt_default() {
 int gemm_pair_split(const GemmArgs& a, const GemmArgs& b) {
   for (const GemmArgs* q : {&a, &b}) {
     const GemmArgs& p = *q;
-    if (p.a_kc || p.b_kc || p.epi_mode != EPI_STORE || p.accumulate || p.force_generic) return 0;
+    if (p.a_kc || p.b_kc || (p.epi_mode != EPI_STORE && p.epi_mode != EPI_OPT) || p.accumulate || p.force_generic)
+      return 0;
     if (p.bias || p.colsum || p.mask || p.out8 || p.aux || p.bias64 || p.colsum64) return 0;
     if (p.M % 256 || p.N % 256 || p.K % 64 || !mfma_eligible(p)) return 0;
     if (p.in_dtype != DT_FP8 && (!buffer_ok(p) || epi_kind(p) != (p.out_dtype == DT_BF16 ? EK_STORE : EK_ANY)))
       return 0;
   }
   if (a.K != b.K || a.in_dtype != b.in_dtype || a.out_dtype != b.out_dtype || a.a_fmt != b.a_fmt ||
-      a.b_fmt != b.b_fmt)
+      a.b_fmt != b.b_fmt || a.epi_mode != b.epi_mode)
     return 0;
   if (a.in_dtype == DT_FP8 && a.out_dtype != DT_BF16) return 0;
   const int tiles = (a.M / 256) * (a.N / 256) + (b.M / 256) * (b.N / 256);
@@ -1188,7 +1095,7 @@ hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
   g.p[0] = a;
   g.p[1] = b;
   g.p[0].store_wt = g.p[1].store_wt = store_wt_default();
-  g.p[0].prio = g.p[1].prio = prio_default();
+  g.p[0].prio = g.p[1].prio = 1;
   g.nwg0 = (a.M / 256) * (a.N / 256) * split;
   const int nwg = g.nwg0 + (b.M / 256) * (b.N / 256) * split;
   if (a.in_dtype == DT_FP8) return launch_pair_cfg<uint16_t, 14, EK_STORE>(g, nwg, s);
@@ -1199,7 +1106,7 @@ hipError_t gemm_pair(const GemmArgs& a, const GemmArgs& b, hipStream_t s) {
 hipError_t gemm_mfma(const GemmArgs& in, hipStream_t s) {
   GemmArgs p = in;
   p.store_wt = store_wt_default();
-  p.prio = prio_default();
+  p.prio = 1;
   if (p.split_k > 1 && (p.ws == nullptr || p.counters == nullptr)) return hipErrorInvalidValue;
   if (p.in_dtype == DT_FP8) return launch_fp8(p, s);
   if (p.out_dtype == DT_BF16) return launch_tiles<uint16_t, uint16_t>(p, s);

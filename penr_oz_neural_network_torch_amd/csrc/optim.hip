@@ -383,11 +383,7 @@ hipError_t step_finalize(const FinalizeArgs& a, hipStream_t s) {
 
 hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
   if (a.total_blocks <= 0) return hipSuccess;
-  static const int max_grid = [] {  // PZ_OPT_GRID: resident workgroups (0 = one per work block)
-    const char* e = getenv("PZ_OPT_GRID");
-    return e ? atoi(e) : 0;
-  }();
-  const int cap = a.max_grid > 0 ? a.max_grid : max_grid;
+  const int cap = a.max_grid;  // resident workgroups (0 = one per work block)
   const int grid = cap > 0 && cap < a.total_blocks ? cap : a.total_blocks;
   // one 16-B vector of each stream per load group (PRE = 1): measured 5.7 TB/s for the whole-model
   // Adam update in isolation vs 5.2 with all four of a thread's vectors loaded up front (PRE = 4:
@@ -396,17 +392,9 @@ hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
     if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((optimizer_kernel<false, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   } else {
-    static const bool nt = [] {  // non-temporal state streams, on by default (PZ_OPT_NT=0: off)
-      const char* e = getenv("PZ_OPT_NT");
-      return e == nullptr || atoi(e) != 0;
-    }();
-    if (nt) {
-      if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
-      else hipLaunchKernelGGL((optimizer_kernel<false, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
-    } else {
-      if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
-      else hipLaunchKernelGGL((optimizer_kernel<false, float, 1>), dim3(grid), dim3(kThreads), 0, s, a);
-    }
+    // non-temporal state streams (r4 A/B: mlp4 1.1081 -> 1.1023 ms)
+    if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((optimizer_kernel<false, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
   }
   return hipGetLastError();
 }

@@ -289,15 +289,9 @@ hipError_t quantize_rows_fmt(const void* x, int dtype, int64_t ldx, int rows, in
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(out) & 7) == 0 &&
                     static_cast<int64_t>(rows) * (cols / 8) < (int64_t(1) << 31) && esz > 0;
   if (vec8) {
-    // block cap (PZ_QUANT_GRID): the per-block amax atomics hit one address and serialise, so
-    // fewer, longer-lived blocks; see profiles/r2_ab_quant_grid.txt
-    static const int cap = [] {
-      const char* e = getenv("PZ_QUANT_GRID");
-      return e != nullptr ? atoi(e) : 256;
-    }();
-    // (no amax output: no serialising atomics, 4 blocks per CU)
-    const int g8 = grid_for(static_cast<int64_t>(rows) * (cols / 8), 256 * 4,
-                            amax == nullptr ? 1024 : (cap > 0 ? cap : 256));
+    // block cap 256: the per-block amax atomics hit one address and serialise, so fewer,
+    // longer-lived blocks (profiles/r2_ab_quant_grid.txt); no amax output: 4 blocks per CU
+    const int g8 = grid_for(static_cast<int64_t>(rows) * (cols / 8), 256 * 4, amax == nullptr ? 1024 : 256);
     if (dtype == DT_BF16)
       hipLaunchKernelGGL((quantize_rows8_kernel<uint16_t, E5M2>), dim3(g8), dim3(256), 0, s,
                          static_cast<const uint16_t*>(x), ldx, rows, cols, out, ldo, qs, amax, amax_in, amax_clear);

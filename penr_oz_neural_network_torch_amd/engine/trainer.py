@@ -41,6 +41,7 @@ from ..ops import functional as PF
 from ..ops import native
 from ..parallel.dist import DataParallelContext, get_context
 from .events import StreamEvents
+from .fp8_policy import Fp8Policy
 from .optim import FusedOptimizer
 
 ROW_PAD = 64  # batch rows padded to the GEMM K-tile so dW = XᵀdZ stays on the MFMA path
@@ -160,7 +161,7 @@ def compile_stages(model) -> tuple[list[Stage], str]:
     return stages, head
 
 
-class FusedTrainer:
+class FusedTrainer(Fp8Policy):
     """Owns the device buffers of one GPU model's training run."""
 
     def __init__(self, model, context: DataParallelContext | None = None):
@@ -314,25 +315,37 @@ class FusedTrainer:
         self.fuse_opt = (want and self.overlap and not self.ctx.enabled and self.compute == torch.bfloat16
                          and not self.fp8)
         self._fuse_ok: dict = {}
-        self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
-        self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
-        # the side-stream updates of all layers but the first are queued together behind the last
-        # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
-        self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
-        self._side_pending: list = []
         # PAIRED weight-gradient GEMMs (one process): the dW GEMM of the GEMM stage after the first
         # with the fewest output tiles is deferred to the end of the backward and launched
         # TOGETHER with the first layer's (pz::gemm_pair): two skinny GEMMs that alone each need a
         # 4-way split-K to fill the CUs (mlp4: 64 tiles each) share one launch with a 2-way split
-        # (mlp8192: none) — half the slab hand-offs, one launch and one ramp fewer. Its update
-        # then joins the side stream right behind the pair. PZ_DW_PAIR=0: one launch per dW.
+        # (mlp8192: none) — half the slab hand-offs, one launch and one ramp fewer. bf16 policy:
+        # both weights' updates run in that launch's epilogue (pz::gemm_pair_update), so no update
+        # launch sits between the last dW and the next step's first GEMM; otherwise the partner's
+        # update joins the side stream behind the pair. PZ_DW_PAIR=0: one launch per dW.
         self._pair_idx = None
         if (os.environ.get("PZ_DW_PAIR", "1") == "1" and not self.ctx.enabled and not self.fuse_opt
                 and self.overlap and self.stages[0].kind == "gemm"):
             cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
             if cands:
                 self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
+        self._pair_update = (self._pair_idx is not None and self.compute == torch.bfloat16 and not self.fp8
+                             and self.master == torch.float32)
+        self._w1_pending = None  # (pair_update fallback: the first layer's own update group)
+        fused = gemm_w if (self.fuse_opt or self._pair_update) else gemm_w[1:]
+        self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
+        self.opt.define_groups(fused)
+        # the side-stream updates of all layers but the first are queued together behind the last
+        # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
+        self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
+        self._side_pending: list = []
         self._pair_dw = None       # (stage, x_in, dZ) of the dW GEMM that waits for its partner
+        # data parallel: the backward GEMMs issued while a gradient bucket is on the wire run on the
+        # persistent engine with the CUs the collective kernels leave (parallel/dist.py comm_cus)
+        self._cus = 0
+        self._cus_comm = 0
+        if self.ctx.enabled and self.ctx.comm_cus > 0 and self.dev.type == "cuda":
+            self._cus_comm = torch.cuda.get_device_properties(self.dev).multi_processor_count - self.ctx.comm_cus
         self._opt_done = None
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
         self._ov = None
@@ -475,40 +488,6 @@ class FusedTrainer:
 
     # ------------------------------------------------------------------------------------
     # epilogue specs
-    def _refresh_fp8_weights(self, only: Stage | None = None, parity: int | None = None) -> None:
-        """Current-scaled e4m3 weight copies, transposed to [out, in] (K-contiguous GEMM operand).
-        ``parity``: the shadow parity of the optimizer update that just wrote the weights (its amax
-        is already reduced); None: reduce the amax here (initial copies)."""
-        ops = torch.ops.pz
-        if parity is not None and self._w8_fused:
-            return  # the optimizer update wrote the e4m3 copies and their scale records
-        for st in self.stages if only is None else [only]:
-            if st.kind != "gemm":
-                continue
-            k = st.w8_index
-            w = self.store.view(st.seg_w)
-            if self._w8_nat:
-                w8 = self.w8[st.seg_w.offset]
-                if parity is not None:  # q from the amax the update reduced; clear the other parity's
-                    p = parity % 2
-                    ops.quantize_rows(w, w8, self.wqs[k], None, self.wamax2[p, k:k + 1], self.wamax2[1 - p, k:k + 1])
-                else:
-                    ops.amax_abs(w, self.wamax[k:k + 1])
-                    ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
-                    ops.quantize_rows(w, w8, self.wqs[k], None)
-                continue
-            if parity is not None:
-                p = parity % 2
-                ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k], self.wamax2[p, k:k + 1],
-                                    self.wamax2[1 - p, k:k + 1])
-            else:
-                ops.amax_abs(w, self.wamax[k:k + 1])
-                ops.scale_update(self.wamax[k:k + 1], self.wqs[k], 1.0, True)
-                ops.quant_transpose(w, self.w8[st.seg_w.offset], self.wqs[k])
-            w8n = self.w8n.get(st.seg_w.offset)
-            if w8n is not None:  # [in, out] copy for the backward dX GEMM, same scale
-                ops.quantize_rows(w, w8n, self.wqs[k], None)
-
     def _opt_async(self, items: list) -> None:
         """Queue the updates of optimizer groups ``[(key, handles, stages)]`` on the side stream
         behind their gradients: ONE event recorded on the compute stream for all of them (each
@@ -525,80 +504,6 @@ class FusedTrainer:
                 if self.fp8:
                     for st in stages:
                         self._refresh_fp8_weights(st, 1 - self.parity)
-
-    def _plan_fp8(self, rows_b: int) -> None:
-        """Which GEMM stages run their forward on e4m3 operands (shape-eligible ones)."""
-        for st in self.stages:
-            st.fp8 = False
-            st.buffers.pop("y8", None)
-        if not self.fp8:
-            return
-        self.x8 = None
-        for i, st in enumerate(self.stages):
-            if st.kind != "gemm":
-                continue
-            prev = self.stages[i - 1] if i > 0 else None
-            if prev is None:
-                x = self.x_in
-                if x.dtype != torch.bfloat16 or x.shape[1] % 64:
-                    continue
-                x8 = torch.empty(x.shape, device=self.dev, dtype=torch.float8_e4m3fn)
-            else:
-                # the producing GEMM writes the e4m3 copy from its epilogue: it must be on the MFMA path
-                if prev.kind != "gemm" or prev.buffers["y"].shape[1] % 64:
-                    continue
-                px = self.x8 if prev.fp8 and prev.index == 0 else (
-                    self.stages[prev.index - 1].buffers.get("y8") if prev.fp8 else
-                    (self.stages[prev.index - 1].buffers["y"] if prev.index > 0 else self.x_in))
-                pw = self.w8[prev.seg_w.offset] if prev.fp8 else self._w(prev)
-                if px is None or PF.gemm_path(px, True, pw, prev.fp8 and self.w8_kc, prev.buffers["y"]) != "mfma":
-                    continue
-                x8 = torch.empty(prev.buffers["y"].shape, device=self.dev, dtype=torch.float8_e4m3fn)
-            if PF.gemm_path(x8, True, self.w8[st.seg_w.offset], self.w8_kc, st.buffers["y"]) != "mfma":
-                continue
-            st.fp8 = True
-            if prev is None:
-                self.x8 = x8
-            else:
-                prev.buffers["y8"] = x8
-        for i, st in enumerate(self.stages):  # backward: e5m2 dZ x e4m3 W for fused dX GEMMs
-            st.fp8_bwd = False
-            st.buffers.pop("g8", None)
-            prev = self.stages[i - 1] if i > 0 else None
-            # (the [in, out] e4m3 copy is single-buffered: the update of W must not run before this
-            # step's dX GEMM has read it — true with the updates queued after the dX GEMMs)
-            if (st.kind != "gemm" or not st.fp8 or prev is None or prev.kind != "gemm" or not prev.has_epi
-                    or st.seg_w.offset not in self.w8n):
-                continue
-            if st.out_width % 64 or prev.out_width % 8 or rows_b < 64:
-                continue
-            st.fp8_bwd = True
-            st.buffers["g8"] = torch.empty(st.buffers["g"].shape, device=self.dev, dtype=torch.float8_e5m2)
-        # fp8 dW for fp8 stages whose dZ is NOT quantised for a dX GEMM (the first layer): the next
-        # stage's fused dX GEMM writes dZ's e5m2 copy from its epilogue (delayed scaling), so the
-        # weight-gradient GEMM runs on e4m3 x e5m2 without a separate quantisation pass
-        for i, st in enumerate(self.stages):
-            st.g8_from_epi = False
-            nxt = self.stages[i + 1] if i + 1 < len(self.stages) else None
-            if (st.kind != "gemm" or not st.fp8 or getattr(st, "fp8_bwd", False)
-                    or nxt is None or nxt.kind != "gemm" or not st.has_epi or st.out_width % 256
-                    or st.in_width % 256 or rows_b % 64):
-                continue
-            st.g8_from_epi = True
-            st.buffers["g8"] = torch.empty(st.buffers["g"].shape, device=self.dev, dtype=torch.float8_e5m2)
-        self._g8_epi_ready = set()
-        self._y_dead_cache = {}
-        self.data8 = None
-        if self.x8 is not None:
-            # first-layer input: the device-resident dataset is quantised to e4m3 ONCE with a static
-            # dataset-wide scale (its amax bounds every minibatch's), and the per-step gather copies
-            # the sampled e4m3 rows next to the bf16 ones: no per-step amax / quantise pass
-            ops = torch.ops.pz
-            self.data8 = torch.empty(self.data.shape, device=self.dev, dtype=torch.float8_e4m3fn)
-            self.xamax.zero_()
-            ops.amax_abs(self.data, self.xamax)
-            ops.scale_update(self.xamax, self.xqs, 1.0, True)
-            ops.quantize_rows(self.data, self.data8, self.xqs, None)
 
     def _plan_relu_masks(self, rows_b: int) -> None:
         """ReLU GEMM stages feeding a GEMM stage keep a 1-bit mask of ``y > 0`` next to ``y``: the
@@ -845,6 +750,7 @@ class FusedTrainer:
 
         # ---------------- backward
         self._phase("pz.backward")
+        self._cus = 0  # (full grid until the first bucket is on the wire)
         handles = []
         g = last.buffers["g"]
         for si in range(len(self.stages) - 1, -1, -1):
@@ -876,6 +782,9 @@ class FusedTrainer:
             self._side_pending = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
+            if self._w1_pending is not None:
+                self.opt.step_group(self._w1_pending, self.grads, l2, 1.0, 1 - self.parity)
+                self._w1_pending = None
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
             if self.fp8:
                 for st in self._late_stages:
@@ -1113,10 +1022,10 @@ class FusedTrainer:
         else:
             if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
                 x8, sx, g8, sg = f8
-                PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
+                PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg, cus=self._cus)
             else:
-                PF.gemm(x_in, False, g, False, w_grad)
-            mine = [self.ctx.all_reduce_async(w_grad)]
+                PF.gemm(x_in, False, g, False, w_grad, cus=self._cus)
+            mine = [self._bucket(w_grad)]
         handles.extend(mine)
         # the update writes the OTHER shadow set, but it is queued after this layer's dX GEMM
         # (the fp8 dX operand and the float32 policy's GEMMs read the weight itself)
@@ -1142,6 +1051,12 @@ class FusedTrainer:
         f8_p = self._fp8_dw(sp, gp, wp)
         ops0 = (f8_0[0], f8_0[2]) if f8_0 is not None else (x0, g0)
         opsp = (f8_p[0], f8_p[2]) if f8_p is not None else (xp, gp)
+        if self._pair_update and f8_0 is None and f8_p is None and self._pair_update_ok(x0, g0, st0, xp, gp, sp):
+            _, l2, scale = self._ov
+            self.opt.gemm_pair_update(x0, g0, st0.seg_w, xp, gp, sp.seg_w, l2, scale, 1 - self.parity)
+            return None  # (both weights updated: no bucket, no side-stream update)
+        if self._pair_update:  # not eligible here: the first layer's update runs as its own group
+            self._w1_pending = st0.seg_w.offset
         key = ("pair", (f8_0 is None), (f8_p is None), ops0[0].shape, ops0[1].shape, opsp[0].shape, opsp[1].shape)
         ok = self._y_dead_cache.get(key)
         if ok is None:
@@ -1157,90 +1072,23 @@ class FusedTrainer:
                     PF.gemm(a, False, b, False, w, scale_a=f8[1], scale_b=f8[3])
                 else:
                     PF.gemm(a, False, b, False, w)
-        hp = self.ctx.all_reduce_async(wp)
+        hp = self._bucket(wp)
         handles.append(hp)
         self._side_pending.append((sp.seg_w.offset, [hp], [sp]))
-        return self.ctx.all_reduce_async(w0)
+        return self._bucket(w0)
 
-    def _quantize_g8(self, st: Stage, g):
-        """dZ of an fp8 stage -> its e5m2 copy (delayed scaling; the first step calibrates on its
-        own amax), once per step: the dW GEMM and the dX GEMM of the stage both consume it."""
-        g8 = st.buffers["g8"]
-        if self._g8_done.get(st.index) is g:
-            return g8
-        k, ops = st.index, torch.ops.pz
-        if not self._g8_calibrated:  # first step: current scaling from this gradient
-            ops.amax_abs(g, self.gamax[k:k + 1])
-            ops.scale_update(self.gamax[k:k + 1], self.gqs[k], 2.0, True, 57344.0)
-        ops.quantize_rows(g, g8, self.gqs[k], self.gamax[k:k + 1])
-        self._g8_done[st.index] = g
-        return g8
-
-    def _head_g8_ok(self, last: Stage, y, g) -> bool:
-        """The softmax head can write the last stage's e5m2 dZ (fp8 dX stage, delayed scale
-        calibrated, the head kernel's bf16 fast path)."""
-        if not (self.fp8 and getattr(last, "fp8_bwd", False) and self._g8_calibrated and "g8" in last.buffers):
-            return False
-        key = ("head", last.index)
-        if key not in self._y_dead_cache:
-            cols = y.shape[1]
-            self._y_dead_cache[key] = (y.dtype == torch.bfloat16 and g.dtype == torch.bfloat16 and cols % 8 == 0
-                                       and cols <= 2048 and y.stride(0) % 8 == 0 and g.stride(0) % 8 == 0)
-        return self._y_dead_cache[key]
-
-    def _fp8_dw_ready(self, st: Stage) -> bool:
-        """This step's dW GEMM of ``st`` will run on fp8 operands (``_fp8_dw`` returns them)."""
-        if not (self.fp8 and st.fp8 and st.kind == "gemm"):
-            return False
-        if getattr(st, "g8_from_epi", False):
-            if st.index not in self._g8_epi_ready:
-                return False
-        elif not getattr(st, "fp8_bwd", False):
-            return False
-        x8 = self.x8 if st.index == 0 else self.stages[st.index - 1].buffers.get("y8")
-        w_grad = self._w_grad(st.seg_w)
-        return x8 is not None and w_grad.dtype == torch.bfloat16 and self._fp8_dw_shape_ok(st, x8, w_grad)
-
-    def _fp8_dw_shape_ok(self, st: Stage, x8, w_grad) -> bool:
-        """The fp8 dW GEMM (x8 x e5m2 dZ) takes the MFMA path."""
-        key = ("dwshape", st.index)
+    def _pair_update_ok(self, x0, g0, st0, xp, gp, sp) -> bool:
+        key = ("pair_upd", x0.shape, g0.shape, xp.shape, gp.shape)
         ok = self._y_dead_cache.get(key)
         if ok is None:
-            ok = self._y_dead_cache[key] = PF.gemm_path(x8, False, st.buffers["g8"], False, w_grad) == "mfma"
+            ok = self._y_dead_cache[key] = torch.ops.pz.gemm_pair_update_ok(
+                x0, g0, self.store.view(st0.seg_w), xp, gp, self.store.view(sp.seg_w)) > 0
         return ok
 
-    def _fp8_dw_ready_cached(self, st: Stage) -> bool:
-        key = ("dw", st.index, st.index in self._g8_epi_ready)
-        if key not in self._y_dead_cache:
-            self._y_dead_cache[key] = self._fp8_dw_ready(st)
-        return self._y_dead_cache[key]
-
-    def _y_dead(self, st: Stage) -> bool:
-        """fp8 policy: nobody reads the bf16 output of ``st`` this step — the next stage's forward
-        and weight-gradient GEMMs take its e4m3 copy, the next dX GEMM's ReLU derivative its
-        bitmask — so the forward epilogue writes only those (mlp8192: 128 MB of writes a step)."""
-        if "y8" not in st.buffers or st.buffers.get("mask") is None or st.index + 1 >= len(self.stages):
-            return False
-        return self._fp8_dw_ready_cached(self.stages[st.index + 1])
-
-    def _fp8_dw(self, st: Stage, g, w_grad):
-        """fp8 weight-gradient operands (BASELINE config 5): the stage input's e4m3 copy (written by
-        the previous GEMM's epilogue, or the gathered e4m3 dataset rows) and dZ's e5m2 copy, both
-        M/N-contiguous, with their dequantisation factors — or None (bf16 dW)."""
-        if not (self.fp8 and st.fp8):
-            return None
-        if getattr(st, "g8_from_epi", False):  # dZ's e5m2 copy came from the dX epilogue this step
-            if self._g8_done.get(st.index) is not g:
-                return None
-        elif not getattr(st, "fp8_bwd", False):
-            return None
-        i = st.index
-        x8, sx = (self.x8, self.xqs[1:2]) if i == 0 else (self.stages[i - 1].buffers.get("y8"), self.aqs[i - 1, 1:2])
-        if x8 is None or w_grad.dtype != torch.bfloat16:
-            return None
-        if not self._fp8_dw_shape_ok(st, x8, w_grad):
-            return None
-        return x8, sx, self._quantize_g8(st, g), self.gqs[i, 1:2]
+    def _bucket(self, t):
+        """Start a gradient bucket's all-reduce; the GEMMs behind it get the comm CU budget."""
+        self._cus = self._cus_comm
+        return self.ctx.all_reduce_async(t)
 
     def _dw_update(self, st: Stage, x_in, g) -> None:
         """dW GEMM + the weight's optimizer update in one launch (fuse_opt). The update writes the
@@ -1284,10 +1132,10 @@ class FusedTrainer:
                 PF.gemm(g8, True, self.w8n[st.seg_w.offset], True, dx,
                         aux=None if mask is not None else before.buffers["y"], colsum=colsum, mode=PF.EPI_BWD,
                         epi=(ei, ef), mask=mask, scale_a=self.gqs[k, 1:2], scale_b=self.wqs[st.w8_index, 1:2],
-                        **kw8)
+                        cus=self._cus, **kw8)
             else:
                 PF.gemm(g, True, self._w(st), True, dx, aux=None if mask is not None else before.buffers["y"],
-                        colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask, **kw8)
+                        colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask, cus=self._cus, **kw8)
             if kw8:
                 self._g8_done[b] = dx
             elif getattr(before, "g8_from_epi", False) and rec is None and self._ov is not None \
@@ -1299,7 +1147,7 @@ class FusedTrainer:
         colsum = None
         if no_epi_prev and before.seg_b is not None:
             colsum = self.store.view(before.seg_b, self.grads)
-        PF.gemm(g, True, self._w(st), True, dx, colsum=colsum, mode=PF.EPI_STORE)
+        PF.gemm(g, True, self._w(st), True, dx, colsum=colsum, mode=PF.EPI_STORE, cus=self._cus)
         if rec is not None:
             rec[("grad", before.layers[-1])] = dx[:batch * before.pos_out]
         if no_epi_prev or before.kind == "embed":
