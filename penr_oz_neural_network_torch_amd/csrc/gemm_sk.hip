@@ -103,22 +103,83 @@ PZ_DEV void sk_barrier() {
 // step's LDS-DMA and fragment reads into the gaps (hazard argument: gemm_mfma.hip gemm_body, BK 64
 // branch). Group 0 stages step t+1 in its read interval of step t; every wave waits for it
 // (vmcnt(0)) before the barrier that opens the next read interval.
+// One operand's LDS-DMA of a 64-deep step by the four staging waves (team index tw): piece i of
+// 8 per wave = 1 KiB at LDS byte tw * 8 KiB + i KiB of the operand image. The per-lane offsets
+// carry the read-side swizzle and depend on the piece only through (i & 1) (K-contiguous) or
+// (i & 1, i >> 2 & 1) (M/N-contiguous), so they are computed ONCE per kernel; everything that
+// moves with the unit or the K step is wave-uniform (soffset). (gemm_mfma.hip's stage_mn
+// recomputes row clamps and offsets per call: in the persistent kernel hipcc spilled them and
+// reloaded each from scratch behind an `s_waitcnt vmcnt(0)` that drained the ring.)
+struct PpOperand {
+  uint32_t voff[4];  // per-lane byte offsets by piece class
+  uint32_t base;     // uniform byte offset of this wave's piece 0 at the unit's first step
+  uint32_t pstep;    // bytes between consecutive pieces
+  uint32_t kstep;    // bytes per 64-deep K step
+};
+
+template <bool KC>
+PZ_DEV void pp_lane_offsets(uint32_t (&voff)[4], uint32_t ld, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int par = q & 1, hi = q >> 1;
+    int chunk;
+    uint32_t row;
+    if constexpr (KC) {  // 8 rows x 8 chunks of 16 B; swz_kc<64>(r) = (r >> 1) & 7
+      row = static_cast<uint32_t>(lane >> 3);
+      chunk = (lane & 7) ^ ((par * 4 + (lane >> 4)) & 7);
+      (void)hi;
+    } else {  // 2 k-rows x 32 chunks; swz_mn(kr) from kr & 3 and kr bit 3
+      row = static_cast<uint32_t>(lane >> 5);
+      chunk = (lane & 31) ^ ((((2 * par + (lane >> 5)) & 3) | (hi << 2)) << 1);
+    }
+    voff[q] = (row * ld + static_cast<uint32_t>(chunk) * 8u) * 2u;
+  }
+}
+
+template <bool KC>
+PZ_DEV PpOperand pp_operand(const uint32_t (&voff)[4], uint32_t ld, int row0, int kt0, int tw) {
+  PpOperand o;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) o.voff[q] = voff[q];
+  if constexpr (KC) {
+    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(row0 + tw * 64) * ld + static_cast<uint32_t>(kt0) * 64u) * 2u);
+    o.pstep = __builtin_amdgcn_readfirstlane(8u * ld * 2u);
+    o.kstep = 128u;
+  } else {
+    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(kt0 * 64 + tw * 16) * ld + static_cast<uint32_t>(row0)) * 2u);
+    o.pstep = __builtin_amdgcn_readfirstlane(2u * ld * 2u);
+    o.kstep = __builtin_amdgcn_readfirstlane(64u * ld * 2u);
+  }
+  return o;
+}
+
+template <bool KC>
+PZ_DEV void pp_dma(const PpOperand& o, i32x4_t rs, int kt, uint32_t lds) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = KC ? (i & 1) : ((i & 1) | (((i >> 2) & 1) << 1));
+    blds16<0>(rs, o.voff[q], o.base + static_cast<uint32_t>(i) * o.pstep + static_cast<uint32_t>(kt) * o.kstep,
+              lds + static_cast<uint32_t>(i) * 1024u);
+  }
+}
+
+// ------------------------------------------------------------------ W = 8: the ping-pong loop
+// Waves 0-3 (group 0) and 4-7 (group 1) share the four SIMDs and run one barrier interval apart:
+// while one wave of a SIMD issues its 64-MFMA block (setprio 1), its partner issues the next
+// step's LDS-DMA and fragment reads into the gaps (hazard argument: gemm_mfma.hip gemm_body, BK 64
+// branch). Group 0 stages step t+1 in its read interval of step t; every wave waits for it
+// (vmcnt(0)) before the barrier that opens the next read interval.
 template <bool A_KC, bool B_KC>
-PZ_DEV void pp_mainloop(f32x4_t (&acc)[8][4], PZ_LDS char* smem, const GemmArgs& p, i32x4_t rs_a, i32x4_t rs_b,
-                        int m0, int n0, int kt0, int nk, int wave, int lane) {
+PZ_DEV void pp_mainloop(f32x4_t (&acc)[8][4], PZ_LDS char* smem, const PpOperand& oa, const PpOperand& ob,
+                        i32x4_t rs_a, i32x4_t rs_b, int nk, int wave, int lane) {
   constexpr int BK = 64, A_BYTES = kSkB * BK * 2, SLOT = 2 * A_BYTES;
   const int grp = wave >> 2, tw = wave & 3;
   const int wm = wave >> 2, wn = wave & 3;
-  const uint16_t* __restrict__ A = static_cast<const uint16_t*>(p.A);
-  const uint16_t* __restrict__ B = static_cast<const uint16_t*>(p.B);
-  auto stage = [&](int kt, auto team, int tw_) __attribute__((always_inline)) {
-    constexpr int TEAM = decltype(team)::value;
-    PZ_LDS char* base = smem + (kt & 1) * SLOT;
-    const int k0 = (kt0 + kt) * BK;
-    if constexpr (A_KC) stage_kc<kSkB, TEAM, BK, true, 0, true>(A, p.lda, m0, p.M, k0, base, tw_, lane, rs_a);
-    else stage_mn<kSkB, TEAM, BK, true, 0>(A, p.lda, m0, p.M, k0, base, tw_, lane, rs_a);
-    if constexpr (B_KC) stage_kc<kSkB, TEAM, BK, true, 0, true>(B, p.ldb, n0, p.N, k0, base + A_BYTES, tw_, lane, rs_b);
-    else stage_mn<kSkB, TEAM, BK, true, 0>(B, p.ldb, n0, p.N, k0, base + A_BYTES, tw_, lane, rs_b);
+  const uint32_t lds0 = lds_addr(smem) + static_cast<uint32_t>(tw) * 8u * 1024u;
+  auto stage = [&](int kt) __attribute__((always_inline)) {
+    const uint32_t lds = lds0 + static_cast<uint32_t>(kt & 1) * SLOT;
+    pp_dma<A_KC>(oa, rs_a, kt, lds);
+    pp_dma<B_KC>(ob, rs_b, kt, lds + A_BYTES);
   };
   struct Frags { i16x8_t a[2][8]; i16x8_t b[2][4]; };
   auto read = [&](int slot, Frags& f) __attribute__((always_inline)) {
@@ -138,18 +199,16 @@ PZ_DEV void pp_mainloop(f32x4_t (&acc)[8][4], PZ_LDS char* smem, const GemmArgs&
       }
     }
   };
-  using T4 = std::integral_constant<int, 4>;
-  using T8 = std::integral_constant<int, 8>;
   // the previous unit's epilogue stores share the VM counter with the DMAs; and every wave is done
   // with the LDS image before slot 0 is refilled
   wait_vm<0>();
   sk_barrier();
-  stage(0, T8{}, wave);
+  if (grp == 0) stage(0);
   wait_vm<0>();
   sk_barrier();
   if (grp == 1) sk_barrier();
   for (int t = 0; t < nk; ++t) {
-    if (grp == 0 && t + 1 < nk) stage(t + 1, T4{}, tw);
+    if (grp == 0 && t + 1 < nk) stage(t + 1);
     Frags f;
     read(t & 1, f);
     if (grp == 1) wait_vm<0>();  // step t+1 (issued by group 0 one interval ago) landed
@@ -386,7 +445,17 @@ gemm_sk_kernel(const SkArgs g) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    if constexpr (W == 8) pp_mainloop<A_KC, B_KC>(acc, smem, p, buf_rsrc(p.A), buf_rsrc(p.B), m0, n0, kb, ke - kb, wave, lane);
+    if constexpr (W == 8) {
+      const int tw = wave & 3;
+      // (the staging lane offsets: recomputed per unit, ~20 VALU ops, rather than held live
+      // through the fold and the epilogue)
+      uint32_t va[4], vb[4];
+      pp_lane_offsets<A_KC>(va, static_cast<uint32_t>(p.lda), lane);
+      pp_lane_offsets<B_KC>(vb, static_cast<uint32_t>(p.ldb), lane);
+      const PpOperand oa = pp_operand<A_KC>(va, static_cast<uint32_t>(p.lda), m0, kb, tw);
+      const PpOperand ob = pp_operand<B_KC>(vb, static_cast<uint32_t>(p.ldb), n0, kb, tw);
+      pp_mainloop<A_KC, B_KC>(acc, smem, oa, ob, buf_rsrc(p.A), buf_rsrc(p.B), ke - kb, wave, lane);
+    }
     else w4_mainloop<A_KC, B_KC>(acc, smem, p, buf_rsrc(p.A), buf_rsrc(p.B), m0, n0, kb, ke - kb, wave, lane);
 
     if (slab >= 0) {

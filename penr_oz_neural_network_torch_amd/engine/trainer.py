@@ -330,7 +330,7 @@ class FusedTrainer(Fp8Policy):
             if cands:
                 self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
         self._pair_update = (self._pair_idx is not None and self.compute == torch.bfloat16 and not self.fp8
-                             and self.master == torch.float32)
+                             and self.master == torch.float32 and os.environ.get("PZ_PAIR_UPDATE", "1") == "1")
         self._w1_pending = None  # (pair_update fallback: the first layer's own update group)
         fused = gemm_w if (self.fuse_opt or self._pair_update) else gemm_w[1:]
         self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
@@ -344,7 +344,7 @@ class FusedTrainer(Fp8Policy):
         # persistent engine with the CUs the collective kernels leave (parallel/dist.py comm_cus)
         self._cus = 0
         self._cus_comm = 0
-        if self.ctx.enabled and self.ctx.comm_cus > 0 and self.dev.type == "cuda":
+        if self.ctx.enabled and self.ctx.comm_cus > 0:
             self._cus_comm = torch.cuda.get_device_properties(self.dev).multi_processor_count - self.ctx.comm_cus
         self._opt_done = None
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done

@@ -394,6 +394,19 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         activations = None
         every = max(1, epochs // MAX_PROGRESS_POINTS)
         last_saved = time.time()
+        # GPU models: the parameters live in one flat device buffer (ParamStore); autograd
+        # accumulates every gradient into views of one flat gradient buffer and the update is the
+        # fused optimizer kernel (csrc/optim.hip, the trainer's), not torch.optim's per-tensor ops —
+        # same math, and the torch.optim.Adam state stays the checkpointed object (its moments
+        # become views of the kernel's flat buffers)
+        fused, flat_grad, grad_views = None, None, None
+        if self._param_store is not None and self._param_store.device.type == "cuda":
+            from ..engine.optim import FusedOptimizer
+            store = self._param_store
+            fused = FusedOptimizer(store, self.params, self.optimizer, {})
+            flat_grad = torch.zeros_like(store.flat)
+            by_param = {seg.param_index: seg for seg in store.segments}
+            grad_views = [store.view(by_param[i], flat_grad) for i in range(len(self.params))]
         for epoch in range(epochs):
             if sampler is None:  # the reference's draw from the global RNG
                 picks = torch.randint(0, len(data), (sample_size,))
@@ -414,8 +427,13 @@ class NeuralNetworkModel(MultiLayerPerceptron):
             activations, cost = self._forward(inputs, target, dropout_rate)
             if l2_lambda > 0.0:
                 cost = cost + l2_lambda * sum((w ** 2).sum() for w in self.weights)
-            for p in self.params:
-                p.grad = None
+            if fused is not None:  # backward accumulates into the zeroed flat buffer's views
+                flat_grad.zero_()
+                for p, gv in zip(self.params, grad_views):
+                    p.grad = gv
+            else:
+                for p in self.params:
+                    p.grad = None
             long_training = time.time() - last_saved >= CHECKPOINT_INTERVAL_S
             if epoch + 1 == epochs or long_training:
                 for a in activations:
@@ -427,7 +445,10 @@ class NeuralNetworkModel(MultiLayerPerceptron):
                 self._average_gradients(ctx, 1.0)
             else:
                 cost.backward()
-            if self.optimizer is not None:
+            if fused is not None:  # (the L2 term is already in the autograd gradient)
+                fused.step(flat_grad, lr, 0.0, 1.0)
+                fused.sync_torch_state()
+            elif self.optimizer is not None:
                 self.optimizer.step()
             else:
                 for p in self.params:

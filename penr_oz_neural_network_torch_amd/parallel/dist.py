@@ -40,11 +40,13 @@ class DataParallelContext:
     # the comm-stream / wait ordering of the data-parallel step is exercised on a single GPU
     force: bool = False
     native: object = None  # _NativeComm: the extension's RCCL communicator (gradient buckets)
-    # CUs the gradient collectives hold while a bucket is on the wire (RCCL: one workgroup per
-    # channel, capped by NCCL_MAX_NCHANNELS; the comm proxy: its workgroups). The fused trainer runs
-    # the GEMMs that overlap a collective on the persistent engine with a grid that many CUs smaller
-    # (csrc/gemm_sk.hip): a full grid would leave that many workgroups waiting for the comm kernels
-    # to drain, a straggler round for the whole GEMM.
+    # PZ_COMM_BUDGET=k (default 0 = off): CUs to leave to the gradient collectives while a bucket is
+    # on the wire (RCCL holds one workgroup per channel). The fused trainer then runs the GEMMs that
+    # overlap a collective on the persistent stream-K engine with a grid k CUs smaller
+    # (csrc/gemm_sk.hip) instead of the tiled grid, whose last round waits for the held CUs. Off by
+    # default: measured on one GPU against the collective-footprint proxy (16 workgroups held for a
+    # modelled 8-rank ring), the stream-K grid's split-tile hand-offs cost more than the tiled
+    # kernels' straggler round (mlp4 1.606 vs 1.459 ms/step, profiles/r5_comm_pressure.txt).
     comm_cus: int = 0
 
     @property
@@ -212,10 +214,7 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
             backend = os.environ.get("PZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
-            # bound the CUs a bucket all-reduce takes (one workgroup per channel): 16 channels carry
-            # the mlp4 step's ~84 MB of ring traffic per GPU in ~0.3 ms at ~20 GB/s per channel,
-            # inside the backward they overlap; the GEMMs keep 240 of 256 CUs meanwhile
-            os.environ.setdefault("NCCL_MAX_NCHANNELS", "16")
+
             # failure detection: a rank that dies or a collective that hangs must abort the job
             # (RCCL async error handling + the collective watchdog timeout) instead of hanging the
             # node; the REST layer then persists status "Failed" 
@@ -231,8 +230,7 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
     comm_dtype = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp32": None, None: None}.get(comm)
     if dist.is_initialized():
         _CONTEXT = DataParallelContext(dist.get_rank(), dist.get_world_size(), None, comm_dtype, force=force)
-        if dist.get_backend() == "nccl":
-            _CONTEXT.comm_cus = int(os.environ.get("NCCL_MAX_NCHANNELS", "16"))
+        _CONTEXT.comm_cus = int(os.environ.get("PZ_COMM_BUDGET", "0"))
         # PZ_COMM=native: gradient buckets on the extension's own RCCL communicator instead of
         # ProcessGroupNCCL. Opt-in: with the same bucket schedule it measured 1.8% slower on the
         # forced 1-rank step (1.390-1.396 vs 1.366-1.373 ms, profiles/r2_ab_native_comm.txt), and
@@ -245,7 +243,6 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
                 raise RuntimeError("PZ_COMM=proxy models the collectives of a multi-GPU step on ONE GPU "
                                    "(PZ_FORCE_COMM=1, world size 1)")
             _CONTEXT.native = _ProxyComm()
-            _CONTEXT.comm_cus = int(os.environ.get("PZ_COMM_PROXY_WGS", "16"))
     else:
         _CONTEXT = DataParallelContext(0, 1, None, comm_dtype)
     return _CONTEXT

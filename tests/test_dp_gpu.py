@@ -134,8 +134,8 @@ def _forced_main(rank, comm, out_path, impl="native"):
     all-reduce on its comm stream, waited for by the optimizer's stream."""
     os.environ.update(PZ_FORCE_COMM="1", PZ_GRAD_COMM_DTYPE=comm, PZ_COMM=impl, MASTER_ADDR="127.0.0.1",
                       MASTER_PORT=str(_free_port()))
-    if impl == "proxy":
-        os.environ.update(PZ_COMM_CUS="16", PZ_COMM_PROXY_WGS="16")
+    if impl == "proxy":  # (the proxy's 16 workgroups, and the GEMMs behind a bucket on 240 CUs)
+        os.environ.update(PZ_COMM_PROXY_WGS="16", PZ_COMM_BUDGET="16")
     os.environ.pop("WORLD_SIZE", None)
     from penr_oz_neural_network_torch_amd.engine.trainer import FusedTrainer
     from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
@@ -148,6 +148,11 @@ def _forced_main(rank, comm, out_path, impl="native"):
     model = _build("adam", "bf16")
     tr = FusedTrainer(model, ctx)
     assert bool(tr.grads16) == (comm == "bf16")
+    # PZ_COMM_BUDGET: the backward GEMMs behind a bucket run on the persistent engine with the CUs
+    # the collective kernels leave
+    budget = 16 if impl == "proxy" else 0
+    assert ctx.comm_cus == budget
+    assert tr._cus_comm == (torch.cuda.get_device_properties(0).multi_processor_count - 16 if budget else 0)
     x, y, idx = _data()
     tr.load_tensors(x, y, seed=3)
     tr.begin(3)
@@ -176,9 +181,10 @@ def test_forced_rccl_world1_matches_no_comm(tmp_path, monkeypatch, comm, impl):
     costs = [c for _, c, _, _ in tr.drain()]
     flat = model._param_store.flat.cpu()
     if comm == "fp32":
-        # a 1-rank fp32 all-reduce is the identity; what remains is the run-to-run order of the
-        # bias-gradient column-sum atomics (fp32), which Adam turns into ~lr-sized flips only on
-        # near-zero gradients
+        # a 1-rank fp32 all-reduce is the identity; what remains is the schedule's summation order
+        # (the single process pairs the first layer's dW with its partner's and runs the tiled
+        # split-K engine; the DP step runs one dW per bucket on the budgeted stream-K engine),
+        # which Adam turns into ~lr-sized flips only on near-zero gradients
         for a, b in zip(got["costs"], costs):
             assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (got["costs"], costs)
         d = (got["flat"] - flat).abs()

@@ -370,17 +370,20 @@ def test_fused_dw_update_matches_separate_launches(monkeypatch, optimizer):
         assert (a is None) == (b is None)
         if a is not None:
             assert all(abs(x - y) < 1e-3 * abs(x) + 1e-7 for x, y in zip(a, b)), (a, b)
-    # both schedules sum split-K slices and bias column sums in arrival order, so two runs of the
-    # SAME schedule already differ at fp32 rounding level, which bf16 activation rounding and Adam's
-    # ~lr * sign(m) first steps amplify: fused vs separate must stay within that noise floor
+    # the schedules sum the dW tiles in different orders (split-K 4 beside the fused update, the
+    # paired launch's split-K 2 in the unfused schedule), which bf16 activation rounding and Adam's
+    # ~lr * sign(m) first steps amplify; two runs of the SAME schedule are bit-identical
+    # (PZ_DETERMINISTIC), so the bounds are absolute
     pn = runs["0b"][2]
+    assert torch.equal(p0, pn)
     d, dn = (p0 - p1).abs(), (p0 - pn).abs()
     mean, mean_n = d.mean().item(), dn.mean().item()
     frac, frac_n = (d > 1e-3).double().mean().item(), (dn > 1e-3).double().mean().item()
     assert mean <= 3 * mean_n + 2e-5 and frac <= 3 * frac_n + 1e-3, (mean, mean_n, frac, frac_n)
     if optimizer == "adam":
         assert mean < 1e-4, mean
-        assert (m0 - m1).abs().mean().item() <= 3 * (m0 - runs["0b"][4]).abs().mean().item() + 1e-8
+        assert torch.equal(m0, runs["0b"][4])
+        assert (m0 - m1).abs().mean().item() <= 1e-3 * m0.abs().mean().item()
         for k in s0["state"]:
             assert float(s0["state"][k]["step"]) == float(s1["state"][k]["step"]) == steps
     else:

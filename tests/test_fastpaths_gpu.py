@@ -417,3 +417,32 @@ def test_fp8_data_parallel_dw_matches_single_rank(tmp_path):
     assert rel < 0.15, rel
     for r in ranks:
         assert torch.equal(r["flat"], ranks[0]["flat"])
+
+
+@pytest.mark.parametrize("optimizer", ["adam", None])
+def test_gpu_autograd_fallback_updates_through_fused_optimizer(optimizer):
+    """A GPU model trained on the autograd path (models/network.py _autograd_epochs: the runtime of
+    layer stacks the fused engine does not compile) takes its update from the fused optimizer kernel
+    (csrc/optim.hip) over the flat parameter / gradient buffers: same trajectory as the reference's
+    CPU fp64 torch.optim.Adam / SGD loop on the same picks, and a torch.optim.Adam state_dict whose
+    moments and step counters match."""
+    sizes, algos = [16, 32, 8], ["relu", "softmax"]
+    g = torch.Generator().manual_seed(3)
+    data = [(torch.randn(16, generator=g).tolist(), [int(torch.randint(0, 8, (1,), generator=g))]) for _ in range(64)]
+    models = {}
+    for dev in ("cpu", "cuda"):
+        torch.manual_seed(0)
+        m = NeuralNetworkModel(f"fb_{dev}", sizes, "xavier", "random", algos, optimizer, device=dev)
+        torch.manual_seed(7)  # the reference's global-RNG picks
+        m._train_autograd(data, epochs=5, learning_rate=0.01, sample_size=16, decay_rate=0.9, dropout_rate=0.0,
+                          l2_lambda=0.001)
+        models[dev] = m
+    cpu, gpu = models["cpu"], models["cuda"]
+    for pc, pg in zip(cpu.params, gpu.params):
+        torch.testing.assert_close(pg.detach().cpu(), pc.detach(), rtol=1e-9, atol=1e-12)
+    if optimizer is not None:
+        sc, sg = cpu.optimizer.state_dict()["state"], gpu.optimizer.state_dict()["state"]
+        for k in sc:
+            assert float(sg[k]["step"]) == float(sc[k]["step"]) == 5
+            torch.testing.assert_close(sg[k]["exp_avg"].cpu(), sc[k]["exp_avg"], rtol=1e-9, atol=1e-14)
+            torch.testing.assert_close(sg[k]["exp_avg_sq"].cpu(), sc[k]["exp_avg_sq"], rtol=1e-9, atol=1e-16)

@@ -7,11 +7,13 @@ ms/step, interleaved over rounds (same box):
   torch         PZ_FORCE_COMM=1: a real 1-rank RCCL all-reduce per bucket via ProcessGroupNCCL
   native        PZ_FORCE_COMM=1 PZ_COMM=native: the extension's own RCCL communicator
   dpnone        PZ_FORCE_COMM=1 PZ_COMM=proxy with a zero-duration proxy: the DP schedule alone
-  proxy_k<K>    PZ_COMM=proxy: the collective-footprint kernel (csrc/comm_proxy.hip) holds
-                16 channel workgroups for a modelled 8-rank ring all-reduce of every bucket
-                at 150 GB/s, its stream CU-masked to K CUs (K=0: unmasked)
+  proxy_w<W>    PZ_COMM=proxy: the collective-footprint kernel (csrc/comm_proxy.hip) holds W
+                channel workgroups for a modelled 8-rank ring all-reduce of every bucket at
+                150 GB/s (the default schedule: full-grid tiled GEMMs)
+  proxy_w<W>_sk the same with PZ_COMM_BUDGET=W: the backward GEMMs behind a bucket on the
+                persistent stream-K engine with 256 - W CUs (parallel/dist.py comm_cus)
 
-    python tools/comm_pressure.py [--rounds 2] [--steps 60] [--ks 0,8,16,32]
+    python tools/comm_pressure.py [--rounds 2] [--steps 60] [--wgs 16,32]
 """
 import argparse
 import json
@@ -37,15 +39,16 @@ def main():
     ap.add_argument("--rounds", type=int, default=2)
     ap.add_argument("--steps", type=int, default=60)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--ks", default="0,8,16,32")
+    ap.add_argument("--wgs", default="16,32")
     ap.add_argument("--gbps", default="150")
     a = ap.parse_args()
     forced = {"PZ_FORCE_COMM": "1"}
     cases = {"none": {}, "torch": dict(forced, PZ_COMM="torch"), "native": dict(forced, PZ_COMM="native"),
              "dpnone": dict(forced, PZ_COMM="proxy", PZ_COMM_PROXY_GBPS="1e12")}
-    for k in [int(x) for x in a.ks.split(",")]:
-        cases[f"proxy_k{k}"] = dict(forced, PZ_COMM="proxy", PZ_COMM_CUS=str(k),
-                                    PZ_COMM_PROXY_WGS=str(k if k else 16), PZ_COMM_PROXY_GBPS=a.gbps)
+    for w in [int(x) for x in a.wgs.split(",")]:
+        proxy = dict(forced, PZ_COMM="proxy", PZ_COMM_PROXY_WGS=str(w), PZ_COMM_PROXY_GBPS=a.gbps)
+        cases[f"proxy_w{w}"] = proxy
+        cases[f"proxy_w{w}_sk"] = dict(proxy, PZ_COMM_BUDGET=str(w))
     res = {name: [] for name in cases}
     for r in range(a.rounds):
         for name, env in cases.items():

@@ -27,15 +27,20 @@ def timeit(fn, n=30, w=5):
 def main():
     dev = "cuda"
     B = 8192
-    cases = [  # name, M, N, K, a_kc, b_kc, out dtype, mode
-        ("fwd_L1", B, 4096, 1024, True, False, torch.bfloat16, "fwd"),
-        ("fwd_L2", B, 4096, 4096, True, False, torch.bfloat16, "fwd"),
+    cases = [  # name, M, N, K, a_kc, b_kc, out dtype, mode — the default rows are the mlp4 step's
+        # GEMMs with the epilogue kinds the trainer runs: forward stages writing the ReLU bitmask,
+        # dX reading it (+ bias-gradient column sums), dW straight into the bf16 gradient buffer
+        ("fwd_L1", B, 4096, 1024, True, False, torch.bfloat16, "fwd_mask"),
+        ("fwd_L2", B, 4096, 4096, True, False, torch.bfloat16, "fwd_mask"),
         ("fwd_L3", B, 1024, 4096, True, False, torch.bfloat16, "fwd_nodrop"),
-        ("dX_L3", B, 4096, 1024, True, True, torch.bfloat16, "bwd"),
-        ("dX_L2", B, 4096, 4096, True, True, torch.bfloat16, "bwd"),
-        ("dW_L3", 4096, 1024, B, False, False, torch.float32, "store"),
-        ("dW_L2", 4096, 4096, B, False, False, torch.float32, "store"),
-        ("dW_L1", 1024, 4096, B, False, False, torch.float32, "store"),
+        ("dX_L3", B, 4096, 1024, True, True, torch.bfloat16, "bwd_mask"),
+        ("dX_L2", B, 4096, 4096, True, True, torch.bfloat16, "bwd_mask"),
+        ("dW_L3", 4096, 1024, B, False, False, torch.bfloat16, "store"),
+        ("dW_L2", 4096, 4096, B, False, False, torch.bfloat16, "store"),
+        ("dW_L1", 1024, 4096, B, False, False, torch.bfloat16, "store"),
+        # the previous rows' generic kinds: aux-derivative dX, fp32 weight gradients
+        ("dX_L2_aux", B, 4096, 4096, True, True, torch.bfloat16, "bwd"),
+        ("dW_L2_f32", 4096, 4096, B, False, False, torch.float32, "store"),
         # epilogue probes (only run when named): fwd_L2 with parts of the stage math
         ("fwdL2_bias", B, 4096, 4096, True, False, torch.bfloat16, "fwd_bias"),
         ("fwdL2_relu", B, 4096, 4096, True, False, torch.bfloat16, "fwd_relu"),
