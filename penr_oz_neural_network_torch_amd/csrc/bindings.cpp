@@ -419,37 +419,6 @@ void gemm_pair_op(const Tensor& A0, const Tensor& B0, const Tensor& C0, const Te
   launch_pair(a, b, A0);
 }
 
-// two weight-gradient GEMMs (M/N-contiguous operands, one K) in ONE launch, each with its weight's
-// optimizer update fused into the epilogue (EPI_OPT): the first layer's and its partner's dW at
-// the end of the backward, so no update launch is left between this step and the next. Per
-// weight: grad view (layout only), params, moments, shadow, stats; shared hyper-parameters.
-void gemm_pair_update_op(const Tensor& A0, const Tensor& B0, const Tensor& G0, const Tensor& P0,
-                         const optional<Tensor>& m0, const optional<Tensor>& v0, const optional<Tensor>& sh0,
-                         const optional<Tensor>& st0, const Tensor& A1, const Tensor& B1, const Tensor& G1,
-                         const Tensor& P1, const optional<Tensor>& m1, const optional<Tensor>& v1,
-                         const optional<Tensor>& sh1, const optional<Tensor>& st1, bool adam, double lr, double beta1,
-                         double beta2, double eps, double bias_c1, double bias_c2_sqrt, double grad_scale, double l2,
-                         const optional<Tensor>& hp, const optional<Tensor>& epoch, int64_t stats_every) {
-  const int64_t K = A0.size(0);
-  auto a = update_args(A0, false, B0, false, G0, G0.size(0), G0.size(1), K, 1.0, P0, m0, v0, sh0, st0, c10::nullopt, adam,
-                       lr, beta1, beta2, eps, bias_c1, bias_c2_sqrt, grad_scale, l2, hp, epoch, stats_every);
-  auto b = update_args(A1, false, B1, false, G1, G1.size(0), G1.size(1), K, 1.0, P1, m1, v1, sh1, st1, c10::nullopt, adam,
-                       lr, beta1, beta2, eps, bias_c1, bias_c2_sqrt, grad_scale, l2, hp, epoch, stats_every);
-  launch_pair(a, b, A0);
-}
-
-int64_t gemm_pair_update_ok_op(const Tensor& A0, const Tensor& B0, const Tensor& G0, const Tensor& A1, const Tensor& B1,
-                               const Tensor& G1) {
-  if (A0.size(0) != A1.size(0) || G0.scalar_type() != at::kFloat || G1.scalar_type() != at::kFloat) return 0;
-  auto a = gemm_args(A0, false, B0, false, G0, c10::nullopt, c10::nullopt, c10::nullopt, pz::EPI_OPT, {}, {}, 1.0, false,
-                     G0.size(0), G0.size(1), A0.size(0), 0, false);
-  auto b = gemm_args(A1, false, B1, false, G1, c10::nullopt, c10::nullopt, c10::nullopt, pz::EPI_OPT, {}, {}, 1.0, false,
-                     G1.size(0), G1.size(1), A1.size(0), 0, false);
-  a.opt.params = G0.data_ptr<float>();  // (eligibility only: 16-B aligned state views of the same layout)
-  b.opt.params = G1.data_ptr<float>();
-  return pz::gemm_pair_split(a, b);
-}
-
 int64_t gemm_path_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tensor& C, int64_t M, int64_t N,
                      int64_t K) {
   auto p = gemm_args(A, a_kc, B, b_kc, C, c10::nullopt, c10::nullopt, c10::nullopt, 0, {}, {}, 1.0, false, M, N, K, 0,
@@ -1026,12 +995,6 @@ TORCH_LIBRARY(pz, m) {
         "Tensor(a!) params, Tensor(b!)? exp_avg, Tensor(c!)? exp_avg_sq, Tensor(d!)? shadow, Tensor(e!)? stats, "
         "Tensor(f!)? amax, bool adam, float lr, float beta1, float beta2, float eps, float bias_c1, "
         "float bias_c2_sqrt, float grad_scale, float l2, Tensor? hp=None, Tensor? epoch=None, int stats_every=1) -> ()");
-  m.def("gemm_pair_update(Tensor A0, Tensor B0, Tensor G0, Tensor(a!) P0, Tensor(b!)? m0, Tensor(c!)? v0, "
-        "Tensor(d!)? sh0, Tensor(e!)? st0, Tensor A1, Tensor B1, Tensor G1, Tensor(f!) P1, Tensor(g!)? m1, "
-        "Tensor(h!)? v1, Tensor(i!)? sh1, Tensor(j!)? st1, bool adam, float lr, float beta1, float beta2, float eps, "
-        "float bias_c1, float bias_c2_sqrt, float grad_scale, float l2, Tensor? hp=None, Tensor? epoch=None, "
-        "int stats_every=1) -> ()");
-  m.def("gemm_pair_update_ok(Tensor A0, Tensor B0, Tensor G0, Tensor A1, Tensor B1, Tensor G1) -> int");
   m.def("gemm_path(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor C, int M, int N, int K) -> int");
   m.def("gemm_pair_split(Tensor A0, Tensor B0, Tensor C0, Tensor A1, Tensor B1, Tensor C1, int M0, int N0, int M1, "
         "int N1, int K) -> int");
@@ -1096,8 +1059,7 @@ TORCH_LIBRARY_IMPL(pz, CUDA, m) {
   m.impl("stage_fwd", TORCH_FN(stage_fwd_op));
   m.impl("stage_bwd", TORCH_FN(stage_bwd_op));
   m.impl("xent_head", TORCH_FN(xent_head_op));
-  m.impl("gemm_pair_update", TORCH_FN(gemm_pair_update_op));
-  m.impl("gemm_pair_update_ok", TORCH_FN(gemm_pair_update_ok_op));
+
   m.impl("mse_head", TORCH_FN(mse_head_op));
   m.impl("softmax_rows", TORCH_FN(softmax_rows_op));
   m.impl("softmax_bwd", TORCH_FN(softmax_bwd_op));

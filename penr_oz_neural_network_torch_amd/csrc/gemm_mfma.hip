@@ -581,9 +581,8 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
   // whose add returned split-1 sums the other slabs with `sc1` loads (after a barrier its waves
   // join) and runs the epilogue. No release fence (its L2 write-back of every dirty line of the
   // XCD cost ~2.7x the publish, measured 19-23 us of a split-K GEMM's 85-95 us) and no acquire.
-  // VAR 32 (lab A/B) keeps the plain-store + release/acquire form.
-  constexpr bool WT_SLABS = VAR != 32;
-  if (split > 1 && WT_SLABS) {
+  // (measured, not kept: plain stores + agent release / acquire fences, VAR 32)
+  if (split > 1) {
     constexpr int CH = ACC32 ? TM8 * TN8 * 4 : C::TM * C::TN;  // f32x4 chunks per lane
     const int tid = threadIdx.x;
     auto get_chunk = [&](auto cc) -> f32x4_t {
@@ -595,15 +594,7 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
         return acc[c / C::TN][c % C::TN];
       }
     };
-    auto add_chunk = [&](auto cc, f32x4_t v) {
-      constexpr int c = decltype(cc)::value;
-      if constexpr (ACC32) {
-        constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
-        acc[i][j][q] += v[0]; acc[i][j][q + 1] += v[1]; acc[i][j][q + 2] += v[2]; acc[i][j][q + 3] += v[3];
-      } else {
-        acc[c / C::TN][c % C::TN] += v;
-      }
-    };
+    static_assert(CH % 8 == 0, "the fold runs 8 chunks at a time");
     constexpr int kSlabBytes = BM * BN * 4;
     // one descriptor per tile's slab group (split x 256 KiB: 32-bit offsets always suffice)
     const auto rs = __builtin_amdgcn_make_buffer_rsrc(p.ws + static_cast<int64_t>(tile_id) * split * (BM * BN), 0,
@@ -624,12 +615,20 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
     }
     __syncthreads();
     if (*flag == 0) return;  // block-uniform: another slice finishes this tile
-    // the sum order must not depend on which slice arrived last (deterministic results): two
-    // slices = own + other (addition commutes); more = every slab in slice order, own included
-    if (split > 2) {
-      static_for<CH>([&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        const f32x4_t v = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, (c * C::NT + tid) * 16, 0, kSc1));
+    // The sum order must not depend on which slice arrived last (deterministic results): a fixed
+    // pairwise tree ((s0 + s1) + (s2 + s3)) + ((s4 + s5) + (s6 + s7)) whose leaf pairs and subtree
+    // pairs are each added in either order — float addition commutes exactly — so the last
+    // arriver starts from its own slice in registers and loads only the split - 1 others.
+    auto ld = [&](int sl, int c) {
+      return __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, sl * kSlabBytes + (c * C::NT + tid) * 16, 0, kSc1));
+    };
+    const int mate = slice ^ 1, pair2 = (slice ^ 2) & ~1, quad4 = (slice ^ 4) & ~3;
+    static_for<CH / 8>([&](auto gc) {  // 8 chunks at a time: bounded temporaries
+      static_for<8>([&](auto qc) {
+        constexpr int c = 8 * decltype(gc)::value + decltype(qc)::value;
+        f32x4_t v = get_chunk(std::integral_constant<int, c>{}) + ld(mate, c);
+        if (split >= 4) v = v + (ld(pair2, c) + ld(pair2 + 1, c));
+        if (split >= 8) v = v + ((ld(quad4, c) + ld(quad4 + 1, c)) + (ld(quad4 + 2, c) + ld(quad4 + 3, c)));
         if constexpr (ACC32) {
           constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
           acc[i][j][q] = v[0]; acc[i][j][q + 1] = v[1]; acc[i][j][q + 2] = v[2]; acc[i][j][q + 3] = v[3];
@@ -637,61 +636,8 @@ PZ_DEV void gemm_body(const GemmArgs& p, int wgid) {
           acc[c / C::TN][c % C::TN] = v;
         }
       });
-    }
-    for (int sl = split > 2 ? 1 : 0; sl < split; ++sl) {
-      if (split <= 2 && sl == slice) continue;
-      static_for<CH>([&](auto cc) {
-        constexpr int c = decltype(cc)::value;
-        add_chunk(cc, __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       rs, sl * kSlabBytes + (c * C::NT + tid) * 16, 0, kSc1)));
-      });
-    }
-  }
-  if (split > 1 && !WT_SLABS) {
-    constexpr int CH = ACC32 ? TM8 * TN8 * 4 : C::TM * C::TN;  // f32x4 chunks per lane
-    const int tid = threadIdx.x;
-    auto get_chunk = [&](auto cc) -> f32x4_t {
-      constexpr int c = decltype(cc)::value;
-      if constexpr (ACC32) {
-        constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
-        return f32x4_t{acc[i][j][q], acc[i][j][q + 1], acc[i][j][q + 2], acc[i][j][q + 3]};
-      } else {
-        return acc[c / C::TN][c % C::TN];
-      }
-    };
-    auto add_chunk = [&](auto cc, f32x4_t v) {
-      constexpr int c = decltype(cc)::value;
-      if constexpr (ACC32) {
-        constexpr int i = (c / 4) / TN8, j = (c / 4) % TN8, q = 4 * (c % 4);
-        acc[i][j][q] += v[0]; acc[i][j][q + 1] += v[1]; acc[i][j][q + 2] += v[2]; acc[i][j][q + 3] += v[3];
-      } else {
-        acc[c / C::TN][c % C::TN] += v;
-      }
-    };
-    f32x4_t* mine = reinterpret_cast<f32x4_t*>(p.ws + static_cast<int64_t>(tile_id * split + slice) * (BM * BN));
-    static_for<CH>([&](auto cc) { mine[decltype(cc)::value * C::NT + tid] = get_chunk(cc); });
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    PZ_LDS int* flag = (PZ_LDS int*)(smem);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const int prev = __hip_atomic_fetch_add(p.counters + tile_id, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = prev == split - 1;
-    }
-    __syncthreads();
-    if (*flag == 0) return;  // block-uniform: another slice finishes this tile
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      p.counters[tile_id] = 0;  // ready for the next launch
-    }
-    __syncthreads();
-    for (int sl = 0; sl < split; ++sl) {
-      if (sl == slice) continue;
-      const f32x4_t* other = reinterpret_cast<const f32x4_t*>(p.ws + static_cast<int64_t>(tile_id * split + sl) * (BM * BN));
-      static_for<CH>([&](auto cc) { add_chunk(cc, other[decltype(cc)::value * C::NT + tid]); });
-    }
+      __builtin_amdgcn_sched_barrier(0);
+    });
   }
 
   // ---------------------------------------------------------------- epilogue
@@ -1067,15 +1013,14 @@ int store_wt_default() {
 int gemm_pair_split(const GemmArgs& a, const GemmArgs& b) {
   for (const GemmArgs* q : {&a, &b}) {
     const GemmArgs& p = *q;
-    if (p.a_kc || p.b_kc || (p.epi_mode != EPI_STORE && p.epi_mode != EPI_OPT) || p.accumulate || p.force_generic)
-      return 0;
+    if (p.a_kc || p.b_kc || p.epi_mode != EPI_STORE || p.accumulate || p.force_generic) return 0;
     if (p.bias || p.colsum || p.mask || p.out8 || p.aux || p.bias64 || p.colsum64) return 0;
     if (p.M % 256 || p.N % 256 || p.K % 64 || !mfma_eligible(p)) return 0;
     if (p.in_dtype != DT_FP8 && (!buffer_ok(p) || epi_kind(p) != (p.out_dtype == DT_BF16 ? EK_STORE : EK_ANY)))
       return 0;
   }
   if (a.K != b.K || a.in_dtype != b.in_dtype || a.out_dtype != b.out_dtype || a.a_fmt != b.a_fmt ||
-      a.b_fmt != b.b_fmt || a.epi_mode != b.epi_mode)
+      a.b_fmt != b.b_fmt)
     return 0;
   if (a.in_dtype == DT_FP8 && a.out_dtype != DT_BF16) return 0;
   const int tiles = (a.M / 256) * (a.N / 256) + (b.M / 256) * (b.N / 256);

@@ -210,27 +210,6 @@ class FusedOptimizer:
                                  self.amax_sets[parity].get(seg.offset), self.adam, lr, b1, b2, eps, bc1, bc2s,
                                  grad_scale, l2, hp, ctr, every)
 
-    def _update_views(self, seg, parity: int):
-        slot = self.slot_of.get(id(seg))
-        stats = self.stats[self.cur][4 * slot:4 * slot + 4] if slot is not None else None
-        view = self.store.view
-        return (view(seg), view(seg, self.exp_avg) if self.adam else None,
-                view(seg, self.exp_avg_sq) if self.adam else None, self.shadow_sets[parity].get(seg.offset), stats)
-
-    def gemm_pair_update(self, a0, b0, seg0, a1, b1, seg1, l2: float, grad_scale: float, parity: int = 0) -> None:
-        """The weight-gradient GEMMs ``a_iᵀ @ b_i`` of two segments in ONE launch, each with its
-        weight's update fused into the epilogue (``pz::gemm_pair_update``): the first layer's and
-        its partner's dW at the end of the backward leave no update launch at the step boundary."""
-        lr, b1_, b2, eps, bc1, bc2s = self._hp
-        hp, ctr = self.graph_tables or (None, None)
-        every = self.stats_every
-        if every > 1 and ctr is None:
-            every = 1
-        w0, m0, v0, sh0, st0 = self._update_views(seg0, parity)
-        w1, m1, v1, sh1, st1 = self._update_views(seg1, parity)
-        torch.ops.pz.gemm_pair_update(a0, b0, w0, w0, m0, v0, sh0, st0, a1, b1, w1, w1, m1, v1, sh1, st1, self.adam,
-                                      lr, b1_, b2, eps, bc1, bc2s, grad_scale, l2, hp, ctr, every)
-
     def begin_step(self, lr: float) -> None:
         if self.adam:
             group = self.torch_opt.param_groups[0]

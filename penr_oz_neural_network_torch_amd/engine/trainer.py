@@ -319,22 +319,22 @@ class FusedTrainer(Fp8Policy):
         # with the fewest output tiles is deferred to the end of the backward and launched
         # TOGETHER with the first layer's (pz::gemm_pair): two skinny GEMMs that alone each need a
         # 4-way split-K to fill the CUs (mlp4: 64 tiles each) share one launch with a 2-way split
-        # (mlp8192: none) — half the slab hand-offs, one launch and one ramp fewer. bf16 policy:
-        # both weights' updates run in that launch's epilogue (pz::gemm_pair_update), so no update
-        # launch sits between the last dW and the next step's first GEMM; otherwise the partner's
-        # update joins the side stream behind the pair. PZ_DW_PAIR=0: one launch per dW.
+        # (mlp8192: none) — half the slab hand-offs, one launch and one ramp fewer. Its update
+        # then joins the side stream right behind the pair. PZ_DW_PAIR=0: one launch per dW.
+        # (measured, not kept: both weights' updates in that launch's epilogue, EPI_OPT — the pair
+        # ran 289 vs 119 us beside the side-stream update, mlp4 1.204 vs 1.111 ms, r5 same box)
+        # Data parallel too: the partner's bucket then leaves with the first layer's at the end of
+        # the backward (mlp4: 8 MB of bf16, ~14 MB of ring traffic per GPU at 8 ranks, ~50 us on
+        # xGMI) while the pair saves ~60 us of GEMM time against two split-4 launches
+        # (profiles/r5_step_timeline_dpnone.txt: 91 + 101 us vs 130 us paired).
         self._pair_idx = None
-        if (os.environ.get("PZ_DW_PAIR", "1") == "1" and not self.ctx.enabled and not self.fuse_opt
+        if (os.environ.get("PZ_DW_PAIR", "1") == "1" and not self.fuse_opt
                 and self.overlap and self.stages[0].kind == "gemm"):
             cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
             if cands:
                 self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
-        self._pair_update = (self._pair_idx is not None and self.compute == torch.bfloat16 and not self.fp8
-                             and self.master == torch.float32 and os.environ.get("PZ_PAIR_UPDATE", "1") == "1")
-        self._w1_pending = None  # (pair_update fallback: the first layer's own update group)
-        fused = gemm_w if (self.fuse_opt or self._pair_update) else gemm_w[1:]
         self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
-        self.opt.define_groups(fused)
+        self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
         # the side-stream updates of all layers but the first are queued together behind the last
         # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
@@ -782,9 +782,6 @@ class FusedTrainer(Fp8Policy):
             self._side_pending = []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
-            if self._w1_pending is not None:
-                self.opt.step_group(self._w1_pending, self.grads, l2, 1.0, 1 - self.parity)
-                self._w1_pending = None
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
             if self.fp8:
                 for st in self._late_stages:
@@ -1051,12 +1048,6 @@ class FusedTrainer(Fp8Policy):
         f8_p = self._fp8_dw(sp, gp, wp)
         ops0 = (f8_0[0], f8_0[2]) if f8_0 is not None else (x0, g0)
         opsp = (f8_p[0], f8_p[2]) if f8_p is not None else (xp, gp)
-        if self._pair_update and f8_0 is None and f8_p is None and self._pair_update_ok(x0, g0, st0, xp, gp, sp):
-            _, l2, scale = self._ov
-            self.opt.gemm_pair_update(x0, g0, st0.seg_w, xp, gp, sp.seg_w, l2, scale, 1 - self.parity)
-            return None  # (both weights updated: no bucket, no side-stream update)
-        if self._pair_update:  # not eligible here: the first layer's update runs as its own group
-            self._w1_pending = st0.seg_w.offset
         key = ("pair", (f8_0 is None), (f8_p is None), ops0[0].shape, ops0[1].shape, opsp[0].shape, opsp[1].shape)
         ok = self._y_dead_cache.get(key)
         if ok is None:
@@ -1076,14 +1067,6 @@ class FusedTrainer(Fp8Policy):
         handles.append(hp)
         self._side_pending.append((sp.seg_w.offset, [hp], [sp]))
         return self._bucket(w0)
-
-    def _pair_update_ok(self, x0, g0, st0, xp, gp, sp) -> bool:
-        key = ("pair_upd", x0.shape, g0.shape, xp.shape, gp.shape)
-        ok = self._y_dead_cache.get(key)
-        if ok is None:
-            ok = self._y_dead_cache[key] = torch.ops.pz.gemm_pair_update_ok(
-                x0, g0, self.store.view(st0.seg_w), xp, gp, self.store.view(sp.seg_w)) > 0
-        return ok
 
     def _bucket(self, t):
         """Start a gradient bucket's all-reduce; the GEMMs behind it get the comm CU budget."""
