@@ -412,10 +412,27 @@ void launch_pair(pz::GemmArgs& a, pz::GemmArgs& b, const Tensor& A0) {
 void gemm_pair_op(const Tensor& A0, const Tensor& B0, const Tensor& C0, const Tensor& A1, const Tensor& B1,
                   const Tensor& C1, int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K,
                   const optional<Tensor>& scale_a0, const optional<Tensor>& scale_b0,
-                  const optional<Tensor>& scale_a1, const optional<Tensor>& scale_b1) {
+                  const optional<Tensor>& scale_a1, const optional<Tensor>& scale_b1, int64_t flags) {
   check_dev(A0, "A0");
   auto a = pair_args(A0, B0, C0, M0, N0, K, scale_a0, scale_b0);
   auto b = pair_args(A1, B1, C1, M1, N1, K, scale_a1, scale_b1);
+  // flags as pz::gemm's: bits 2-3 engine (2 / 3: the two problems as ONE persistent stream-K
+  // schedule), bits 16-31 its CU budget
+  a.engine = b.engine = static_cast<int>((flags >> 2) & 3);
+  a.cus = b.cus = static_cast<int>((flags >> 16) & 0xFFFF);
+  if (a.engine >= 2) {
+    TORCH_CHECK(pz::sk_eligible(a) && pz::sk_eligible(b), "pz::gemm_pair: the stream-K engine cannot run this pair");
+    pz::GemmArgs probs[2] = {a, b};
+    const int64_t sk_floats = pz::sk_ws_floats(probs, 2);
+    at::Tensor ws;
+    int* tickets = nullptr;
+    if (sk_floats > 0) {
+      ws = at::empty({sk_floats}, A0.options().dtype(at::kFloat));
+      tickets = split_counters(pz::sk_tickets(probs, 2), A0.device());
+    }
+    PZ_HIP_CHECK(pz::gemm_sk(probs, 2, sk_floats > 0 ? ws.data_ptr<float>() : nullptr, tickets, cur_stream(A0)));
+    return;
+  }
   launch_pair(a, b, A0);
 }
 
@@ -1000,7 +1017,7 @@ TORCH_LIBRARY(pz, m) {
         "int N1, int K) -> int");
   m.def("gemm_pair(Tensor A0, Tensor B0, Tensor(a!) C0, Tensor A1, Tensor B1, Tensor(b!) C1, int M0, int N0, int M1, "
         "int N1, int K, Tensor? scale_a0=None, Tensor? scale_b0=None, Tensor? scale_a1=None, "
-        "Tensor? scale_b1=None) -> ()");
+        "Tensor? scale_b1=None, int flags=0) -> ()");
   m.def("stage_fwd(Tensor x, Tensor(a!) y, int[] epi_i, float[] epi_f) -> ()");
   m.def("stage_bwd(Tensor g, Tensor y, Tensor(a!) dx, int[] epi_i, float[] epi_f) -> ()");
   m.def("xent_head(Tensor logits, Tensor labels, int rows_valid, Tensor(a!)? loss, float loss_scale, Tensor(b!)? dh, "

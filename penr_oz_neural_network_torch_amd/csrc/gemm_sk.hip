@@ -45,6 +45,26 @@ namespace {
 #include "gemm_common.h"
 #include "gemm_epilogue.h"
 
+// tools/sk_stamps.hip (diagnostic build only): s_memrealtime stamps per workgroup and unit at
+// unit start / main loop done / slab handed off / fold done / epilogue done, plus the unit's tile
+// and K range, into g.p[0].dbg ([grid][kSkStampUnits][8] u64)
+constexpr int kSkStampUnits = 6;
+#ifdef PZ_GEMM_STAMPS
+#define PZ_SK_STAMP(u, i)                                                                            \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && (u) < kSkStampUnits)                                                     \
+      g.p[0].dbg[(static_cast<int64_t>(w) * kSkStampUnits + (u)) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define PZ_SK_NOTE(u, v)                                                                             \
+  do {                                                                                               \
+    if (threadIdx.x == 0 && (u) < kSkStampUnits)                                                     \
+      g.p[0].dbg[(static_cast<int64_t>(w) * kSkStampUnits + (u)) * 8 + 7] = (v);                     \
+  } while (0)
+#else
+#define PZ_SK_STAMP(u, i) do {} while (0)
+#define PZ_SK_NOTE(u, v) do {} while (0)
+#endif
+
 constexpr int kSkB = 256;                    // macro tile BM = BN
 constexpr int kSkSlab = kSkB * kSkB;         // fp32 floats of one partial tile
 constexpr int kSkF32 = 100;                  // epilogue code of the fp32-output store path
@@ -409,6 +429,8 @@ gemm_sk_kernel(const SkArgs g) {
   const long long s0 = s.sk_iters > 0 ? sk_start(s, w) : 0, s1 = s.sk_iters > 0 ? sk_start(s, w + 1) : 0;
   long long it = s0;
   int dp_t = s.sk_tiles + w;
+  int unit = 0;  // (diagnostic stamps only)
+  (void)unit;
   for (;;) {
     // this unit: K steps [kb, ke) of tile t; slab >= 0: a stream-K partial tile
     int t, kb, ke, slab;
@@ -434,6 +456,9 @@ gemm_sk_kernel(const SkArgs g) {
     kb = __builtin_amdgcn_readfirstlane(kb);
     ke = __builtin_amdgcn_readfirstlane(ke);
     slab = __builtin_amdgcn_readfirstlane(slab);
+    PZ_SK_STAMP(unit, 0);
+    PZ_SK_NOTE(unit, (static_cast<uint64_t>(t) << 40) | (static_cast<uint64_t>(kb) << 20) | static_cast<uint64_t>(ke) |
+                         (slab >= 0 ? (uint64_t(1) << 63) : 0));
     const int prob = (s.nprob > 1 && t >= s.tiles0) ? 1 : 0;
     const GemmArgs& p = g.p[prob];
     const int tl = t - prob * s.tiles0;
@@ -458,6 +483,7 @@ gemm_sk_kernel(const SkArgs g) {
     }
     else w4_mainloop<A_KC, B_KC>(acc, smem, p, buf_rsrc(p.A), buf_rsrc(p.B), m0, n0, kb, ke - kb, wave, lane);
 
+    PZ_SK_STAMP(unit, 1);
     if (slab >= 0) {
       // ---- stream-K hand-off (write-through slabs, one ticket per contributor: MI355X_MICROARCH
       // hand-off table, row 1)
@@ -482,7 +508,11 @@ gemm_sk_kernel(const SkArgs g) {
         if (last) g.counters[t] = 0;  // ready for the next launch
       }
       __syncthreads();
-      if (__builtin_amdgcn_readfirstlane(*flag) == 0) continue;  // (uniform) another contributor finishes it
+      PZ_SK_STAMP(unit, 2);
+      if (__builtin_amdgcn_readfirstlane(*flag) == 0) {  // (uniform) another contributor finishes it
+        ++unit;
+        continue;
+      }
       auto slab_of = [&](int c) { return __builtin_amdgcn_readfirstlane(2 * c + (sk_start(s, c) < t0 ? 1 : 0)); };
       auto rs_of = [&](int c) {
         return __builtin_amdgcn_make_buffer_rsrc(g.ws + static_cast<int64_t>(slab_of(c)) * kSkSlab, 0, kSkSlab * 4,
@@ -518,12 +548,18 @@ gemm_sk_kernel(const SkArgs g) {
       }
     }
 
+    PZ_SK_STAMP(unit, 3);
     // ---- epilogue
     if constexpr (EK == kSkF32) {
       sk_store_f32<W>(p, acc, m0, n0, wm, wn, lane);
     } else {
       epilogue_lds<kSkB, kSkB, 2, G::WN, Lay16<8, G::TN>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
     }
+#ifdef PZ_GEMM_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the tile's stores have left this CU
+#endif
+    PZ_SK_STAMP(unit, 4);
+    ++unit;
   }
 }
 

@@ -126,13 +126,14 @@ def gemm(a: Tensor, a_kc: bool, b: Tensor, b_kc: bool, out: Tensor, *, bias: Ten
 
 
 def gemm_pair(a0: Tensor, b0: Tensor, out0: Tensor, a1: Tensor, b1: Tensor, out1: Tensor, *,
-              scales0: tuple = (None, None), scales1: tuple = (None, None)) -> None:
+              scales0: tuple = (None, None), scales1: tuple = (None, None), engine: int = 0, cus: int = 0) -> None:
     """Two weight-gradient GEMMs ``out_i = a_iᵀ @ b_i`` (``a_i`` stored ``[K, M_i]``, ``b_i``
     ``[K, N_i]``, one K) in ONE launch (``pz::gemm_pair``); fp8 operands take their
-    ``(scale_a, scale_b)`` dequantisation scalars. Check :func:`gemm_pair_split` first."""
+    ``(scale_a, scale_b)`` dequantisation scalars. Check :func:`gemm_pair_split` first.
+    ``engine=2`` (bf16): both problems' tiles as one persistent stream-K schedule on ``cus`` CUs."""
     K = a0.shape[0]
     _ops().gemm_pair(a0, b0, out0, a1, b1, out1, out0.shape[0], out0.shape[1], out1.shape[0], out1.shape[1], K,
-                     scales0[0], scales0[1], scales1[0], scales1[1])
+                     scales0[0], scales0[1], scales1[0], scales1[1], ((engine & 3) << 2) | ((cus & 0xFFFF) << 16))
 
 
 def gemm_pair_split(a0: Tensor, b0: Tensor, out0: Tensor, a1: Tensor, b1: Tensor, out1: Tensor) -> int:

@@ -182,3 +182,17 @@ def test_sk_four_wave_lab_loop(native_lib, layout):
         out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
         PF.gemm(a, a_kc, b, b_kc, out, engine=3, cus=cus)
         _close(out, ref, K)
+
+
+@pytest.mark.parametrize("cus", [256, 240, 100])
+def test_sk_two_problem_schedule(native_lib, cus):
+    """Two weight-gradient GEMMs (the first layer's and the last layer's) as ONE persistent
+    stream-K schedule: the second problem's tiles follow the first's; both against fp64."""
+    K = 4096
+    a0, b0, r0 = _ops(1024, 2048, K, False, False, 31)
+    a1, b1, r1 = _ops(2048, 1024, K, False, False, 32)
+    o0 = torch.full((1024, 2048), float("nan"), device=DEV)
+    o1 = torch.full((2048, 1024), float("nan"), device=DEV)
+    PF.gemm_pair(a0, b0, o0, a1, b1, o1, engine=2, cus=cus)
+    _close(o0, r0, K, 1e-5)
+    _close(o1, r1, K, 1e-5)
