@@ -339,6 +339,10 @@ class FusedTrainer(Fp8Policy):
         # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
         self._side_pending: list = []
+        # workgroup cap of the side-stream updates (0: one workgroup per 4096-element block): a
+        # capped update streams its bytes over a longer window beside the GEMMs instead of
+        # taking the HBM from the critical path's kernels
+        self._side_grid = int(os.environ.get("PZ_OPT_SIDE_GRID", "0"))
         self._pair_dw = None       # (stage, x_in, dZ) of the dW GEMM that waits for its partner
         # data parallel: the backward GEMMs issued while a gradient bucket is on the wire run on the
         # persistent engine with the CUs the collective kernels leave (parallel/dist.py comm_cus)
@@ -488,19 +492,21 @@ class FusedTrainer(Fp8Policy):
 
     # ------------------------------------------------------------------------------------
     # epilogue specs
-    def _opt_async(self, items: list) -> None:
+    def _opt_async(self, items: list, ready=None) -> None:
         """Queue the updates of optimizer groups ``[(key, handles, stages)]`` on the side stream
         behind their gradients: ONE event recorded on the compute stream for all of them (each
-        record / cross-stream wait costs the compute stream a few microseconds of idle)."""
+        record / cross-stream wait costs the compute stream a few microseconds of idle), or an
+        already recorded ``ready`` event."""
         main, l2, scale = self._ov
-        ready = self.events.sync(self._capturing)
-        ready.record(main)
+        if ready is None:
+            ready = self.events.sync(self._capturing)
+            ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             ready.wait(self.opt_stream)
             for key, handles, stages in items:
                 for h in handles:
                     self.ctx.wait_one(h)
-                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
+                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity, self._side_grid)
                 if self.fp8:
                     for st in stages:
                         self._refresh_fp8_weights(st, 1 - self.parity)
@@ -777,20 +783,24 @@ class FusedTrainer(Fp8Policy):
             # stream right behind the last dW: the next step's first GEMM follows it in order (no
             # cross-stream wait), and it overlaps the side stream's still-running updates instead
             # of queueing behind them; step_finalize (side) waits for both
-            if self._side_pending:  # (merged side updates not flushed by their last layer)
-                self._opt_async(self._side_pending)
-            self._side_pending = []
+            pending, self._side_pending = self._side_pending, []
             for h in list(self._late_handles) + [handles[-1]]:
                 self.ctx.wait_one(h)
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
             if self.fp8:
                 for st in self._late_stages:
                     self._refresh_fp8_weights(st, 1 - self.parity)
-            self._ov = None
             rest_ev = self.events.sync(capture)
             rest_ev.record(main)
+            # side updates not flushed by their last layer (the paired partner's) join the side
+            # stream behind the SAME event: one record on this stream fewer (~7 us of idle; the
+            # side stream is still busy with the earlier layers' updates when it comes)
+            if pending:
+                self._opt_async(pending, ready=rest_ev)
+            self._ov = None
             with torch.cuda.stream(self.opt_stream):
-                rest_ev.wait(self.opt_stream)
+                if not pending:
+                    rest_ev.wait(self.opt_stream)
                 self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
                 ev = self.events.sync(capture)
