@@ -339,13 +339,13 @@ class FusedTrainer(Fp8Policy):
         # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
         self._side_pending: list = []
-        # workgroup cap of the side-stream updates (0: one workgroup per 4096-element block): a
-        # capped update streams its bytes over a longer window beside the GEMMs instead of
-        # taking the HBM from the critical path's kernels
-        self._side_grid = int(os.environ.get("PZ_OPT_SIDE_GRID", "0"))
+
         self._pair_dw = None       # (stage, x_in, dZ) of the dW GEMM that waits for its partner
-        # data parallel: the backward GEMMs issued while a gradient bucket is on the wire run on the
-        # persistent engine with the CUs the collective kernels leave (parallel/dist.py comm_cus)
+        # data parallel: the paired dW launch issued while a gradient bucket is on the wire runs as
+        # one persistent stream-K schedule on the CUs the collective kernels leave
+        # (parallel/dist.py comm_cus). Only the pair: a one-round grid is where a held CU costs a
+        # whole extra round; the multi-round GEMMs absorb it (dX_L2 217 vs 194 us under the proxy)
+        # better than the budgeted engine's split-tile hand-offs (profiles/r5_sk_stamps.txt)
         self._cus = 0
         self._cus_comm = 0
         if self.ctx.enabled and self.ctx.comm_cus > 0:
@@ -506,7 +506,7 @@ class FusedTrainer(Fp8Policy):
             for key, handles, stages in items:
                 for h in handles:
                     self.ctx.wait_one(h)
-                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity, self._side_grid)
+                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
                 if self.fp8:
                     for st in stages:
                         self._refresh_fp8_weights(st, 1 - self.parity)
@@ -1029,9 +1029,9 @@ class FusedTrainer(Fp8Policy):
         else:
             if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
                 x8, sx, g8, sg = f8
-                PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg, cus=self._cus)
+                PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
             else:
-                PF.gemm(x_in, False, g, False, w_grad, cus=self._cus)
+                PF.gemm(x_in, False, g, False, w_grad)
             mine = [self._bucket(w_grad)]
         handles.extend(mine)
         # the update writes the OTHER shadow set, but it is queued after this layer's dX GEMM
@@ -1063,7 +1063,13 @@ class FusedTrainer(Fp8Policy):
         if ok is None:
             ok = self._y_dead_cache[key] = ((f8_0 is None) == (f8_p is None)
                                             and PF.gemm_pair_split(ops0[0], ops0[1], w0, opsp[0], opsp[1], wp) > 0)
-        if ok:
+        if ok and self._cus and f8_0 is None:
+            # a bucket is on the wire: the pair's 256-workgroup grid would leave a straggler round
+            # behind the CUs the collective holds (239 vs 133 us under the 16-workgroup proxy,
+            # profiles/r5_step_timeline_proxy16.txt): both GEMMs as one stream-K schedule on the
+            # CUs left to it instead
+            PF.gemm_pair(ops0[0], ops0[1], w0, opsp[0], opsp[1], wp, engine=2, cus=self._cus)
+        elif ok:
             PF.gemm_pair(ops0[0], ops0[1], w0, opsp[0], opsp[1], wp,
                          scales0=(f8_0[1], f8_0[3]) if f8_0 is not None else (None, None),
                          scales1=(f8_p[1], f8_p[3]) if f8_p is not None else (None, None))
@@ -1125,10 +1131,10 @@ class FusedTrainer(Fp8Policy):
                 PF.gemm(g8, True, self.w8n[st.seg_w.offset], True, dx,
                         aux=None if mask is not None else before.buffers["y"], colsum=colsum, mode=PF.EPI_BWD,
                         epi=(ei, ef), mask=mask, scale_a=self.gqs[k, 1:2], scale_b=self.wqs[st.w8_index, 1:2],
-                        cus=self._cus, **kw8)
+                        **kw8)
             else:
                 PF.gemm(g, True, self._w(st), True, dx, aux=None if mask is not None else before.buffers["y"],
-                        colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask, cus=self._cus, **kw8)
+                        colsum=colsum, mode=PF.EPI_BWD, epi=(ei, ef), mask=mask, **kw8)
             if kw8:
                 self._g8_done[b] = dx
             elif getattr(before, "g8_from_epi", False) and rec is None and self._ov is not None \
@@ -1140,7 +1146,7 @@ class FusedTrainer(Fp8Policy):
         colsum = None
         if no_epi_prev and before.seg_b is not None:
             colsum = self.store.view(before.seg_b, self.grads)
-        PF.gemm(g, True, self._w(st), True, dx, colsum=colsum, mode=PF.EPI_STORE, cus=self._cus)
+        PF.gemm(g, True, self._w(st), True, dx, colsum=colsum, mode=PF.EPI_STORE)
         if rec is not None:
             rec[("grad", before.layers[-1])] = dx[:batch * before.pos_out]
         if no_epi_prev or before.kind == "embed":

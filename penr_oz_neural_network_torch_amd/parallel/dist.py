@@ -41,12 +41,10 @@ class DataParallelContext:
     force: bool = False
     native: object = None  # _NativeComm: the extension's RCCL communicator (gradient buckets)
     # PZ_COMM_BUDGET=k (default 0 = off): CUs to leave to the gradient collectives while a bucket is
-    # on the wire (RCCL holds one workgroup per channel). The fused trainer then runs the GEMMs that
-    # overlap a collective on the persistent stream-K engine with a grid k CUs smaller
-    # (csrc/gemm_sk.hip) instead of the tiled grid, whose last round waits for the held CUs. Off by
-    # default: measured on one GPU against the collective-footprint proxy (16 workgroups held for a
-    # modelled 8-rank ring), the stream-K grid's split-tile hand-offs cost more than the tiled
-    # kernels' straggler round (mlp4 1.606 vs 1.459 ms/step, profiles/r5_comm_pressure.txt).
+    # on the wire (RCCL holds one workgroup per channel). The fused trainer then runs the paired dW
+    # launch that overlaps the largest bucket as one persistent stream-K schedule with a grid k CUs
+    # smaller (csrc/gemm_sk.hip) instead of its one-round tiled grid, whose workgroups on the held
+    # CUs would otherwise form a whole second round (profiles/r5_comm_pressure.txt).
     comm_cus: int = 0
 
     @property
