@@ -68,7 +68,6 @@ constexpr int kSkStampUnits = 6;
 constexpr int kSkB = 256;                    // macro tile BM = BN
 constexpr int kSkSlab = kSkB * kSkB;         // fp32 floats of one partial tile
 constexpr int kSkF32 = 100;                  // epilogue code of the fp32-output store path
-constexpr int kSkMaxCon = 8;                 // contributors per stream-K tile (sk_plan bounds it)
 constexpr int kSkLds = 128 * 1024;           // both main loops' rings = the epilogue's C image
 
 // Main-loop geometry per wave count. W = 8 (the default): two waves per SIMD, 128x64 wave tiles,
@@ -520,7 +519,7 @@ gemm_sk_kernel(const SkArgs g) {
       };
       // in groups of 16 chunks (64 VGPRs of loads in flight): an unbounded unrolled fold let
       // hipcc hoist every load and spill
-      auto fold = [&](const auto& rs, bool first) __attribute__((always_inline)) {
+      auto fold = [&](const auto& rs) __attribute__((always_inline)) {
         static_for<CH / 16>([&](auto qc) {
           constexpr int q = decltype(qc)::value;
           f32x4_t ld[16];
@@ -530,22 +529,15 @@ gemm_sk_kernel(const SkArgs g) {
           });
           static_for<16>([&](auto cc) {
             constexpr int c = 16 * q + decltype(cc)::value;
-            acc[c / G::TN][c % G::TN] = first ? ld[c - 16 * q] : acc[c / G::TN][c % G::TN] + ld[c - 16 * q];
+            acc[c / G::TN][c % G::TN] = acc[c / G::TN][c % G::TN] + ld[c - 16 * q];
           });
           __builtin_amdgcn_sched_barrier(0);
         });
       };
-      if (whi - wlo == 1) {  // two contributors: own + other == the K-ordered sum (addition commutes)
-        fold(rs_of(w == wlo ? whi : wlo), false);
-      } else {  // fold every slab (own included, it was stored above) in K order
-        // (unrolled over at most kSkMaxCon contributors, sk_plan's bound: a runtime loop carried
-        // the accumulators through a loop phi that hipcc could only keep in VGPRs)
-        fold(rs_of(wlo), true);
-        static_for<kSkMaxCon - 1>([&](auto kc) {
-          constexpr int k = decltype(kc)::value + 1;
-          if (wlo + k <= whi) fold(rs_of(wlo + k), false);
-        });
-      }
+      // sk_plan gives every tile at most two contributors: own + other == the K-ordered sum
+      // (addition commutes), one 256 KiB slab read. (Measured, not kept: tiles split over 3-4
+      // contributors — the last arriver's fold of 0.75-1 MiB took 36-41 us, profiles/r5_sk_stamps.txt)
+      fold(rs_of(w == wlo ? whi : wlo));
     }
 
     PZ_SK_STAMP(unit, 3);
@@ -619,16 +611,14 @@ SkSched sk_plan(const GemmArgs* probs, int n) {
   const int cus = device_cus();
   int grid = probs[0].cus > 0 ? std::min(probs[0].cus, cus) : cus;
   const int T = s.tiles;
-  // fewer tiles than workgroups: at most kSkMaxCon contributors per tile (the fold's unroll)
-  if (T < grid) grid = std::min(grid, T * (kSkMaxCon - 1));
+  // At most TWO contributors per tile. Fewer tiles than workgroups: each tile in two K halves on
+  // 2T workgroups when the budget holds them and the halves are >= 256 deep, else one workgroup
+  // per tile (data-parallel; the other CUs idle but the survivors run faster per step). At least
+  // as many tiles: the "two-tile" region gives every workgroup >= one tile of K steps, so a tile
+  // meets at most two workgroups' ranges.
+  if (T < grid) grid = (2 * T <= grid && s.iters * bk >= 512) ? 2 * T : T;
   int sk = 0;
   if (T % grid != 0) sk = T < grid ? T : T % grid + grid;
-  // a stream-K share under 256 K per workgroup: fewer workgroups (each takes at least that)
-  const long long min_steps = 256 / bk;
-  if (sk > 0 && static_cast<long long>(sk) * s.iters < min_steps * grid) {
-    grid = std::max(1, static_cast<int>(static_cast<long long>(sk) * s.iters / min_steps));
-    sk = (T % grid == 0) ? 0 : (T < grid ? T : T % grid + grid);
-  }
   s.grid = grid;
   s.sk_tiles = sk;
   s.sk_iters = static_cast<long long>(sk) * s.iters;

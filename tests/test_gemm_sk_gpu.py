@@ -1,6 +1,6 @@
 """The persistent stream-K GEMM engine (csrc/gemm_sk.hip) against fp64 torch references: every
 layout and epilogue kind the trainer runs, at CU budgets that give pure data-parallel tiles
-(256), a two-tile stream-K region (240, 200) and many contributors per tile (small budgets), plus
+(256), a two-tile stream-K region (240, 200) and tiles far outnumbering the workgroups (37), plus
 bit-for-bit determinism of the stream-K fold (run on MI355X)."""
 import math
 
@@ -105,8 +105,8 @@ def test_sk_backward_epilogues_and_colsum(native_lib, use_mask, cus):
 
 @pytest.mark.parametrize("shape,cus", [((8192, 1024, 4096), 256), ((4096, 1024, 8192), 256), ((2048, 4096, 1024), 96)])
 def test_sk_stream_k_fold_is_deterministic(native_lib, shape, cus):
-    """Stream-K tiles (2 and 4 contributors) folded in K order: bit-identical across runs, whichever
-    workgroup arrives last."""
+    """Stream-K tiles split over two contributors (K halves on 2T workgroups, or the two-tile
+    region): bit-identical across runs, whichever workgroup arrives last."""
     M, N, K = shape
     a, b, ref = _ops(M, N, K, True, False, 3)
     outs = []

@@ -136,6 +136,25 @@ def main():
             res[k] = {"best": round(v[-1], 1), "median": round(v[len(v) // 2], 1)}
         out[name] = res
         print(name, json.dumps({k: res[k] for k in variants}), flush=True)
+    if not args.cases or "pair" in args.cases:  # the paired first-layer + last-layer dW launch
+        K = B
+        x0 = (torch.rand(K, 1024, device=dev) * 2 - 1).to(torch.bfloat16)
+        z0 = (torch.rand(K, 4096, device=dev) * 2 - 1).to(torch.bfloat16)
+        x1 = (torch.rand(K, 4096, device=dev) * 2 - 1).to(torch.bfloat16)
+        z1 = (torch.rand(K, 1024, device=dev) * 2 - 1).to(torch.bfloat16)
+        w0 = torch.empty(1024, 4096, device=dev, dtype=torch.bfloat16)
+        w1 = torch.empty(4096, 1024, device=dev, dtype=torch.bfloat16)
+        fl = 2.0 * 2 * 1024 * 4096 * K
+        variants = {"tiled_pair": lambda: PF.gemm_pair(x0, z0, w0, x1, z1, w1)}
+        for cus in cus_list:
+            variants[f"sk_pair_cus{cus}"] = (lambda cc: (lambda: PF.gemm_pair(x0, z0, w0, x1, z1, w1, engine=2, cus=cc)))(cus)
+        tf = {k: [] for k in variants}
+        for _ in range(args.rounds):
+            for k, fn in variants.items():
+                tf[k].append(fl / timeit(fn) / 1e12)
+        res = {k: {"best": round(max(v), 1), "median": round(sorted(v)[len(v) // 2], 1)} for k, v in tf.items()}
+        out["pair"] = res
+        print("pair", json.dumps(res), flush=True)
     print(json.dumps(out))
 
 

@@ -51,7 +51,7 @@ int main(int argc, char** argv) {
   for (int i = 1; i < argc; ++i) budgets.push_back(atoi(argv[i]));
   if (budgets.empty()) budgets = {256, 240, 224, 128};
   const Shape shapes[] = {{"dX_L2", 8192, 4096, 4096, true, true}, {"dW_L2", 4096, 4096, 8192, false, false},
-                          {"fwd_L1", 8192, 4096, 1024, true, false}};
+                          {"fwd_L1", 8192, 4096, 1024, true, false}, {"dW_L1", 1024, 4096, 8192, false, false}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (const Shape& sh : shapes) {
