@@ -25,10 +25,14 @@ def test_progress_poll_of_25m_param_gpu_model(models_tmpdir, native_lib):
     client.get("/progress/", params={"model_id": "big"})  # warm the route
     torch.cuda.synchronize()
     before = torch.cuda.memory_allocated()
-    t0 = time.perf_counter()
-    r = client.get("/progress/", params={"model_id": "big"})
-    dt = time.perf_counter() - t0
-    assert r.status_code == 200 and r.json()["status"] == "Created"
+    # best of three: the 1.1 GiB checkpoint was just written and its write-back can stall one
+    # stat/open on a busy box (157 ms seen once); parsing it would take seconds on every poll
+    dt = float("inf")
+    for _ in range(3):
+        t0 = time.perf_counter()
+        r = client.get("/progress/", params={"model_id": "big"})
+        dt = min(dt, time.perf_counter() - t0)
+        assert r.status_code == 200 and r.json()["status"] == "Created"
     assert torch.cuda.memory_allocated() == before
     assert dt < 0.05, f"/progress/ took {dt * 1e3:.1f} ms on a {size_mb:.0f} MiB checkpoint"
     r = client.get("/stats/", params={"model_id": "big"})
