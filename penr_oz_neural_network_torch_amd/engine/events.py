@@ -6,6 +6,12 @@ invalidated each time, ~7 us of idle compute stream per record / wait in the r4 
 Ordering two streams of one device needs a device-scope release only, and the per-step timestamps
 read back after a synchronize need no fence at all. Inside hipGraph capture the torch events are
 kept (capture records them as graph dependencies).
+
+(Measured, not kept: the producing kernel's last workgroup storing a flag that the other stream
+waits for with hipStreamWaitValue32 — no packet on the producing stream, and the lab's producer idle
+fell from 5-9 to ~1 us — but ROCm 7.2 serves that wait with a one-workgroup spin kernel
+(__amd_rocclr_streamOpsWait) that holds a CU for as long as it waits, so every 512-tile GEMM of the
+step ran a straggler round: mlp4 1.61 vs 1.11 ms, profiles/r5_stream_sig_lab.txt.)
 """
 from __future__ import annotations
 

@@ -341,6 +341,7 @@ class FusedTrainer(Fp8Policy):
         self._side_pending: list = []
 
         self._pair_dw = None       # (stage, x_in, dZ) of the dW GEMM that waits for its partner
+        self._pair_late = None     # (stage, gradient) of the paired partner, bucketed in the update phase
         # data parallel: the paired dW launch issued while a gradient bucket is on the wire runs as
         # one persistent stream-K schedule on the CUs the collective kernels leave
         # (parallel/dist.py comm_cus). Only the pair: a one-round grid is where a held CU costs a
@@ -773,7 +774,14 @@ class FusedTrainer(Fp8Policy):
 
         # ---------------- reduce + update
         self._phase("pz.update")
-        handles.append(self.ctx.all_reduce_async(self.grads[self.store.accum_offset:], exact=True))
+        acc_h = self.ctx.all_reduce_async(self.grads[self.store.accum_offset:], exact=True)
+        handles.append(acc_h)
+        if self._pair_late is not None:
+            sp, wp = self._pair_late
+            self._pair_late = None
+            hp = self._bucket(wp)
+            handles.append(hp)
+            self._side_pending.append((sp.seg_w.offset, [hp], [sp]))
         fin = dict(epoch_ctr=self.epoch_ctr, every=self._plan["every"] if self._plan else 1,
                    # fused e4m3 weight copies: this step's updates read the amax slot of the
                    # current parity; step_finalize clears it for the next step's updates
@@ -784,7 +792,7 @@ class FusedTrainer(Fp8Policy):
             # cross-stream wait), and it overlaps the side stream's still-running updates instead
             # of queueing behind them; step_finalize (side) waits for both
             pending, self._side_pending = self._side_pending, []
-            for h in list(self._late_handles) + [handles[-1]]:
+            for h in list(self._late_handles) + [acc_h]:
                 self.ctx.wait_one(h)
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
             if self.fp8:
@@ -1079,9 +1087,11 @@ class FusedTrainer(Fp8Policy):
                     PF.gemm(a, False, b, False, w, scale_a=f8[1], scale_b=f8[3])
                 else:
                     PF.gemm(a, False, b, False, w)
-        hp = self._bucket(wp)
-        handles.append(hp)
-        self._side_pending.append((sp.seg_w.offset, [hp], [sp]))
+        # the partner's bucket leaves in the update phase, after the first layer's and the
+        # accumulated-gradient bucket: the first-layer update (the step boundary) waits for those
+        # two only, and the partner's all-reduce overlaps it (its weight is next read by the next
+        # step's later forward GEMMs)
+        self._pair_late = (sp, wp)
         return self._bucket(w0)
 
     def _bucket(self, t):

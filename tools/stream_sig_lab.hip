@@ -15,6 +15,7 @@
 //   tiny     a one-workgroup kernel on the main stream stores the flag after busy1; the side
 //            stream waits with hipStreamWaitValue32
 //   write    hipStreamWriteValue32 on the main stream after busy1; hipStreamWaitValue32 on the side
+//   vwait    main waits with hipStreamWaitValue32 on a flag a side-stream kernel stored long before
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/stream_sig_lab.hip -o tools/stream_sig_lab
 #include <hip/hip_runtime.h>
@@ -101,16 +102,17 @@ int main() {
   hipEvent_t ev, evs;
   CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventReleaseToDevice));
   CK(hipEventCreateWithFlags(&evs, hipEventDisableTiming | hipEventReleaseToDevice));
-  const char* names[] = {"none", "event", "flag", "mwait", "tiny", "write"};
+  const char* names[] = {"none", "event", "flag", "mwait", "tiny", "write", "vwait"};
   uint32_t val = 0;
   for (int rep = 0; rep < 4; ++rep) {
-    for (int mode = 0; mode < 6; ++mode) {
+    for (int mode = 0; mode < 7; ++mode) {
       ++val;
       CK(hipDeviceSynchronize());
       if (mode == 3) {  // the side event is long complete when main reaches the wait
         hipLaunchKernelGGL(busy, dim3(GS), dim3(256), 0, s, out + 2 * G * 256, 10, st + 2 * 2 * G, nullptr, nullptr, 0u);
         CK(hipEventRecord(evs, s));
       }
+      if (mode == 6) hipLaunchKernelGGL(set_flag, dim3(1), dim3(64), 0, s, flag, val);
       hipLaunchKernelGGL(busy, dim3(G), dim3(256), 0, m, out, IT, st, ctr, mode == 2 ? flag : nullptr, val);
       if (mode == 1) {
         CK(hipEventRecord(ev, m));
@@ -122,12 +124,14 @@ int main() {
       } else if (mode == 4) {
         hipLaunchKernelGGL(set_flag, dim3(1), dim3(64), 0, m, flag, val);
         CK(hipStreamWaitValue32(s, flag, val, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      } else if (mode == 6) {
+        CK(hipStreamWaitValue32(m, flag, val, hipStreamWaitValueGte, 0xFFFFFFFFu));
       } else if (mode == 5) {
         CK(hipStreamWriteValue32(m, flag, val, 0));
         CK(hipStreamWaitValue32(s, flag, val, hipStreamWaitValueGte, 0xFFFFFFFFu));
       }
       hipLaunchKernelGGL(busy, dim3(G), dim3(256), 0, m, out + G * 256, IT, st + 2 * G, nullptr, nullptr, 0u);
-      if (mode == 1 || mode == 2 || mode >= 4)
+      if (mode == 1 || mode == 2 || mode == 4 || mode == 5)
         hipLaunchKernelGGL(busy, dim3(GS), dim3(256), 0, s, out + 2 * G * 256, 10, st + 2 * 2 * G, nullptr, nullptr, 0u);
       CK(hipDeviceSynchronize());
       std::vector<uint64_t> h((2 * G + GS) * 2);
@@ -135,7 +139,7 @@ int main() {
       const Span b1 = span(h, 0, G), b2 = span(h, G, G), sd = span(h, 2 * G, GS);
       printf("%-6s rep %d: busy1 %.1f us, main gap busy1 end -> busy2 start %.2f us", names[mode], rep,
              (b1.e - b1.s) * 0.01, (static_cast<double>(b2.s) - static_cast<double>(b1.e)) * 0.01);
-      if (mode == 1 || mode == 2 || mode >= 4)
+      if (mode == 1 || mode == 2 || mode == 4 || mode == 5)
         printf(", side kernel start - busy1 end %.2f us", (static_cast<double>(sd.s) - static_cast<double>(b1.e)) * 0.01);
       printf("\n");
     }
