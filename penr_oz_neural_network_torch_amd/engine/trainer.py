@@ -696,6 +696,7 @@ class FusedTrainer(Fp8Policy):
             self._ov = (main, l2, 1.0)  # gradients arrive as the global mean (1/S-scaled heads)
             self._late_stages, self._late_handles = [], []
             self._side_pending = []
+            self._pair_late = None
 
         # (no zeroing pass: the previous step's update kernel reset the accumulated-gradient region
         # as it read it, and its step_finalize the loss slots)

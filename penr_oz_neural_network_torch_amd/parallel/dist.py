@@ -208,8 +208,12 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
         os.environ.setdefault("MASTER_PORT", str(_free_port()))
     if (world > 1 or force) and not dist.is_initialized():
         if backend is None:
-            # PZ_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU
-            backend = os.environ.get("PZ_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+            # PZ_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU; so
+            # does a launch with more ranks on this node than visible GPUs (RCCL needs one GPU per
+            # rank: "invalid usage" otherwise), e.g. torchrun --nproc-per-node 4 on a 1-GPU box
+            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+            backend = os.environ.get("PZ_DIST_BACKEND") or (
+                "nccl" if torch.cuda.is_available() and torch.cuda.device_count() >= local_world else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
 
