@@ -1034,7 +1034,7 @@ class FusedTrainer(Fp8Policy):
         paired = self._pair_dw if st.index == 0 else None
         self._pair_dw = None if st.index == 0 else self._pair_dw
         if paired is not None:
-            mine = [self._run_pair(paired, st, x_in, g, w_grad, f8, handles)]
+            mine = [self._run_pair(paired, st, x_in, g, w_grad, f8)]
         else:
             if f8 is not None:  # e4m3 activations x e5m2 dZ on the scaled fp8 MFMA
                 x8, sx, g8, sg = f8
@@ -1057,11 +1057,11 @@ class FusedTrainer(Fp8Policy):
                 self._side_pending = []
         return out
 
-    def _run_pair(self, paired, st0: Stage, x0, g0, w0, f8_0, handles):
+    def _run_pair(self, paired, st0: Stage, x0, g0, w0, f8_0):
         """The first layer's dW GEMM together with the deferred partner's (``_pair_idx``) in one
         launch when both take the same operand precision and the pair is eligible, else one
-        after the other. The partner's update joins the side-stream queue (flushed with the
-        step's remaining side updates); returns the first layer's bucket handle."""
+        after the other. The partner's bucket and update are queued in the update phase
+        (``_pair_late``); returns the first layer's bucket handle."""
         sp, xp, gp = paired
         wp = self._w_grad(sp.seg_w)
         f8_p = self._fp8_dw(sp, gp, wp)
