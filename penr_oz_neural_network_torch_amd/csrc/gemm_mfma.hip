@@ -795,6 +795,18 @@ hipError_t launch_bk64_256(const GemmArgs& p, hipStream_t s) {
   return launch_layout<256, 256, 2, 4, OutT, AuxT, VAR>(p, s);
 }
 
+// Fixed-kind bf16 forward GEMMs with too few 256x256 tiles to fill the CUs (the logits GEMM,
+// [8192, 1024] at K = 4096) run as 256x128 tiles on the 64-deep ring WITHOUT split-K: the
+// deterministic split-K fold's slab round trip and the split tile's heavier epilogue cost more
+// than the narrower tile's extra LDS traffic. r5 same box: fused fwd_L3 885-949 vs 830-841 TF/s,
+// mlp4 step 1.111-1.113 vs 1.130-1.138 ms (profiles/r5_ab_w128_fixed.txt). (r2, before the
+// fixed epilogue kinds and the deterministic fold: the generic-epilogue 256x128 form lost in-step.)
+bool w128_fixed(const GemmArgs& p) {
+  if (p.in_dtype != DT_BF16 || p.out_dtype != DT_BF16 || !p.a_kc || p.b_kc || p.accumulate) return false;
+  if (p.M % 256 || p.N % 128 || !ek_fixed(epi_kind(p))) return false;
+  return ((p.M / 256) * ((p.N + 255) / 256)) < 240 && (p.M / 256) * (p.N / 128) >= 240;
+}
+
 template <typename OutT, typename AuxT>
 hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
   auto tiles = [&](int bm, int bn) { return ((p.M + bm - 1) / bm) * ((p.N + bn - 1) / bn); };
@@ -812,6 +824,14 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     return buf ? launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s) : launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
   }
   if (tiles(256, 128) >= kFill) {
+    if constexpr (std::is_same<OutT, uint16_t>::value) {
+      if (bk64 && w128_fixed(p)) {
+        const int ek = epi_kind(p);
+        if (ek == EK_F_RELU_POST) return launch_cfg<256, 128, 4, 2, true, false, OutT, AuxT, 30, EK_F_RELU_POST>(p, s);
+        if (ek == EK_F_RELU_PREPOST) return launch_cfg<256, 128, 4, 2, true, false, OutT, AuxT, 30, EK_F_RELU_PREPOST>(p, s);
+        if (ek == EK_F_PRE) return launch_cfg<256, 128, 4, 2, true, false, OutT, AuxT, 30, EK_F_PRE>(p, s);
+      }
+    }
     if (bk64) return launch_layout<256, 128, 4, 2, OutT, AuxT, 30>(p, s);
     return buf ? launch_layout<256, 128, 4, 2, OutT, AuxT, 6>(p, s) : launch_layout<256, 128, 4, 2, OutT, AuxT>(p, s);
   }
@@ -980,11 +1000,13 @@ int gemm_split(const GemmArgs& p) {
   // (and the N-contiguous-weight fp8 forward, VAR 15: 256x256 tiles only)
   const bool f8_dw = p.in_dtype == DT_FP8 && !p.b_kc;
   if ((p.in_dtype == DT_FP8 && !f8_dw) || !mfma_eligible(p)) return 1;
+  if (w128_fixed(p)) return 1;
   const int tiles = ((p.M + 255) / 256) * ((p.N + 255) / 256);
   constexpr int kFill = 240;
   if (tiles >= kFill) return 1;
-  // (measured, not kept: bf16 outputs on 256x128 tiles instead of a split — fwd [8192,1024]
-  // K=4096 1008 vs 881 TF/s alone, the mlp4 step slower, profiles/r2_lab_skinny_fwd.txt)
+  // (fixed-kind forwards: 256x128 tiles instead, w128_fixed above; the generic-epilogue kinds
+  // keep the split — r2: 1008 vs 881 TF/s alone but the mlp4 step slower,
+  // profiles/r2_lab_skinny_fwd.txt)
   const int nk = p.K / (p.in_dtype == DT_FP8 ? 64 : kBK);
   for (int sp : {2, 4, 8})
     if (tiles * sp >= kFill && nk % sp == 0 && nk / sp >= 16) return sp;
