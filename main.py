@@ -217,25 +217,31 @@ async def train_model(body: TrainingRequest = Body(...)):
     _starting.add(model_id)
     try:
         model = await run_in_threadpool(NeuralNetworkModel.deserialize, model_id)
+        data = [(item.activation_vector, item.target_vector) for item in body.training_data]
+        hp = dict(epochs=body.epochs, learning_rate=body.learning_rate, batch_size=body.batch_size,
+                  decay_rate=body.decay_rate, dropout_rate=body.dropout_rate, l2_lambda=body.l2_lambda,
+                  beta1=body.adam_beta1, beta2=body.adam_beta2, epsilon=body.adam_epsilon)
+
+        async def train():
+            try:
+                async with lock:
+                    _starting.discard(model_id)  # the lock now says "in progress"
+                    # one thread trains; with a multi-GPU train group up, a GPU model trains on every rank
+                    await run_in_threadpool(service.train, model, data, hp)
+            finally:
+                _starting.discard(model_id)
+
+        def _done(task) -> None:
+            if task.cancelled():  # cancelled before its first step: its body (and finally) never ran
+                _starting.discard(model_id)
+            _log_task_failure(task)
+
+        create_task(train()).add_done_callback(_done)
     except BaseException:
+        # anything before the task exists (load, request unpacking, task creation) must not leave
+        # the id marked as starting: every later PUT /train/ would answer 409
         _starting.discard(model_id)
         raise
-    data = [(item.activation_vector, item.target_vector) for item in body.training_data]
-
-    hp = dict(epochs=body.epochs, learning_rate=body.learning_rate, batch_size=body.batch_size,
-              decay_rate=body.decay_rate, dropout_rate=body.dropout_rate, l2_lambda=body.l2_lambda,
-              beta1=body.adam_beta1, beta2=body.adam_beta2, epsilon=body.adam_epsilon)
-
-    async def train():
-        try:
-            async with lock:
-                _starting.discard(model_id)  # the lock now says "in progress"
-                # one thread trains; with a multi-GPU train group up, a GPU model trains on every rank
-                await run_in_threadpool(service.train, model, data, hp)
-        finally:
-            _starting.discard(model_id)
-
-    create_task(train()).add_done_callback(_log_task_failure)
     return JSONResponse(content={"message": f"Training for model {model_id} started asynchronously."},
                         status_code=202)
 

@@ -261,8 +261,8 @@ void gemm_op(const Tensor& A, bool a_kc, const Tensor& B, bool b_kc, const Tenso
     p.cs_tickets = split_counters(((p.N + 127) / 128) * (groups + 1), A.device());
   }
   at::Tensor ws;  // split-K / stream-K slabs: from the caching allocator, stream-ordered reuse is safe
-  // flags bits 2-3: engine (0 default, 1 tiled gemm_mfma, 2 persistent stream-K, 3 its 4-wave lab
-  // loop); bits 16-31: the CU budget of the persistent engine (0 = every CU)
+  // flags bits 2-3: engine (0 default, 1 tiled gemm_mfma, 2 persistent stream-K; 3, the round-5
+  // 4-wave lab loop, is refused: tools/gemm_w4_lab.hip); bits 16-31: the CU budget of the persistent engine (0 = every CU)
   p.engine = static_cast<int>((flags >> 2) & 3);
   p.cus = static_cast<int>((flags >> 16) & 0xFFFF);
   // (engine 0 with a CU budget: the persistent engine wherever it is eligible)
@@ -386,10 +386,15 @@ pz::GemmArgs pair_args(const Tensor& A, const Tensor& B, const Tensor& C, int64_
   return p;
 }
 
+// engine 2: also 0 unless the persistent stream-K engine takes BOTH problems (pz::sk_eligible:
+// e.g. K >= two 64-deep steps) — the trainer's budgeted pair checks this before it asks for it
 int64_t gemm_pair_split_op(const Tensor& A0, const Tensor& B0, const Tensor& C0, const Tensor& A1, const Tensor& B1,
-                           const Tensor& C1, int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K) {
-  return pz::gemm_pair_split(pair_args(A0, B0, C0, M0, N0, K, c10::nullopt, c10::nullopt),
-                             pair_args(A1, B1, C1, M1, N1, K, c10::nullopt, c10::nullopt));
+                           const Tensor& C1, int64_t M0, int64_t N0, int64_t M1, int64_t N1, int64_t K, int64_t engine) {
+  const auto a = pair_args(A0, B0, C0, M0, N0, K, c10::nullopt, c10::nullopt);
+  const auto b = pair_args(A1, B1, C1, M1, N1, K, c10::nullopt, c10::nullopt);
+  const int split = pz::gemm_pair_split(a, b);
+  if (engine >= 2 && !(pz::sk_eligible(a) && pz::sk_eligible(b))) return 0;
+  return split;
 }
 
 void launch_pair(pz::GemmArgs& a, pz::GemmArgs& b, const Tensor& A0) {
@@ -1014,7 +1019,7 @@ TORCH_LIBRARY(pz, m) {
         "float bias_c2_sqrt, float grad_scale, float l2, Tensor? hp=None, Tensor? epoch=None, int stats_every=1) -> ()");
   m.def("gemm_path(Tensor A, bool a_kc, Tensor B, bool b_kc, Tensor C, int M, int N, int K) -> int");
   m.def("gemm_pair_split(Tensor A0, Tensor B0, Tensor C0, Tensor A1, Tensor B1, Tensor C1, int M0, int N0, int M1, "
-        "int N1, int K) -> int");
+        "int N1, int K, int engine=0) -> int");
   m.def("gemm_pair(Tensor A0, Tensor B0, Tensor(a!) C0, Tensor A1, Tensor B1, Tensor(b!) C1, int M0, int N0, int M1, "
         "int N1, int K, Tensor? scale_a0=None, Tensor? scale_b0=None, Tensor? scale_a1=None, "
         "Tensor? scale_b1=None, int flags=0) -> ()");

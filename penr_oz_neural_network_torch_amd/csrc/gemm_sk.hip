@@ -1,23 +1,23 @@
-// N1b — persistent stream-K bf16 GEMM for gfx950: the step GEMMs' engine.
+// N1b — persistent stream-K bf16 GEMM for gfx950 (engine 2 of pz::gemm / pz::gemm_pair).
 //
 // Replaces the reference's per-layer matmuls (neural_net_model.py:117 forward `x @ W`, and the two
 // autograd `mm` of cost.backward(), :495) with the fused stage epilogues around them (bias :119,
 // activation :172-184, dropout :393-395, bias-gradient column sums).
 //
+// Where it runs: NOT the default step engine (gemm_mfma.hip's tiled kernels are; at the full CU
+// budget both reach the same main-loop rate and the tiled epilogues are lighter). The trainer uses
+// it for ONE launch: under data parallelism with PZ_COMM_BUDGET=k, the paired weight-gradient
+// GEMMs issued while a gradient bucket is on the wire run as one stream-K schedule on the CUs the
+// collective leaves (a one-round tiled grid would leave a straggler round behind the held CUs).
+// PZ_GEMM_SK=1 routes every eligible GEMM here (A/B). The 4-wave 128x128-wave-tile loop measured
+// in round 5 (0.70-0.75x the ping-pong, profiles/r5_pmc_sk4_vs_pingpong.txt) lives in
+// tools/gemm_w4_lab.hip, not in the library.
+//
 // Design (MI355X-first; /opt/skills/guides/cdna_hip_programming.md §5, MI355X_MICROARCH.md):
-//  * 256x256 macro tile on FOUR waves, one per SIMD, each owning a 128x128 wave tile = 8x8
-//    v_mfma_f32_16x16x32_bf16 accumulators (the whole 256-register AGPR file). Per 32-deep K step
-//    a wave reads 16 fragments for 64 MFMAs: 0.25 LDS reads per MFMA (the 8-wave 128x64 wave
-//    tiles of gemm_mfma.hip read 0.375).
-//  * LDS ring of NS 32-deep slots (32 KiB: A [256 rows][32 k], B likewise), filled by buffer-
-//    addressed LDS-DMA (`buffer_load_dwordx4 ... lds`, swizzle on the per-lane SOURCE offset).
-//    Fragments are read one step AHEAD into a second VGPR set, so a slot is free again one step
-//    after it landed; its refill for step h+NS is issued in step h and has NS-1 steps (1.5 full
-//    64-deep K steps at NS = 4) to land — the 2-slot 64-deep ring gave the DMA one step.
-//  * One raw s_barrier per step: every wave's counted `vmcnt` for step h+2 and `lgkmcnt(0)` for
-//    its reads of step h+1 precede it (RAW for the next reads, WAR for the next refill).
-//  * MFMAs, next-step fragment reads and refill DMAs interleaved in 16 groups per step (4 MFMAs,
-//    one fragment, every other group one DMA), fenced by sched_barrier so hipcc keeps the mix.
+//  * 256x256 macro tile on EIGHT waves (two per SIMD, 128x64 wave tiles of 16x16x32 bf16 MFMAs) in
+//    the ping-pong schedule of gemm_mfma.hip VAR 30: a 2-slot ring of 64-deep K steps filled by
+//    buffer-addressed LDS-DMA (`buffer_load_dwordx4 ... lds`, swizzle on the per-lane SOURCE
+//    offset), the staging lane offsets precomputed once per piece class.
 //  * PERSISTENT: the grid is the CU budget (GemmArgs::cus, at most the device's CUs, one
 //    workgroup per CU). Every workgroup walks a static schedule: a stream-K region — the tiles
 //    that do not fill whole rounds of workgroups, their K iterations split evenly over ALL
@@ -28,7 +28,7 @@
 //    into a slab, drains, joins a barrier and takes a relaxed agent-scope ticket (MI355X_MICROARCH
 //    hand-off table, row 1); the LAST arriver folds the slabs in K order with sc1 loads and runs
 //    the epilogue. The sum order never depends on which workgroup arrives last: deterministic.
-//  * Epilogues: gemm_epilogue.h's LDS-staged kinds on 128-column wave tiles; fp32 outputs (weight
+//  * Epilogues: gemm_epilogue.h's LDS-staged kinds on 64-column wave tiles; fp32 outputs (weight
 //    gradients) store straight from the accumulators.
 //  * Two problems of one layout / epilogue kind / K may share a launch (the two skinny weight-
 //    gradient GEMMs of a 3-layer MLP): their tiles form one schedule.
@@ -70,15 +70,15 @@ constexpr int kSkSlab = kSkB * kSkB;         // fp32 floats of one partial tile
 constexpr int kSkF32 = 100;                  // epilogue code of the fp32-output store path
 constexpr int kSkLds = 128 * 1024;           // both main loops' rings = the epilogue's C image
 
-// Main-loop geometry per wave count. W = 8 (the default): two waves per SIMD, 128x64 wave tiles,
-// the ping-pong over a 2-slot 64-deep ring of the tiled kernels (gemm_mfma.hip VAR 30). W = 4
-// (engine 3, lab): one wave per SIMD, 128x128 wave tiles, a 4-slot 32-deep ring.
+// Main-loop geometry (W = 8 waves): two waves per SIMD, 128x64 wave tiles, the ping-pong over a
+// 2-slot 64-deep ring of the tiled kernels (gemm_mfma.hip VAR 30)
 template <int W> struct SkGeo {
+  static_assert(W == 8, "the library's stream-K engine runs the 8-wave ping-pong loop");
   static constexpr int NT = W * 64;
   static constexpr int WN = W / 2;           // wave grid 2 x WN
   static constexpr int TN = 16 / WN;         // 16x16 accumulator tiles across a wave tile
   static constexpr int WTN = kSkB / WN;
-  static constexpr int BK = W == 8 ? 64 : 32;  // K depth of one schedule step
+  static constexpr int BK = 64;              // K depth of one schedule step
   static constexpr int CH = 8 * TN;          // f32x4 accumulator chunks per lane
 };
 
@@ -249,145 +249,6 @@ PZ_DEV void pp_mainloop(f32x4_t (&acc)[8][4], PZ_LDS char* smem, const PpOperand
   if (grp == 0) sk_barrier();
 }
 
-// ------------------------------------------------------------------ W = 4: the lab loop
-// 256x256 macro tile on FOUR waves (128x128 wave tiles = the whole AGPR file): 0.25 LDS reads per
-// MFMA. LDS ring of 4 32-deep slots filled by buffer-addressed LDS-DMA; fragments read one step
-// ahead into a second VGPR set; MFMAs, fragment reads and refill DMAs interleaved in 16 groups per
-// step. Correct and deterministic, but measured 0.70-0.75x the ping-pong on the step's shapes
-// (profiles/r5_gemm_bench_vs_hipblaslt.txt): one wave per SIMD has no partner to run while it
-// waits at the per-step barrier (SQ_WAIT_ANY 0.30-0.40 of its cycles, profiles/r5_pmc_sk.txt).
-constexpr int kSkW4BK = 32, kSkW4Op = kSkB * kSkW4BK * 2, kSkW4Slot = 2 * kSkW4Op, kSkW4NS = 4;
-constexpr int kSkW4Pieces = kSkW4Op / 1024 / 4;  // LDS-DMA instructions per wave, operand and step
-constexpr int kSkW4G = 2 * kSkW4Pieces;
-
-// One operand's LDS-DMA addressing for a unit. K-contiguous ([rows][K]): piece i of this wave =
-// 16 rows x 64 B; M/N-contiguous ([K][rows]): piece i = 2 k-rows x 512 B. The per-lane offsets
-// carry the read-side swizzle (linear LDS destination, permuted source).
-struct SkOperand {
-  i32x4_t rs;
-  uint32_t voff[2];    // per-lane byte offsets (M/N-contiguous: by piece parity)
-  uint32_t base;       // wave-uniform byte offset of this wave's piece 0 at the unit's first step
-  uint32_t pstep;      // bytes between the wave's consecutive pieces
-  uint32_t kstep;      // bytes per 32-deep K step
-};
-
-template <bool KC>
-PZ_DEV SkOperand sk_operand(i32x4_t rs, int64_t ld, int row0, int kb, int wave, int lane) {
-  SkOperand o;
-  o.rs = rs;
-  const uint32_t l = static_cast<uint32_t>(ld);
-  if constexpr (KC) {
-    const int r = lane >> 2;
-    const int chunk = (lane & 3) ^ swz_kc<32>(r);
-    o.voff[0] = o.voff[1] = (static_cast<uint32_t>(r) * l + static_cast<uint32_t>(chunk) * 8u) * 2u;
-    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(row0 + wave * 4 * 16) * l + static_cast<uint32_t>(kb) * kSkW4BK) * 2u);
-    o.pstep = __builtin_amdgcn_readfirstlane(16u * l * 2u);
-    o.kstep = kSkW4BK * 2;
-  } else {
-#pragma unroll
-    for (int par = 0; par < 2; ++par) {
-      const int kr = wave * 8 + 2 * par + (lane >> 5);
-      const int chunk = (lane & 31) ^ swz_mn(kr);
-      o.voff[par] = (static_cast<uint32_t>(lane >> 5) * l + static_cast<uint32_t>(chunk) * 8u) * 2u;
-    }
-    o.base = __builtin_amdgcn_readfirstlane((static_cast<uint32_t>(kb * kSkW4BK + wave * 8) * l + static_cast<uint32_t>(row0)) * 2u);
-    o.pstep = __builtin_amdgcn_readfirstlane(2u * l * 2u);
-    o.kstep = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(kSkW4BK) * l * 2u);
-  }
-  return o;
-}
-
-template <bool KC>
-PZ_DEV void sk_dma(const SkOperand& o, int i, int ks, uint32_t lds) {
-  const uint32_t voff = KC ? o.voff[0] : o.voff[i & 1];
-  blds16<0>(o.rs, voff, o.base + static_cast<uint32_t>(i) * o.pstep + static_cast<uint32_t>(ks) * o.kstep,
-            lds + static_cast<uint32_t>(i) * 1024u);
-}
-
-template <bool KC>
-PZ_DEV i16x8_t sk_frag(const PZ_LDS char* img, int wg, int f, int lane, uint32_t kc_lane) {
-  if constexpr (KC) return *reinterpret_cast<const PZ_LDS i16x8_t*>(img + (wg * 128 + f * 16) * (kSkW4BK * 2) + kc_lane);
-  else return frag_mn<kSkB>(img, wg * 128 + f * 16, 8 * (lane >> 4), lane);
-}
-
-struct SkFrag {
-  i16x8_t a[8];
-  i16x8_t b[8];
-};
-
-template <bool A_KC, bool B_KC>
-PZ_DEV void w4_mainloop(f32x4_t (&acc)[8][8], PZ_LDS char* smem, const GemmArgs& p, i32x4_t rs_a, i32x4_t rs_b,
-                        int m0, int n0, int kt0, int n, int wave, int lane) {
-  constexpr int NS = kSkW4NS;
-  const int wm = wave >> 1, wn = wave & 1;
-  const SkOperand oa = sk_operand<A_KC>(rs_a, p.lda, m0, kt0, wave, lane);
-  const SkOperand ob = sk_operand<B_KC>(rs_b, p.ldb, n0, kt0, wave, lane);
-  const uint32_t lds0 = lds_addr(smem);
-  const uint32_t wpiece = static_cast<uint32_t>(wave) * kSkW4Pieces * 1024u;
-  const uint32_t kc_lane = static_cast<uint32_t>((lane & 15) * (kSkW4BK * 2) + (((lane >> 4) ^ swz_kc<32>(lane & 15)) << 4));
-  auto dma_step = [&](int ks) __attribute__((always_inline)) {
-    const uint32_t sb = lds0 + static_cast<uint32_t>(ks % NS) * kSkW4Slot + wpiece;
-#pragma unroll
-    for (int i = 0; i < kSkW4Pieces; ++i) sk_dma<A_KC>(oa, i, ks, sb);
-#pragma unroll
-    for (int i = 0; i < kSkW4Pieces; ++i) sk_dma<B_KC>(ob, i, ks, sb + kSkW4Op);
-  };
-  auto read_all = [&](SkFrag& f, int ks) __attribute__((always_inline)) {
-    const PZ_LDS char* img = smem + (ks % NS) * kSkW4Slot;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f.b[j] = sk_frag<B_KC>(img + kSkW4Op, wn, j, lane, kc_lane);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) f.a[i] = sk_frag<A_KC>(img, wm, i, lane, kc_lane);
-  };
-  // step h: 64 MFMAs on `cur`; rd: read step h+1 into `nxt`; dm: refill slot h % NS with step
-  // h+NS. ONE body with scalar guards (three specialised bodies kept every fragment set live)
-  auto step = [&](const SkFrag& cur, SkFrag& nxt, int h) __attribute__((always_inline)) {
-    const bool rd = h + 1 < n, dm = h + NS < n;
-    const PZ_LDS char* img = smem + ((h + 1) % NS) * kSkW4Slot;
-    const uint32_t sb = lds0 + static_cast<uint32_t>(h % NS) * kSkW4Slot + wpiece;
-    __builtin_amdgcn_sched_barrier(0);
-    static_for<16>([&](auto gc) {
-      constexpr int g = decltype(gc)::value;
-      static_for<4>([&](auto qc) {
-        constexpr int idx = 4 * g + decltype(qc)::value, i = idx >> 3, j = idx & 7;
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, cur.b[j]),
-                                                            __builtin_bit_cast(bf16x8_t, cur.a[i]), acc[i][j], 0, 0, 0);
-      });
-      if (rd) {
-        if constexpr (g < 8) nxt.b[g] = sk_frag<B_KC>(img + kSkW4Op, wn, g, lane, kc_lane);
-        else nxt.a[g - 8] = sk_frag<A_KC>(img, wm, g - 8, lane, kc_lane);
-      }
-      if constexpr ((g & 1) == 0) {
-        constexpr int pc = g / 2;
-        if (dm) {
-          if constexpr (pc < kSkW4Pieces) sk_dma<A_KC>(oa, pc, h + NS, sb);
-          else sk_dma<B_KC>(ob, pc - kSkW4Pieces, h + NS, sb + kSkW4Op);
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    });
-    if (h + 2 < n) {  // step h+2 landed for every wave; every read of slot (h+1) % NS retired
-      wait_newer<kSkW4G, NS - 2>(min(h + NS, n - 1) - (h + 2));
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      sk_barrier();
-    }
-  };
-  wait_vm<0>();
-  sk_barrier();
-  const int pre = min(NS, n);
-  for (int s = 0; s < pre; ++s) dma_step(s);
-  wait_newer<kSkW4G, NS - 2>(max(pre - 2, 0));  // steps 0 and 1 landed
-  sk_barrier();
-  SkFrag f0, f1;
-  read_all(f0, 0);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  sk_barrier();  // every wave read slot 0 before step 0 refills it
-  for (int h = 0; h < n; h += 2) {
-    step(f0, f1, h);
-    if (h + 1 < n) step(f1, f0, h + 1);
-  }
-}
-
 // fp32-output epilogue (weight gradients): alpha, bias, accumulate; 16-B stores
 template <int W>
 PZ_DEV void sk_store_f32(const GemmArgs& p, f32x4_t (&acc)[8][SkGeo<W>::TN], int m0, int n0, int wm, int wn, int lane) {
@@ -469,7 +330,7 @@ gemm_sk_kernel(const SkArgs g) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < G::TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
-    if constexpr (W == 8) {
+    {
       const int tw = wave & 3;
       // (the staging lane offsets: recomputed per unit, ~20 VALU ops, rather than held live
       // through the fold and the epilogue)
@@ -480,7 +341,6 @@ gemm_sk_kernel(const SkArgs g) {
       const PpOperand ob = pp_operand<B_KC>(vb, static_cast<uint32_t>(p.ldb), n0, kb, tw);
       pp_mainloop<A_KC, B_KC>(acc, smem, oa, ob, buf_rsrc(p.A), buf_rsrc(p.B), ke - kb, wave, lane);
     }
-    else w4_mainloop<A_KC, B_KC>(acc, smem, p, buf_rsrc(p.A), buf_rsrc(p.B), m0, n0, kb, ke - kb, wave, lane);
 
     PZ_SK_STAMP(unit, 1);
     if (slab >= 0) {
@@ -598,15 +458,12 @@ int sk_epi_kind(const GemmArgs& p) {
   return -1;
 }
 
-// wave count of the engine a GEMM runs on: 8 (ping-pong) unless engine 3 asks for the 4-wave lab
-int sk_waves(const GemmArgs& p) { return p.engine == 3 ? 4 : 8; }
-
 SkSched sk_plan(const GemmArgs* probs, int n) {
   SkSched s{};
   s.nprob = n;
   s.tiles0 = (probs[0].M / kSkB) * (probs[0].N / kSkB);
   s.tiles = s.tiles0 + (n > 1 ? (probs[1].M / kSkB) * (probs[1].N / kSkB) : 0);
-  const int bk = sk_waves(probs[0]) == 8 ? SkGeo<8>::BK : SkGeo<4>::BK;
+  constexpr int bk = SkGeo<8>::BK;
   s.iters = probs[0].K / bk;
   const int cus = device_cus();
   int grid = probs[0].cus > 0 ? std::min(probs[0].cus, cus) : cus;
@@ -640,12 +497,6 @@ hipError_t sk_launch(const SkArgs& a, hipStream_t st) {
 
 hipError_t sk_dispatch(const SkArgs& a, int ek, hipStream_t st) {
   const GemmArgs& p = a.p[0];
-  if (sk_waves(p) == 4) {  // lab engine: plain stores only
-    if (ek != EK_STORE) return hipErrorInvalidValue;
-    if (p.a_kc && !p.b_kc) return sk_launch<true, false, uint16_t, EK_STORE, 4>(a, st);
-    if (p.a_kc && p.b_kc) return sk_launch<true, true, uint16_t, EK_STORE, 4>(a, st);
-    return sk_launch<false, false, uint16_t, EK_STORE, 4>(a, st);
-  }
   if (p.a_kc && !p.b_kc) {  // forward X · W[in, out]
     switch (ek) {
       case EK_STORE: return sk_launch<true, false, uint16_t, EK_STORE, 8>(a, st);
@@ -696,7 +547,8 @@ bool deterministic() {
 bool sk_eligible(const GemmArgs& p) {
   if (p.force_generic || p.in_dtype != DT_BF16 || (p.out_dtype != DT_BF16 && p.out_dtype != DT_F32)) return false;
   if (p.bias64 != nullptr || p.colsum64 != nullptr) return false;
-  const int bk = sk_waves(p) == 8 ? SkGeo<8>::BK : SkGeo<4>::BK;
+  constexpr int bk = SkGeo<8>::BK;
+  if (p.engine == 3) return false;  // (round-5 lab loop: tools/gemm_w4_lab.hip)
   if (p.M <= 0 || p.N <= 0 || p.M % kSkB != 0 || p.N % kSkB != 0 || p.K % bk != 0 || p.K < 2 * bk) return false;
   if (!p.a_kc && p.b_kc) return false;  // (no MLP GEMM has this layout)
   auto al16 = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
@@ -711,7 +563,7 @@ bool sk_eligible(const GemmArgs& p) {
                             (reinterpret_cast<uintptr_t>(p.out8) & 7) != 0 || p.out8_qscale == nullptr))
     return false;
   const int ek = sk_epi_kind(p);
-  return ek >= 0 && (sk_waves(p) == 8 || ek == EK_STORE);
+  return ek >= 0;
 }
 
 int sk_tickets(const GemmArgs* probs, int n) { return sk_plan(probs, n).sk_tiles; }

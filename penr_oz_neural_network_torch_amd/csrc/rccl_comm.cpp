@@ -7,6 +7,12 @@
 //                          --event[ticket]-->  (returns the ticket)
 //   rccl_wait(h, ticket)   the CURRENT stream waits for that bucket (no host blocking) — the
 //                          optimizer side stream waits for exactly the buckets it updates
+//   rccl_reduce_scatter(h, full, shard) / rccl_all_gather(h, shard, full)
+//                          the sharded optimizer (ZeRO-1, engine/zero.py): each rank receives the
+//                          SUM of its 1/W slice of a gradient bucket, updates only that slice of
+//                          the fp32 master / Adam moments, and the updated bf16 weight slices are
+//                          gathered back into every rank's GEMM copy — the same ring bytes as one
+//                          all-reduce, 1/W of the optimizer's HBM traffic per rank
 //
 // so a layer's gradient bucket crosses xGMI while the following layers' backward GEMMs run, and
 // nothing but stream waits orders the update behind it (the ordering ProcessGroupNCCL's
@@ -33,6 +39,8 @@ struct Api {
   ncclResult_t (*get_unique_id)(ncclUniqueId*);
   ncclResult_t (*init_rank)(ncclComm_t*, int, ncclUniqueId, int);
   ncclResult_t (*all_reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*reduce_scatter)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t, hipStream_t);
+  ncclResult_t (*all_gather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t);
   ncclResult_t (*destroy)(ncclComm_t);
   ncclResult_t (*async_error)(ncclComm_t, ncclResult_t*);
   const char* (*error_string)(ncclResult_t);
@@ -54,6 +62,8 @@ const Api& api() {
     resolve(lib, "ncclGetUniqueId", x.get_unique_id);
     resolve(lib, "ncclCommInitRank", x.init_rank);
     resolve(lib, "ncclAllReduce", x.all_reduce);
+    resolve(lib, "ncclReduceScatter", x.reduce_scatter);
+    resolve(lib, "ncclAllGather", x.all_gather);
     resolve(lib, "ncclCommDestroy", x.destroy);
     resolve(lib, "ncclCommGetAsyncError", x.async_error);
     resolve(lib, "ncclGetErrorString", x.error_string);
@@ -188,34 +198,75 @@ int64_t init_op(const at::Tensor& id, int64_t nranks, int64_t rank, bool high_pr
   return add_comm(std::move(c));
 }
 
-int64_t all_reduce_op(int64_t h, const at::Tensor& t) {
+enum class Coll { AllReduce, ReduceScatter, AllGather };
+
+// One collective on the comm stream, fenced to the current stream by events. `send` / `recv`:
+// all-reduce in place (send == recv); reduce-scatter full [W * n] -> shard [n]; all-gather shard
+// [n] -> full [W * n] (in place when the shard is the rank's slice of the full buffer). Proxy
+// communicators hold the collective's workgroups for the ring time instead: all-reduce 2 (W-1)/W
+// x bytes, reduce-scatter / all-gather (W-1)/W x the FULL buffer's bytes, at the bus bandwidth.
+int64_t collective(int64_t h, Coll kind, const at::Tensor& send, const at::Tensor& recv) {
   const std::shared_ptr<Comm> cp = get(h);
   Comm& c = *cp;
   std::lock_guard<std::mutex> lock(c.mu);
   TORCH_CHECK(!c.closed, "pz rccl: communicator destroyed");
-  TORCH_CHECK(t.is_cuda() && t.device().index() == c.device, "pz rccl: tensor must live on the communicator's GPU");
-  TORCH_CHECK(t.is_contiguous(), "pz rccl: contiguous buckets only");
+  for (const at::Tensor* t : {&send, &recv}) {
+    TORCH_CHECK(t->is_cuda() && t->device().index() == c.device, "pz rccl: tensor must live on the communicator's GPU");
+    TORCH_CHECK(t->is_contiguous(), "pz rccl: contiguous buckets only");
+  }
+  TORCH_CHECK(send.scalar_type() == recv.scalar_type(), "pz rccl: send / recv dtypes differ");
+  const at::Tensor& full = kind == Coll::AllGather ? recv : send;
+  const at::Tensor& part = kind == Coll::AllGather ? send : recv;
+  // (a proxy communicator models `proxy_world` ranks on one GPU: the caller shards for that world
+  // as virtual rank 0, so any whole number of shards per buffer)
+  if (kind != Coll::AllReduce)
+    TORCH_CHECK(c.proxy ? (part.numel() > 0 && full.numel() % part.numel() == 0) : full.numel() == part.numel() * c.nranks,
+                "pz rccl: the full buffer must hold ", c.proxy ? c.proxy_world : c.nranks, " shards of ", part.numel(),
+                " elements (got ", full.numel(), ")");
   const int64_t ticket = c.next++;
-  if (t.numel() == 0) {
+  if (full.numel() == 0) {
     PZ_HIP_OK(hipEventRecord(c.done[ticket % kRing], c10::hip::getCurrentHIPStream(c.device).stream()));
     return ticket;
   }
   const hipStream_t cur = c10::hip::getCurrentHIPStream(c.device).stream();
   PZ_HIP_OK(hipEventRecord(c.ready, cur));
   PZ_HIP_OK(hipStreamWaitEvent(c.stream.stream(), c.ready, 0));
-  if (c.proxy) {  // ring all-reduce time: 2 (W-1)/W x bytes at the bus bandwidth
-    const double bytes = static_cast<double>(t.numel()) * t.element_size();
-    const double us = 2.0 * (c.proxy_world - 1) / c.proxy_world * bytes / (c.proxy_gbps * 1e3);
+  if (c.proxy) {
+    const double bytes = static_cast<double>(full.numel()) * full.element_size();
+    const double f = (kind == Coll::AllReduce ? 2.0 : 1.0) * (c.proxy_world - 1) / c.proxy_world;
+    const double us = f * bytes / (c.proxy_gbps * 1e3);
     const double step_us = 4096.0 * c.proxy_wgs / (c.proxy_gbps * 1e3);
     PZ_HIP_OK(pz::comm_proxy(c.scratch.data_ptr(), c.proxy_wgs, 64 << 10, us, step_us, c.stream.stream()));
+    // virtual rank 0's slice moves (its sum over one real rank is itself)
+    if (send.data_ptr() != recv.data_ptr() && kind != Coll::AllReduce)
+      PZ_HIP_OK(hipMemcpyAsync(recv.data_ptr(), send.data_ptr(), part.numel() * part.element_size(),
+                               hipMemcpyDeviceToDevice, c.stream.stream()));
+  } else if (kind == Coll::AllReduce) {
+    PZ_NCCL_CHECK(api().all_reduce(send.data_ptr(), recv.data_ptr(), static_cast<size_t>(recv.numel()), nccl_type(recv),
+                                   ncclSum, c.comm, c.stream.stream()));
+  } else if (kind == Coll::ReduceScatter) {
+    PZ_NCCL_CHECK(api().reduce_scatter(send.data_ptr(), recv.data_ptr(), static_cast<size_t>(recv.numel()),
+                                       nccl_type(recv), ncclSum, c.comm, c.stream.stream()));
   } else {
-    PZ_NCCL_CHECK(api().all_reduce(t.data_ptr(), t.data_ptr(), static_cast<size_t>(t.numel()), nccl_type(t), ncclSum,
+    PZ_NCCL_CHECK(api().all_gather(send.data_ptr(), recv.data_ptr(), static_cast<size_t>(send.numel()), nccl_type(send),
                                    c.comm, c.stream.stream()));
   }
-  // the caching allocator must not hand the bucket's memory out again before the comm stream is done
-  c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(), c.stream);
+  // the caching allocator must not hand the buffers' memory out again before the comm stream is done
+  c10::hip::HIPCachingAllocator::recordStream(send.storage().data_ptr(), c.stream);
+  if (recv.data_ptr() != send.data_ptr())
+    c10::hip::HIPCachingAllocator::recordStream(recv.storage().data_ptr(), c.stream);
   PZ_HIP_OK(hipEventRecord(c.done[ticket % kRing], c.stream.stream()));
   return ticket;
+}
+
+int64_t all_reduce_op(int64_t h, const at::Tensor& t) { return collective(h, Coll::AllReduce, t, t); }
+
+int64_t reduce_scatter_op(int64_t h, const at::Tensor& full, const at::Tensor& shard) {
+  return collective(h, Coll::ReduceScatter, full, shard);
+}
+
+int64_t all_gather_op(int64_t h, const at::Tensor& shard, const at::Tensor& full) {
+  return collective(h, Coll::AllGather, shard, full);
 }
 
 void wait_op(int64_t h, int64_t ticket) {
@@ -255,6 +306,8 @@ TORCH_LIBRARY_FRAGMENT(pz, m) {
   m.def("rccl_init(Tensor uid, int nranks, int rank, bool high_priority, int cu_count=0) -> int");
   m.def("rccl_proxy_init(int world, int wgs, float gbps, int cu_count=0, bool high_priority=False) -> int");
   m.def("rccl_all_reduce(int comm, Tensor(a!) t) -> int");
+  m.def("rccl_reduce_scatter(int comm, Tensor full, Tensor(a!) shard) -> int");
+  m.def("rccl_all_gather(int comm, Tensor shard, Tensor(a!) full) -> int");
   m.def("rccl_wait(int comm, int ticket) -> ()");
   m.def("rccl_destroy(int comm) -> ()");
 }
@@ -264,6 +317,8 @@ TORCH_LIBRARY_IMPL(pz, CompositeExplicitAutograd, m) {
   m.impl("rccl_init", TORCH_FN(init_op));
   m.impl("rccl_proxy_init", TORCH_FN(proxy_init_op));
   m.impl("rccl_all_reduce", TORCH_FN(all_reduce_op));
+  m.impl("rccl_reduce_scatter", TORCH_FN(reduce_scatter_op));
+  m.impl("rccl_all_gather", TORCH_FN(all_gather_op));
   m.impl("rccl_wait", TORCH_FN(wait_op));
   m.impl("rccl_destroy", TORCH_FN(destroy_op));
 }

@@ -76,10 +76,12 @@ class FusedOptimizer:
         # epoch's lr / bias corrections from the table instead of the baked-in scalars
         self.graph_tables = None
 
-    def define_groups(self, keys: list[int]) -> None:
+    def define_groups(self, keys: list[int], rest_stats: bool = True) -> None:
         """Split the update into launches: one per listed segment offset (a dense weight whose
         gradient bucket is ready early in the backward) plus one for every other segment. Each
-        launch is the same fused kernel over its own packed segment table."""
+        launch is the same fused kernel over its own packed segment table. ``rest_stats=False``:
+        the rest group adds nothing to the per-weight statistics (sharded optimizer, ranks > 0:
+        rank 0's replicated copy counts once in the all-reduced sums)."""
         dev = self.store.device
         by_off = {s.offset: s for s in self.store.segments}
         rest = sorted((s for s in self.store.segments if s.offset not in set(keys)), key=lambda s: s.offset)
@@ -92,15 +94,32 @@ class FusedOptimizer:
                 starts.append(acc)
                 acc += b
             block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
+            stats = rest_stats or key != "rest"
             for parity in range(len(self.shadow_sets)):
-                self.groups[(key, parity)] = (self._pack(segs, parity), block_seg, len(segs), acc)
+                self.groups[(key, parity)] = (self._pack(segs, parity, stats), block_seg, len(segs), acc)
 
-    def _pack(self, segs, parity: int) -> torch.Tensor:
+    def define_slice(self, key, seg, lo: int, numel: int, shadows: list[torch.Tensor | None],
+                     grad16: torch.Tensor) -> None:
+        """A group updating only elements ``[lo, lo + numel)`` of weight segment ``seg`` (the
+        sharded optimizer's slice of this rank): masters / moments at ``seg.offset + lo``, the
+        gradient from ``grad16`` (the reduce-scattered bf16 slice), per parity the shadow slice
+        ``shadows[parity]`` it writes. Same statistics slot as the whole weight (its sums are
+        all-reduced over the ranks before step_finalize)."""
+        dev = self.store.device
+        blocks = max(1, math.ceil(numel / ELEMS_PER_BLOCK))
+        block_seg = torch.tensor([0], dtype=torch.int64, device=dev)
+        for parity in range(len(self.shadow_sets)):
+            pack = torch.ops.pz.pack_segments(
+                [seg.offset + lo], [numel], [int(seg.is_weight)], [self.slot_of.get(id(seg), -1)],
+                [shadows[parity]], [grad16], [0], [None], [None], [None], [None]).to(dev)
+            self.groups[(key, parity)] = (pack, block_seg, 1, blocks)
+
+    def _pack(self, segs, parity: int, stats: bool = True) -> torch.Tensor:
         sh, am, w8 = self.shadow_sets[parity], self.amax_sets[parity], self.w8_sets[parity]
         trip = [w8.get(s.offset, (None, None, None)) for s in segs]
         return torch.ops.pz.pack_segments(
             [s.offset for s in segs], [s.numel for s in segs], [int(s.is_weight) for s in segs],
-            [self.slot_of.get(id(s), -1) for s in segs], [sh.get(s.offset) for s in segs],
+            [self.slot_of.get(id(s), -1) if stats else -1 for s in segs], [sh.get(s.offset) for s in segs],
             [self.grads16.get(s.offset) for s in segs], self._zero_flags(segs),
             [am.get(s.offset) for s in segs], [t[0] for t in trip], [t[1] for t in trip],
             [t[2] for t in trip]).to(self.store.device)

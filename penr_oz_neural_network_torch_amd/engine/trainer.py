@@ -43,6 +43,7 @@ from ..parallel.dist import DataParallelContext, get_context
 from .events import StreamEvents
 from .fp8_policy import Fp8Policy
 from .optim import FusedOptimizer
+from .zero import ZeroShards
 
 ROW_PAD = 64  # batch rows padded to the GEMM K-tile so dW = XᵀdZ stays on the MFMA path
 _M32 = 0xFFFFFFFF
@@ -192,10 +193,27 @@ class FusedTrainer(Fp8Policy):
         # gradient is reduced, even while the dX GEMM of the same layer still reads it
         self.shadow_sets: list[dict[int, torch.Tensor]] = [{}, {}]
         self.parity = 0
+        # SHARDED OPTIMIZER under data parallelism (ZeRO-1, engine/zero.py; PZ_ZERO=0 replicates):
+        # every dense weight's bf16 gradient is reduce-scattered, each rank updates its 1/N slice of
+        # the fp32 master and Adam moments, and the bf16 GEMM copies are all-gathered in place —
+        # the xGMI bytes of one all-reduce, 1/N of the optimizer's work per rank. bf16 GEMM copies
+        # with bf16 gradient buckets and the overlapped update only (fp8 keeps replicated updates:
+        # its e4m3 copies and weight amax are written by the update itself). PZ_ZERO=1 forces it
+        # (e.g. a forced 1-rank RCCL group, or the one-GPU collective proxy's modelled world).
+        zmode = os.environ.get("PZ_ZERO", "auto")
+        self.zero: ZeroShards | None = None
+        if ((zmode == "1" or (zmode == "auto" and self.ctx.world_size > 1)) and self.ctx.enabled
+                and model.precision.name == "bfloat16" and self.master == torch.float32
+                and os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
+                and os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower() in ("bf16", "bfloat16")):
+            self.zero = ZeroShards(self.ctx, [st.seg_w for st in self.stages if st.kind == "gemm"],
+                                   len(self.shadow_sets), self.dev)
+        self._zero_ar = False  # record step: all-reduced dense gradients (the record needs them whole)
         for st in self.stages:
             if st.kind == "gemm" and self.compute != self.master:
-                for sset in self.shadow_sets:
-                    sset[st.seg_w.offset] = torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute)
+                for par, sset in enumerate(self.shadow_sets):
+                    sset[st.seg_w.offset] = (self.zero.shadow_view(st.seg_w.offset, par) if self.zero is not None
+                                             else torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute))
         # Data parallel: dense weight gradients are written by the dW GEMMs straight in bf16 and
         # all-reduced in bf16 (half the xGMI bytes of fp32 — rings over xGMI are per-link bound,
         # SURVEY §5.8); the fused optimizer reads them back as fp32. Biases, BN, embeddings and
@@ -214,10 +232,12 @@ class FusedTrainer(Fp8Policy):
         policy = os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower()
         local16 = os.environ.get("PZ_GRAD_DTYPE", "bf16").lower() in ("bf16", "bfloat16")
         if self.compute == torch.bfloat16 and (local16 if not self.ctx.enabled else policy in ("bf16", "bfloat16")):
-            buf16 = torch.zeros(max(1, self.store.accum_offset), device=self.dev, dtype=torch.bfloat16)
+            buf16 = torch.zeros(max(1, self.store.accum_offset), device=self.dev, dtype=torch.bfloat16) \
+                if self.zero is None else None
             for st in self.stages:
                 if st.kind == "gemm":
-                    self.grads16[st.seg_w.offset] = self.store.view(st.seg_w, buf16)
+                    self.grads16[st.seg_w.offset] = (self.zero.grad_view(st.seg_w.offset) if self.zero is not None
+                                                     else self.store.view(st.seg_w, buf16))
         self.opt = FusedOptimizer(self.store, model.params, model.optimizer, self.shadow_sets, self.grads16)
         self.ctx.broadcast_(self.store.flat)  # identical replicas (rank 0 wins)
         for sset in self.shadow_sets:
@@ -334,7 +354,13 @@ class FusedTrainer(Fp8Policy):
             if cands:
                 self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
         self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
-        self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
+        if self.zero is not None:
+            # every dense weight by slices (the first layer's too, on this stream at the step end);
+            # the rest group is the small replicated parameters, whose statistics rank 0 reports
+            self.opt.define_groups(gemm_w, rest_stats=self.zero.rank == 0)
+            self.zero.define_groups(self.opt)
+        else:
+            self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
         # the side-stream updates of all layers but the first are queued together behind the last
         # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
@@ -349,8 +375,12 @@ class FusedTrainer(Fp8Policy):
         # better than the budgeted engine's split-tile hand-offs (profiles/r5_sk_stamps.txt)
         self._cus = 0
         self._cus_comm = 0
-        if self.ctx.enabled and self.ctx.comm_cus > 0:
-            self._cus_comm = torch.cuda.get_device_properties(self.dev).multi_processor_count - self.ctx.comm_cus
+        if self.ctx.enabled and self.ctx.comm_cus != 0:
+            n_cu = torch.cuda.get_device_properties(self.dev).multi_processor_count
+            if not 0 < self.ctx.comm_cus < n_cu:
+                raise ValueError(f"PZ_COMM_BUDGET={self.ctx.comm_cus}: the CUs left to the collectives must be "
+                                 f"in 1..{n_cu - 1} on this device ({n_cu} CUs)")
+            self._cus_comm = n_cu - self.ctx.comm_cus
         self._opt_done = None
         self._early_done = None  # previous step's side-stream updates (layers 2..n) + step_finalize done
         self._ov = None
@@ -504,13 +534,19 @@ class FusedTrainer(Fp8Policy):
             ready.record(main)
         with torch.cuda.stream(self.opt_stream):
             ready.wait(self.opt_stream)
+            gathers = []
             for key, handles, stages in items:
                 for h in handles:
                     self.ctx.wait_one(h)
-                self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
+                if self.zero is not None:  # this rank's slice, then the all-gather of the bf16 copy
+                    gathers.append(self.zero.update(self.opt, key, self.grads, l2, scale, 1 - self.parity))
+                else:
+                    self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
                 if self.fp8:
                     for st in stages:
                         self._refresh_fp8_weights(st, 1 - self.parity)
+            for h in gathers:  # (the side stream's completion event then covers the gathered copies)
+                self.ctx.wait_one(h)
 
     def _plan_relu_masks(self, rows_b: int) -> None:
         """ReLU GEMM stages feeding a GEMM stage keep a 1-bit mask of ``y > 0`` next to ``y``: the
@@ -687,6 +723,11 @@ class FusedTrainer(Fp8Policy):
         keys = self._keys(epoch)
         ops = torch.ops.pz
         main = torch.cuda.current_stream(self.dev)
+        self._zero_ar = record and self.zero is not None
+        if self._zero_ar:  # the record's weight gradients read whole fp32 masters (2 l2 W)
+            if self._opt_done is not None:  # (the previous step's side-stream slice updates)
+                self._opt_done.wait(main)
+            self.zero.gather_state(self.store.flat)
         overlap = self.overlap and not record
         # update-ratio sums only on progress epochs (row >= 0; captured steps: decided on device)
         self.opt.stats_every = (self._plan["every"] if self._plan else 1) if row == -2 else (1 if row >= 0 else 0)
@@ -780,7 +821,7 @@ class FusedTrainer(Fp8Policy):
         if self._pair_late is not None:
             sp, wp = self._pair_late
             self._pair_late = None
-            hp = self._bucket(wp)
+            hp = self._bucket_seg(sp.seg_w)
             handles.append(hp)
             self._side_pending.append((sp.seg_w.offset, [hp], [sp]))
         fin = dict(epoch_ctr=self.epoch_ctr, every=self._plan["every"] if self._plan else 1,
@@ -793,9 +834,21 @@ class FusedTrainer(Fp8Policy):
             # cross-stream wait), and it overlaps the side stream's still-running updates instead
             # of queueing behind them; step_finalize (side) waits for both
             pending, self._side_pending = self._side_pending, []
-            for h in list(self._late_handles) + [acc_h]:
-                self.ctx.wait_one(h)
+            gathers = []
+            if self.zero is not None:
+                # the first layer's slice on this stream, its all-gather overlapping the small
+                # replicated update behind it; the next forward (this stream) then reads it
+                for h in self._late_handles:
+                    self.ctx.wait_one(h)
+                gathers = [self.zero.update(self.opt, st.seg_w.offset, self.grads, l2, 1.0, 1 - self.parity)
+                           for st in self._late_stages]
+                self.ctx.wait_one(acc_h)
+            else:
+                for h in list(self._late_handles) + [acc_h]:
+                    self.ctx.wait_one(h)
             self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
+            for h in gathers:
+                self.ctx.wait_one(h)
             if self.fp8:
                 for st in self._late_stages:
                     self._refresh_fp8_weights(st, 1 - self.parity)
@@ -810,6 +863,8 @@ class FusedTrainer(Fp8Policy):
             with torch.cuda.stream(self.opt_stream):
                 if not pending:
                     rest_ev.wait(self.opt_stream)
+                if self.zero is not None:  # every slice's statistics partials, summed (exact)
+                    self.zero.all_reduce_stats(self.opt.stats[self.opt.cur])
                 self.opt.finalize(self.loss_slot, 1, l2, self.costs, -1 if capture else epoch, self.ratios, row,
                                   **fin)
                 ev = self.events.sync(capture)
@@ -829,7 +884,16 @@ class FusedTrainer(Fp8Policy):
         self.ctx.wait_all(handles)
         if record:
             self._finish_record(rec, batch, l2)
-        self.opt.step(self.grads, lr, l2, 1.0, 1 - self.parity)
+        if self.zero is not None:  # (record step: this rank's slices of the all-reduced gradients)
+            self.opt.begin_step(lr)
+            gathers = [self.zero.update(self.opt, off, self.grads, l2, 1.0, 1 - self.parity, source="ar")
+                       for off in self.zero.shards]
+            self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
+            for h in gathers:
+                self.ctx.wait_one(h)
+            self.zero.all_reduce_stats(self.opt.stats[self.opt.cur])
+        else:
+            self.opt.step(self.grads, lr, l2, 1.0, 1 - self.parity)
         self.parity = 1 - self.parity
         if self.fp8:
             self._refresh_fp8_weights(parity=self.parity)
@@ -1041,7 +1105,7 @@ class FusedTrainer(Fp8Policy):
                 PF.gemm(x8, False, g8, False, w_grad, scale_a=sx, scale_b=sg)
             else:
                 PF.gemm(x_in, False, g, False, w_grad)
-            mine = [self._bucket(w_grad)]
+            mine = [self._bucket_seg(st.seg_w)]
         handles.extend(mine)
         # the update writes the OTHER shadow set, but it is queued after this layer's dX GEMM
         # (the fp8 dX operand and the float32 policy's GEMMs read the weight itself)
@@ -1072,7 +1136,16 @@ class FusedTrainer(Fp8Policy):
         if ok is None:
             ok = self._y_dead_cache[key] = ((f8_0 is None) == (f8_p is None)
                                             and PF.gemm_pair_split(ops0[0], ops0[1], w0, opsp[0], opsp[1], wp) > 0)
+        sk_ok = False
         if ok and self._cus and f8_0 is None:
+            # the budgeted engine needs both problems stream-K eligible (a per-rank batch of 64 rows
+            # is one 64-deep K step: below the engine's two); otherwise the tiled pair runs
+            key_sk = key + ("sk",)
+            sk_ok = self._y_dead_cache.get(key_sk)
+            if sk_ok is None:
+                sk_ok = self._y_dead_cache[key_sk] = PF.gemm_pair_split(ops0[0], ops0[1], w0, opsp[0], opsp[1], wp,
+                                                                        engine=2) > 0
+        if sk_ok:
             # a bucket is on the wire: the pair's 256-workgroup grid would leave a straggler round
             # behind the CUs the collective holds (239 vs 133 us under the 16-workgroup proxy,
             # profiles/r5_step_timeline_proxy16.txt): both GEMMs as one stream-K schedule on the
@@ -1093,12 +1166,15 @@ class FusedTrainer(Fp8Policy):
         # two only, and the partner's all-reduce overlaps it (its weight is next read by the next
         # step's later forward GEMMs)
         self._pair_late = (sp, wp)
-        return self._bucket(w0)
+        return self._bucket_seg(st0.seg_w)
 
-    def _bucket(self, t):
-        """Start a gradient bucket's all-reduce; the GEMMs behind it get the comm CU budget."""
+    def _bucket_seg(self, seg):
+        """Start a weight's gradient bucket: reduce-scatter (sharded optimizer) or all-reduce (the
+        replicated update, and record steps); the GEMMs behind it get the comm CU budget."""
         self._cus = self._cus_comm
-        return self.ctx.all_reduce_async(t)
+        if self.zero is not None:
+            return self.zero.all_reduce(seg.offset) if self._zero_ar else self.zero.reduce_scatter(seg.offset)
+        return self.ctx.all_reduce_async(self._w_grad(seg))
 
     def _dw_update(self, st: Stage, x_in, g) -> None:
         """dW GEMM + the weight's optimizer update in one launch (fuse_opt). The update writes the
@@ -1240,6 +1316,8 @@ class FusedTrainer(Fp8Policy):
             self._last_ms = ms
         self._pending = []
         self.events.release(keep=self._start_event)  # (read: the step timestamps can go)
+        if self.zero is not None:  # whole masters and Adam moments for the checkpoint / inference
+            self.zero.gather_state(self.store.flat, self.opt.exp_avg, self.opt.exp_avg_sq)
         self.opt.sync_torch_state()
         return out
 

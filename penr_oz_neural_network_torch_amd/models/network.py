@@ -39,6 +39,52 @@ log = logging.getLogger("neural_net_model")
 
 CHECKPOINT_INTERVAL_S = 10.0   # reference neural_net_model.py:488
 MAX_PROGRESS_POINTS = 100      # reference :504
+
+
+class _SaveAgreement:
+    """Data parallel fused training: every rank must take the SAME record / checkpoint steps — a
+    record step issues its collectives in another order (no paired dW launch, all-reduced instead
+    of reduce-scattered buckets, the sharded optimizer's state gathers), so ranks whose 10 s
+    wall clocks disagree would pair mismatched collectives. Each rank's "10 s since the last save"
+    flag is summed over the ranks asynchronously; the step ``LAG`` epochs later acts on that
+    agreed value. The sum is read through pinned memory behind an event on a side stream: the
+    host waits for a two-step-old collective, never for the compute stream."""
+    LAG = 2
+
+    def __init__(self, ctx, device: torch.device):
+        self.ctx, self.device = ctx, device
+        self.side = torch.cuda.Stream(device=device) if device.type == "cuda" else None
+        self.queue: list = []
+        self.skip = 0
+
+    def decide(self, flag: bool) -> bool:
+        t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device=self.device)
+        h = self.ctx.all_reduce_async(t, exact=True)
+        if self.side is not None:
+            host = torch.empty(1, dtype=torch.float64, pin_memory=True)
+            self.side.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.side):
+                self.ctx.wait_one(h)
+                host.copy_(t, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.side)
+            t.record_stream(self.side)
+            self.queue.append((ev, host))
+        else:
+            self.ctx.wait_one(h)
+            self.queue.append((None, t))
+        if len(self.queue) <= self.LAG:
+            return False
+        ev, host = self.queue.pop(0)
+        if ev is not None:
+            ev.synchronize()
+        agreed = host.item() > 0.0
+        if self.skip:  # (flags raised before the last agreed save)
+            self.skip -= 1
+            return False
+        if agreed:
+            self.skip = self.LAG
+        return agreed
 MAX_COST_HISTORY = 100         # reference :539
 
 
@@ -512,8 +558,11 @@ class NeuralNetworkModel(MultiLayerPerceptron):
         trainer.begin(epochs, lr_schedule=lambda e: learning_rate * decay_rate ** e)
         every = max(1, epochs // MAX_PROGRESS_POINTS)
         last_saved = time.time()
+        agree = _SaveAgreement(trainer.ctx, trainer.dev) if trainer.ctx.enabled else None
         for epoch in range(epochs):
             long_training = time.time() - last_saved >= CHECKPOINT_INTERVAL_S
+            if agree is not None:
+                long_training = agree.decide(long_training)
             trainer.step(epoch, learning_rate * decay_rate ** epoch, sample_size, dropout_rate, l2_lambda,
                          want_ratios=epoch % every == 0, record=epoch + 1 == epochs or long_training)
             if long_training:

@@ -136,12 +136,13 @@ def gemm_pair(a0: Tensor, b0: Tensor, out0: Tensor, a1: Tensor, b1: Tensor, out1
                      scales0[0], scales0[1], scales1[0], scales1[1], ((engine & 3) << 2) | ((cus & 0xFFFF) << 16))
 
 
-def gemm_pair_split(a0: Tensor, b0: Tensor, out0: Tensor, a1: Tensor, b1: Tensor, out1: Tensor) -> int:
-    """Split-K factor the pair would run with, 0 when the two GEMMs cannot share a launch."""
+def gemm_pair_split(a0: Tensor, b0: Tensor, out0: Tensor, a1: Tensor, b1: Tensor, out1: Tensor, engine: int = 0) -> int:
+    """Split-K factor the pair would run with, 0 when the two GEMMs cannot share a launch
+    (``engine=2``: or when the persistent stream-K engine cannot run both)."""
     if a0.shape[0] != a1.shape[0]:
         return 0
     return int(_ops().gemm_pair_split(a0, b0, out0, a1, b1, out1, out0.shape[0], out0.shape[1], out1.shape[0],
-                                      out1.shape[1], a0.shape[0]))
+                                      out1.shape[1], a0.shape[0], engine))
 
 
 def relu_mask_shape(m: int, n: int) -> tuple[int, int]:

@@ -70,6 +70,53 @@ class DataParallelContext:
             work = dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         return (work, low, t if low is not None else None)
 
+    # ---- sharded optimizer (ZeRO-1, engine/zero.py) ------------------------------------------
+    @property
+    def shard_world(self) -> int:
+        """Ranks a sharded buffer is split over: the world, or the world a one-GPU collective
+        proxy models (its caller then runs as that world's rank 0)."""
+        return getattr(self.native, "model_world", None) or self.world_size
+
+    @property
+    def shard_rank(self) -> int:
+        return 0 if getattr(self.native, "model_world", None) else self.rank
+
+    def reduce_scatter_async(self, full: torch.Tensor, shard: torch.Tensor):
+        """Start a SUM reduce-scatter: this rank's ``shard`` receives the sum over the ranks of its
+        slice ``full[r*n:(r+1)*n]`` (``n = shard.numel()``). Same handle contract as
+        :meth:`all_reduce_async` (:meth:`wait_one` makes the current stream wait)."""
+        if not self.enabled:
+            return None
+        if self.native is not None:
+            return (_Ticket(self.native.handle, torch.ops.pz.rccl_reduce_scatter(self.native.handle, full, shard)),
+                    None, None)
+        if full.is_cuda and self.backend == "gloo":
+            # (gloo on device tensors: one all-reduce of a copy, then this rank's slice)
+            n = shard.numel()
+            tmp = full.clone()
+            work = dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            return (work, tmp[self.rank * n:(self.rank + 1) * n], shard)
+        work = dist.reduce_scatter_tensor(shard, full, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        return (work, None, None)
+
+    def all_gather_async(self, shard: torch.Tensor, full: torch.Tensor):
+        """Start an all-gather of every rank's ``shard`` into ``full`` (rank r's at
+        ``[r*n, (r+1)*n)``); ``shard`` may be this rank's slice of ``full`` (in place)."""
+        if not self.enabled:
+            return None
+        if self.native is not None:
+            return (_Ticket(self.native.handle, torch.ops.pz.rccl_all_gather(self.native.handle, shard, full)),
+                    None, None)
+        if full.is_cuda and self.backend == "gloo":
+            # (gloo on device tensors: zeros elsewhere + one exact sum all-reduce)
+            n = shard.numel()
+            tmp = torch.zeros_like(full)
+            tmp[self.rank * n:(self.rank + 1) * n].copy_(shard)
+            work = dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            return (work, tmp, full)
+        work = dist.all_gather_into_tensor(full, shard, group=self.group, async_op=True)
+        return (work, None, None)
+
     def all_reduce_(self, t: torch.Tensor) -> None:
         """Blocking exact SUM all-reduce in place (stream-ordered under RCCL): the synchronised
         batchnorm statistics, which the next kernel needs right away."""
@@ -169,6 +216,7 @@ class _ProxyComm:
         from ..ops import native
         native.require()
         env = os.environ.get
+        self.model_world = int(env("PZ_COMM_PROXY_WORLD", "8"))  # the sharded optimizer's modelled world
         self.handle = torch.ops.pz.rccl_proxy_init(int(env("PZ_COMM_PROXY_WORLD", "8")),
                                                    int(env("PZ_COMM_PROXY_WGS", "16")),
                                                    float(env("PZ_COMM_PROXY_GBPS", "150")),
@@ -193,6 +241,22 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def _default_backend(world: int) -> str:
+    """RCCL unless this node has fewer visible GPUs than ranks. Only an explicit LOCAL_WORLD_SIZE
+    (torchrun sets it) says how many ranks share this node; without one, WORLD_SIZE counts ranks on
+    every node (srun / mpirun with 16 ranks on 8-GPU nodes) and is no reason to leave RCCL."""
+    if not torch.cuda.is_available():
+        return "gloo"
+    lw = os.environ.get("LOCAL_WORLD_SIZE")
+    if lw is not None and int(lw) > torch.cuda.device_count():
+        import logging
+        logging.getLogger(__name__).warning(
+            "LOCAL_WORLD_SIZE=%s ranks share %d visible GPU(s): falling back to the gloo backend "
+            "(host collectives, much slower); set PZ_DIST_BACKEND to override", lw, torch.cuda.device_count())
+        return "gloo"
+    return "nccl"
+
+
 def init_from_env(backend: str | None = None) -> DataParallelContext:
     """Initialise the process group from torchrun's env vars (RANK / WORLD_SIZE / MASTER_*).
 
@@ -211,9 +275,7 @@ def init_from_env(backend: str | None = None) -> DataParallelContext:
             # PZ_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU; so
             # does a launch with more ranks on this node than visible GPUs (RCCL needs one GPU per
             # rank: "invalid usage" otherwise), e.g. torchrun --nproc-per-node 4 on a 1-GPU box
-            local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
-            backend = os.environ.get("PZ_DIST_BACKEND") or (
-                "nccl" if torch.cuda.is_available() and torch.cuda.device_count() >= local_world else "gloo")
+            backend = os.environ.get("PZ_DIST_BACKEND") or _default_backend(world)
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")) % torch.cuda.device_count())
 

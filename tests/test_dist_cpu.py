@@ -230,3 +230,71 @@ def test_native_communicator_plumbing_two_ranks(tmp_path):
         assert log["init"] == [(list(range(128)), 2, r, False)]
         assert log["reduced"] == 5 and [t for _, t in log["waited"]] == [0, 1, 2, 3, 4]
         assert log["closed"] == [7]
+
+
+def _zero_worker(rank, world, port, out_dir):
+    """The sharded optimizer's collectives and slice geometry on gloo / CPU tensors: uneven
+    weights over 3 ranks (a slice padded to 64 elements, a weight smaller than one slice)."""
+    os.environ.update(PZ_RENDEZVOUS_FILE=str(port), RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from penr_oz_neural_network_torch_amd.engine.params import Segment
+    from penr_oz_neural_network_torch_amd.engine.zero import ZeroShards
+    from penr_oz_neural_network_torch_amd.parallel import init_from_env, shutdown
+    ctx = init_from_env("gloo")
+    assert ctx.shard_world == world and ctx.shard_rank == rank
+    segs = [Segment(0, "weights", 0, 1000, (40, 25), True, True, 0),
+            Segment(2, "weights", 1024, 30, (5, 6), True, True, 2),
+            Segment(4, "weights", 1088, 4096, (64, 64), True, True, 4)]
+    z = ZeroShards(ctx, segs, 2, torch.device("cpu"))
+    got = {}
+    for seg in segs:
+        sh = z.shards[seg.offset]
+        assert sh.s % 64 == 0 and sh.s * world >= sh.n and sh.lo == rank * sh.s
+        # reduce-scatter: rank r's gradient = (r + 1) * (i % 16) -> slice sum = 6 * (i % 16) (3 ranks)
+        z.grad_view(seg.offset).copy_((torch.arange(sh.n, dtype=torch.float32) % 16 * (rank + 1)).view(seg.shape))
+        ctx.wait_one(z.reduce_scatter(seg.offset))
+        got[f"rs{seg.offset}"] = sh.g_shard[:sh.cnt].float().clone()
+        # in-place all-gather of a shadow parity: every rank writes only its slice
+        full = sh.sh_full[1]
+        full.zero_()
+        full[sh.lo:sh.lo + sh.cnt] = torch.arange(sh.lo, sh.lo + sh.cnt, dtype=torch.float32).to(full.dtype)
+        ctx.wait_one(ctx.all_gather_async(full[sh.lo:sh.lo + sh.s], full))
+        got[f"ag{seg.offset}"] = z.shadow_view(seg.offset, 1).float().clone()
+    # gather_state: each rank's masters / moments are current on its own slices only
+    flat = torch.full((1088 + 4096,), -1.0)
+    m = torch.full_like(flat, -2.0)
+    for seg in segs:
+        sh = z.shards[seg.offset]
+        flat[seg.offset + sh.lo:seg.offset + sh.lo + sh.cnt] = float(rank)
+        m[seg.offset + sh.lo:seg.offset + sh.lo + sh.cnt] = float(10 + rank)
+    z.gather_state(flat, m, None)
+    got["flat"], got["m"] = flat, m
+    got["cnt"] = [z.shards[s.offset].cnt for s in segs]
+    torch.save(got, os.path.join(out_dir, f"z{rank}.pt"))
+    ctx.barrier()
+    shutdown()
+
+
+def test_gloo_sharded_optimizer_collectives_three_ranks(tmp_path):
+    world = 3
+    mp.start_processes(_zero_worker, args=(world, str(tmp_path / "rdv"), str(tmp_path)), nprocs=world,
+                       start_method="spawn")
+    outs = [torch.load(tmp_path / f"z{r}.pt", weights_only=True) for r in range(world)]
+    sizes = {0: 1000, 1024: 30, 1088: 4096}
+    for off, n in sizes.items():
+        s = -(-(-(-n // world)) // 64) * 64
+        cov = sum(o["cnt"][list(sizes).index(off)] for o in outs)
+        assert cov == n  # the slices tile the weight exactly
+        for r, o in enumerate(outs):
+            lo = r * s
+            cnt = max(0, min(s, n - lo))
+            want = torch.arange(lo, lo + cnt, dtype=torch.float32) % 16 * 6  # (1 + 2 + 3) x, exact in bf16
+            assert torch.equal(o[f"rs{off}"], want)
+            assert torch.equal(o[f"ag{off}"].reshape(-1), torch.arange(n, dtype=torch.float32).bfloat16().float())
+            # the gathered master: each element holds its owner's rank
+            owner = torch.arange(n) // s
+            assert torch.equal(o["flat"][off:off + n], owner.float())
+            assert torch.equal(o["m"][off:off + n], owner.float() + 10)
+    for o in outs[1:]:
+        assert torch.equal(o["flat"], outs[0]["flat"]) and torch.equal(o["m"], outs[0]["m"])
+    # the padding between segments is untouched
+    assert torch.equal(outs[0]["flat"][1000:1024], torch.full((24,), -1.0))

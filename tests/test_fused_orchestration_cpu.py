@@ -17,7 +17,8 @@ class FakeTrainer:
 
     def __init__(self, model):
         self.model = model
-        self.ctx = types.SimpleNamespace(world_size=1)
+        self.ctx = types.SimpleNamespace(world_size=1, enabled=False)
+        self.dev = torch.device("cpu")
         self.steps, self._pending, self.step_ms, self._rec = [], [], {}, None
 
     def load_data(self, data):
@@ -59,8 +60,8 @@ class FakeTrainer:
     def record(self):
         return self._rec
 
-    def close(self):
-        self.closed = True
+    def close(self, ok=True):
+        self.closed = ok
 
 
 def test_fused_orchestration_schedule_progress_and_stats(models_tmpdir, monkeypatch):
@@ -119,3 +120,21 @@ def test_fused_engine_declines_cpu_models_and_gpu_requests_fall_back(models_tmpd
     assert m._fused_trainer() is None  # CPU models train under autograd (reference semantics)
     g = NeuralNetworkModel("want_gpu", [4, 8, 2], activation_algos=["relu", "softmax"], device="cuda")
     assert g.device.type == ("cuda" if torch.cuda.is_available() else "cpu")
+
+
+def test_data_parallel_save_agreement_lags_and_skips():
+    """Data parallel fused training: each rank's 10 s flag is summed over the ranks and acted on
+    LAG steps later (same decision everywhere); flags raised before an agreed save are dropped."""
+    class Ctx:  # one rank; a "sum" over ranks is the flag itself
+        def all_reduce_async(self, t, exact=False):
+            assert exact
+            return None
+
+        def wait_one(self, h):
+            pass
+
+    agree = network_mod._SaveAgreement(Ctx(), torch.device("cpu"))
+    flags = [False, True, True, True, False, False, False, True, False, False, False]
+    got = [agree.decide(f) for f in flags]
+    # step e acts on step e-2's flag; the two flags in flight at a save are skipped
+    assert got == [False, False, False, True, False, False, False, False, False, True, False]

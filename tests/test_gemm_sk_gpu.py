@@ -172,16 +172,14 @@ def test_head_colsums_are_deterministic(native_lib, B, C):
     assert (sums[0][0].double() - ref.sum(0)).abs().max().item() <= 1e-3 * ref.abs().max().item() * math.sqrt(B)
 
 
-@pytest.mark.parametrize("layout", ["fwd", "dx", "dw"])
-def test_sk_four_wave_lab_loop(native_lib, layout):
-    """engine 3: the stream-K engine on its 4-wave 128x128-wave-tile lab loop (plain stores)."""
-    a_kc, b_kc = {"fwd": (True, False), "dx": (True, True), "dw": (False, False)}[layout]
-    M, N, K = 2048, 2048, 1024
-    a, b, ref = _ops(M, N, K, a_kc, b_kc, 5)
-    for cus in (256, 200):
-        out = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
-        PF.gemm(a, a_kc, b, b_kc, out, engine=3, cus=cus)
-        _close(out, ref, K)
+def test_sk_lab_engine_is_not_in_the_library(native_lib):
+    """engine 3 (the round-5 4-wave lab loop) moved to tools/gemm_w4_lab.hip: the library refuses
+    it loudly instead of silently running another engine."""
+    M, N, K = 512, 512, 256
+    a, b, _ = _ops(M, N, K, True, False, 5)
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError, match="stream-K engine cannot run"):
+        PF.gemm(a, True, b, False, out, engine=3)
 
 
 @pytest.mark.parametrize("cus", [256, 240, 100])

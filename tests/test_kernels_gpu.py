@@ -728,6 +728,24 @@ def test_gemm_pair_fp8_and_ineligible(native_lib):
                               torch.randn(K // 2, n1, device=DEV).to(torch.bfloat16), c1) == 0
 
 
+def test_gemm_pair_stream_k_eligibility_at_one_k_step(native_lib):
+    """a 64-row per-rank batch is ONE 64-deep K step — the tiled pair takes it, the
+    stream-K engine (>= two steps) does not, and gemm_pair_split(engine=2) says so instead of the
+    budgeted launch raising mid-step."""
+    K, (m0, n0), (m1, n1) = 64, (1024, 4096), (4096, 1024)
+    bf = torch.bfloat16
+    x0, g0 = torch.randn(K, m0, device=DEV).to(bf), torch.randn(K, n0, device=DEV).to(bf)
+    x1, g1 = torch.randn(K, m1, device=DEV).to(bf), torch.randn(K, n1, device=DEV).to(bf)
+    c0 = torch.empty(m0, n0, device=DEV, dtype=bf)
+    c1 = torch.empty(m1, n1, device=DEV, dtype=bf)
+    assert PF.gemm_pair_split(x0, g0, c0, x1, g1, c1) > 0
+    assert PF.gemm_pair_split(x0, g0, c0, x1, g1, c1, engine=2) == 0
+    PF.gemm_pair(x0, g0, c0, x1, g1, c1)
+    for c, x, g in ((c0, x0, g0), (c1, x1, g1)):
+        ref = x.double().t() @ g.double()
+        assert (c.double() - ref).abs().max().item() <= 2.0 ** -7 * ref.abs().max().item() + 1e-2
+
+
 _WT_SCRIPT = r"""
 import sys, torch
 sys.path.insert(0, sys.argv[2])

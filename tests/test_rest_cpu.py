@@ -55,6 +55,26 @@ def test_buffering_and_conflict(models_tmpdir):
         assert prog["status"] == "Created"  # buffered only: 1 sample < 180 required
 
 
+def test_train_start_failure_does_not_leave_a_stale_409(models_tmpdir, monkeypatch):
+    """An exception between the checkpoint load and the task start (here: create_task itself) must
+    not leave the model marked as starting (every later PUT /train/ answered 409)."""
+    client = TestClient(main.app, raise_server_exceptions=False)
+    client.post("/model/", json={"model_id": "s", "layer_sizes": [9, 9, 9], "activation_algos": ["relu"] * 2})
+    body = {"model_id": "s", "training_data": [{"activation_vector": [0] * 9, "target_vector": [0] * 9}],
+            "epochs": 1}
+
+    def boom(coro):
+        coro.close()
+        raise RuntimeError("no task for you")
+
+    with monkeypatch.context() as m:
+        m.setattr(main, "create_task", boom)
+        assert client.put("/train/", json=body).status_code == 500
+        assert "s" not in main._starting
+    with TestClient(main.app) as c2:
+        assert c2.put("/train/", json=body).status_code == 202
+
+
 def test_dashboard_assets_and_health(models_tmpdir):
     client = TestClient(main.app)
     r = client.get("/")

@@ -92,9 +92,6 @@ def main():
             for cus in cus_list:
                 PF.gemm(a, akc, b, bkc, c2, engine=2, cus=cus)
                 err = (c2.float() - ref).abs().max().item() / scale
-                if odt == torch.bfloat16:
-                    PF.gemm(a, akc, b, bkc, c2, engine=3, cus=cus)
-                    err = max(err, (c2.float() - ref).abs().max().item() / scale)
                 # fused epilogue vs the tiled engine (same stage math; split sums may round differently)
                 m1 = torch.zeros_like(mask_w)
                 m2 = torch.zeros_like(mask_w)
@@ -117,7 +114,6 @@ def main():
         variants = {
             "tiled_plain": lambda: PF.gemm(a, akc, b, bkc, c1, engine=1),
             "sk_plain": lambda: PF.gemm(a, akc, b, bkc, c2, engine=2),
-            **({"sk4_plain": lambda: PF.gemm(a, akc, b, bkc, c2, engine=3)} if odt == torch.bfloat16 else {}),
             "tiled_fused": fused(c1, 1, 0, cs1, mask_w),
             "sk_fused": fused(c2, 2, 0, cs2, mask_w),
         }
