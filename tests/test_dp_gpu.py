@@ -144,9 +144,11 @@ def test_multi_rank_step_equals_single_rank(tmp_path, monkeypatch, world, optimi
     if bn:
         want = _bn_stats(model)
         for r in ranks:
+            # (bf16 buckets: step 2's batch statistics see step 1's bf16-rounded updates)
+            rt, at = (1e-4, 1e-5) if comm == "fp32" else (2e-3, 1e-4)
             for (m, v), (wm, wv) in zip(r["bn"], want):
-                torch.testing.assert_close(m, wm, rtol=1e-4, atol=1e-5)
-                torch.testing.assert_close(v, wv, rtol=1e-4, atol=1e-5)
+                torch.testing.assert_close(m, wm, rtol=rt, atol=at)
+                torch.testing.assert_close(v, wv, rtol=rt, atol=at)
 
 
 def _forced_main(rank, comm, out_path, impl="native", zero="auto"):
