@@ -131,7 +131,7 @@ def _launch_ranks(n: int, argv: list[str]) -> int:
     return rc
 
 
-def _emit(args, cfg, world, elapsed, costs, batch, ctx) -> None:
+def _emit(args, cfg, world, elapsed, costs, batch, ctx, trainer=None) -> None:
     finite = all(c == c and abs(c) != float("inf") for c in costs)
     ms = elapsed * 1e3 / args.steps
     global_batch = batch * world
@@ -162,7 +162,11 @@ def _emit(args, cfg, world, elapsed, costs, batch, ctx) -> None:
                    # dense weight-gradient storage of the fused engine (PZ_GRAD_DTYPE: bf16 default,
                    # fp32 = exact fp32 gradients into the fp32-master Adam)
                    "grad_dtype": os.environ.get("PZ_GRAD_DTYPE", "bf16") if cfg["dtype"] in ("bfloat16", "fp8")
-                   else DTYPE_LABEL[cfg["dtype"]]},
+                   else DTYPE_LABEL[cfg["dtype"]],
+                   # data parallel optimizer: "zero1" = reduce-scatter + 1/N slice updates + all-gather
+                   # (engine/zero.py), "replicated" = all-reduce + full update on every rank
+                   "optimizer_sharding": ("zero1" if getattr(trainer, "zero", None) is not None else "replicated")
+                   if world > 1 or getattr(trainer, "zero", None) is not None else "none"},
     })
     if _JSON_FD is None:
         print(line, flush=True)
@@ -337,7 +341,7 @@ def main(argv=None) -> int:
     elapsed = ctx.all_reduce_scalar_max(elapsed)
 
     costs = [c for _, c, _, _ in trainer.drain()]
-    _emit(args, cfg, world, elapsed, costs, batch, ctx)
+    _emit(args, cfg, world, elapsed, costs, batch, ctx, trainer)
     from penr_oz_neural_network_torch_amd.parallel import shutdown
     shutdown()  # the native RCCL communicator, then the process group
     return 0

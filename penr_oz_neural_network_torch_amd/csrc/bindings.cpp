@@ -577,7 +577,11 @@ void colsum_op(const Tensor& x, const Tensor& out) {
               "pz::colsum: fp32 or fp64 output");
   const int cols = static_cast<int>(x.size(-1));
   const int rows = static_cast<int>(x.numel() / std::max<int64_t>(cols, 1));
-  PZ_HIP_CHECK(pz::colsum(x.data_ptr(), dt_of(x), out.data_ptr(), dt_of(out), rows, cols, cur_stream(x)));
+  at::Tensor ws;  // deterministic: per-block partial rows folded in block order (no float atomics)
+  if (pz::deterministic() && rows > 0 && cols > 0)
+    ws = at::empty({static_cast<int64_t>(pz::colsum_parts(rows)) * cols}, out.options());
+  PZ_HIP_CHECK(pz::colsum(x.data_ptr(), dt_of(x), out.data_ptr(), dt_of(out), rows, cols, cur_stream(x),
+                          ws.defined() ? ws.data_ptr() : nullptr));
 }
 
 void gather_rows_op(const Tensor& data, const optional<Tensor>& indices, int64_t seed_lo, int64_t seed_hi,

@@ -412,11 +412,13 @@ __global__ void __launch_bounds__(256) softmax_bwd_kernel(const T* __restrict__ 
   }
 }
 
-// column sums of a [rows][cols] matrix into fp32 (fp64 for fp64 data; atomic per 64-column strip
-// per block)
+// column sums of a [rows][cols] matrix into fp32 (fp64 for fp64 data). ws == nullptr: atomic per
+// 64-column strip per block; otherwise each block stores its partial row ws[blockIdx.y][c] and
+// colsum_fold_kernel adds the rows to out in block order — the sum order never depends on which
+// block finished first (deterministic training, PZ_DETERMINISTIC)
 template <typename T, typename A>
 __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, A* __restrict__ out, int rows,
-                                                     int cols, int rows_per_block) {
+                                                     int cols, int rows_per_block, A* __restrict__ ws) {
   const int c = blockIdx.x * 64 + (threadIdx.x & 63);
   const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
@@ -426,7 +428,21 @@ __global__ void __launch_bounds__(256) colsum_kernel(const T* __restrict__ x, A*
   __shared__ A part[4][64];
   part[threadIdx.x >> 6][threadIdx.x & 63] = s;
   __syncthreads();
-  if (threadIdx.x < 64 && c < cols) atomicAdd(out + c, part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x]);
+  if (threadIdx.x < 64 && c < cols) {
+    const A v = part[0][threadIdx.x] + part[1][threadIdx.x] + part[2][threadIdx.x] + part[3][threadIdx.x];
+    if (ws != nullptr) ws[static_cast<int64_t>(blockIdx.y) * cols + c] = v;
+    else atomicAdd(out + c, v);
+  }
+}
+
+template <typename A>
+__global__ void __launch_bounds__(256) colsum_fold_kernel(const A* __restrict__ ws, A* __restrict__ out, int parts,
+                                                          int cols) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  A s = A(0);
+  for (int y = 0; y < parts; ++y) s += ws[static_cast<int64_t>(y) * cols + c];
+  out[c] += s;
 }
 
 // Lean bf16 CE head for the trainer's logits stage: no probabilities, dZ always stored, the
@@ -833,17 +849,27 @@ hipError_t softmax_bwd(const void* g, const void* y, void* dx, int dtype, int ro
   return hipGetLastError();
 }
 
-hipError_t colsum(const void* x, int dtype, void* out, int out_dtype, int rows, int cols, hipStream_t s) {
+int colsum_parts(int rows) { return (rows + kColsumRows - 1) / kColsumRows; }
+
+hipError_t colsum(const void* x, int dtype, void* out, int out_dtype, int rows, int cols, hipStream_t s, void* ws) {
   if (rows <= 0 || cols <= 0) return hipSuccess;
-  const int rpb = 256;
-  dim3 grid((cols + 63) / 64, (rows + rpb - 1) / rpb);
+  const int rpb = kColsumRows;
+  const int parts = colsum_parts(rows);
+  dim3 grid((cols + 63) / 64, parts);
   PZ_DISPATCH_FLOAT(dtype, T, {
-    if (out_dtype == DT_F64)
+    if (out_dtype == DT_F64) {
       hipLaunchKernelGGL((colsum_kernel<T, double>), grid, dim3(256), 0, s, static_cast<const T*>(x),
-                         static_cast<double*>(out), rows, cols, rpb);
-    else
+                         static_cast<double*>(out), rows, cols, rpb, static_cast<double*>(ws));
+      if (ws != nullptr)
+        hipLaunchKernelGGL(colsum_fold_kernel<double>, dim3((cols + 255) / 256), dim3(256), 0, s,
+                           static_cast<const double*>(ws), static_cast<double*>(out), parts, cols);
+    } else {
       hipLaunchKernelGGL((colsum_kernel<T, float>), grid, dim3(256), 0, s, static_cast<const T*>(x),
-                         static_cast<float*>(out), rows, cols, rpb);
+                         static_cast<float*>(out), rows, cols, rpb, static_cast<float*>(ws));
+      if (ws != nullptr)
+        hipLaunchKernelGGL(colsum_fold_kernel<float>, dim3((cols + 255) / 256), dim3(256), 0, s,
+                           static_cast<const float*>(ws), static_cast<float*>(out), parts, cols);
+    }
   });
   return hipGetLastError();
 }

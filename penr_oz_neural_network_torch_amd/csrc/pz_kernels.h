@@ -106,7 +106,12 @@ hipError_t xent_head(const XentArgs& a, hipStream_t s);
 hipError_t mse_head(const MseArgs& a, hipStream_t s);
 hipError_t softmax_rows(const void* x, void* y, int dtype, int rows, int cols, hipStream_t s);
 hipError_t softmax_bwd(const void* g, const void* y, void* dx, int dtype, int rows, int cols, hipStream_t s);
-hipError_t colsum(const void* x, int dtype, void* out, int out_dtype, int rows, int cols, hipStream_t s);
+// column sums, out[c] += sum_r x[r][c]; ws (colsum_parts(rows) x cols accumulators of out's dtype):
+// deterministic ordered fold instead of float atomics
+constexpr int kColsumRows = 256;
+int colsum_parts(int rows);
+hipError_t colsum(const void* x, int dtype, void* out, int out_dtype, int rows, int cols, hipStream_t s,
+                  void* ws = nullptr);
 hipError_t gather_rows(const GatherArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------------ optimizer (N6)

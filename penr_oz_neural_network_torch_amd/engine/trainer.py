@@ -200,19 +200,25 @@ class FusedTrainer(Fp8Policy):
         # with bf16 gradient buckets and the overlapped update only (fp8 keeps replicated updates:
         # its e4m3 copies and weight amax are written by the update itself). PZ_ZERO=1 forces it
         # (e.g. a forced 1-rank RCCL group, or the one-GPU collective proxy's modelled world).
+        # PZ_ZERO_SCOPE: "side" (default) shards the weights updated on the side stream while the
+        # backward runs and keeps the step-end (first-layer) update replicated — its all-reduce +
+        # update stays the boundary's one collective hop instead of reduce-scatter -> slice update ->
+        # all-gather; "all" shards every dense weight.
         zmode = os.environ.get("PZ_ZERO", "auto")
         self.zero: ZeroShards | None = None
         if ((zmode == "1" or (zmode == "auto" and self.ctx.world_size > 1)) and self.ctx.enabled
                 and model.precision.name == "bfloat16" and self.master == torch.float32
                 and os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
                 and os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower() in ("bf16", "bfloat16")):
-            self.zero = ZeroShards(self.ctx, [st.seg_w for st in self.stages if st.kind == "gemm"],
-                                   len(self.shadow_sets), self.dev)
+            dense = [st.seg_w for st in self.stages if st.kind == "gemm"]
+            sharded = dense if os.environ.get("PZ_ZERO_SCOPE", "side") == "all" else dense[1:]
+            if sharded:
+                self.zero = ZeroShards(self.ctx, sharded, len(self.shadow_sets), self.dev)
         self._zero_ar = False  # record step: all-reduced dense gradients (the record needs them whole)
         for st in self.stages:
             if st.kind == "gemm" and self.compute != self.master:
                 for par, sset in enumerate(self.shadow_sets):
-                    sset[st.seg_w.offset] = (self.zero.shadow_view(st.seg_w.offset, par) if self.zero is not None
+                    sset[st.seg_w.offset] = (self.zero.shadow_view(st.seg_w.offset, par) if self._sharded(st.seg_w)
                                              else torch.empty(st.seg_w.shape, device=self.dev, dtype=self.compute))
         # Data parallel: dense weight gradients are written by the dW GEMMs straight in bf16 and
         # all-reduced in bf16 (half the xGMI bytes of fp32 — rings over xGMI are per-link bound,
@@ -232,12 +238,15 @@ class FusedTrainer(Fp8Policy):
         policy = os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower()
         local16 = os.environ.get("PZ_GRAD_DTYPE", "bf16").lower() in ("bf16", "bfloat16")
         if self.compute == torch.bfloat16 and (local16 if not self.ctx.enabled else policy in ("bf16", "bfloat16")):
-            buf16 = torch.zeros(max(1, self.store.accum_offset), device=self.dev, dtype=torch.bfloat16) \
-                if self.zero is None else None
+            buf16 = None
             for st in self.stages:
                 if st.kind == "gemm":
-                    self.grads16[st.seg_w.offset] = (self.zero.grad_view(st.seg_w.offset) if self.zero is not None
-                                                     else self.store.view(st.seg_w, buf16))
+                    if self._sharded(st.seg_w):
+                        self.grads16[st.seg_w.offset] = self.zero.grad_view(st.seg_w.offset)
+                        continue
+                    if buf16 is None:
+                        buf16 = torch.zeros(max(1, self.store.accum_offset), device=self.dev, dtype=torch.bfloat16)
+                    self.grads16[st.seg_w.offset] = self.store.view(st.seg_w, buf16)
         self.opt = FusedOptimizer(self.store, model.params, model.optimizer, self.shadow_sets, self.grads16)
         self.ctx.broadcast_(self.store.flat)  # identical replicas (rank 0 wins)
         for sset in self.shadow_sets:
@@ -312,6 +321,9 @@ class FusedTrainer(Fp8Policy):
         # PZ_OPT_OVERLAP=0: every update on the compute stream, after the backward.
         self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
         self.opt_stream = torch.cuda.Stream(device=self.dev) if self.overlap else None
+        # (measured, not kept: the next batch's gather on the side stream during the step, double-
+        # buffered; the step-end update on a high-priority stream — each saved its 12-20 us on the
+        # boundary and paid it back in cross-stream event latency, profiles/r6_ab_boundary.txt)
         self._g8_done: dict = {}  # stage index -> the dZ tensor whose e5m2 copy is current this step
         self._g8_epi_ready: set = set()  # stages whose epilogue-written e5m2 dZ scale is calibrated
         self._y_dead_cache: dict = {}  # fp8 policy: which bf16 GEMM outputs go unwritten (_y_dead)
@@ -355,9 +367,10 @@ class FusedTrainer(Fp8Policy):
                 self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
         self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
         if self.zero is not None:
-            # every dense weight by slices (the first layer's too, on this stream at the step end);
-            # the rest group is the small replicated parameters, whose statistics rank 0 reports
-            self.opt.define_groups(gemm_w, rest_stats=self.zero.rank == 0)
+            # the sharded weights by slices; the rest group (the replicated first layer under the
+            # default scope, and the small parameters) reports its statistics from rank 0 only
+            self.opt.define_groups([o for o in gemm_w if o in self.zero.shards or o in gemm_w[1:]],
+                                   rest_stats=self.zero.rank == 0)
             self.zero.define_groups(self.opt)
         else:
             self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
@@ -521,6 +534,15 @@ class FusedTrainer(Fp8Policy):
         self._plan_fp8(rows_b)
         # record-mode scratch: one buffer per layer output / grad, allocated lazily
 
+    def _gather(self, epoch, idx, batch, capture, su) -> None:
+        ops = torch.ops.pz
+        gseed = self._gather_seed(epoch)
+        ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
+                        self.epoch_ctr if capture else None, self.data8,
+                        self.x8 if self.data8 is not None else None, *su)
+        if self.tgt is not None:
+            ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
+
     # ------------------------------------------------------------------------------------
     # epilogue specs
     def _opt_async(self, items: list, ready=None) -> None:
@@ -538,7 +560,7 @@ class FusedTrainer(Fp8Policy):
             for key, handles, stages in items:
                 for h in handles:
                     self.ctx.wait_one(h)
-                if self.zero is not None:  # this rank's slice, then the all-gather of the bf16 copy
+                if self.zero is not None and key in self.zero.shards:  # slice, then all-gather of the bf16 copy
                     gathers.append(self.zero.update(self.opt, key, self.grads, l2, scale, 1 - self.parity))
                 else:
                     self.opt.step_group(key, self.grads, l2, scale, 1 - self.parity)
@@ -744,7 +766,6 @@ class FusedTrainer(Fp8Policy):
 
         # ---------------- sample + input
         self._phase("pz.sample")
-        gseed = self._gather_seed(epoch)
         idx = None
         if indices is not None:
             idx = indices.to(device=self.dev, dtype=torch.int64).contiguous()
@@ -755,12 +776,8 @@ class FusedTrainer(Fp8Policy):
         # the previous step's gradient amax -> this step's e5m2 scales rides on the gather
         # (delayed scaling: nothing reads them before this step's backward)
         su = (self.gamax, self.gqs, 2.0, 57344.0) if self._grad_su_pending else (None, None, 1.0, 448.0)
-        ops.gather_rows(self.data, idx, gseed[0], gseed[1], self.x_in, batch, self.labels, self.lab, self.picked,
-                        self.epoch_ctr if capture else None, self.data8,
-                        self.x8 if self.data8 is not None else None, *su)
+        self._gather(epoch, idx, batch, capture, su)
         self._grad_su_pending = False
-        if self.tgt is not None:
-            ops.gather_rows(self.targets, self.picked, 0, 0, self.tgt, batch, None, None, None)
 
         rec = {} if record else None
         # the previous step's first-layer / bias update ran on this stream; its side-stream updates
@@ -835,12 +852,12 @@ class FusedTrainer(Fp8Policy):
             # of queueing behind them; step_finalize (side) waits for both
             pending, self._side_pending = self._side_pending, []
             gathers = []
-            if self.zero is not None:
+            if self.zero is not None and any(self._sharded(st.seg_w) for st in self._late_stages):
                 # the first layer's slice on this stream, its all-gather overlapping the small
                 # replicated update behind it; the next forward (this stream) then reads it
                 for h in self._late_handles:
                     self.ctx.wait_one(h)
-                gathers = [self.zero.update(self.opt, st.seg_w.offset, self.grads, l2, 1.0, 1 - self.parity)
+                gathers = [self.zero.update(self.opt, st.seg_w.offset, self.grads, l2, 1.0, 1 - self.parity, side=False)
                            for st in self._late_stages]
                 self.ctx.wait_one(acc_h)
             else:
@@ -1172,9 +1189,12 @@ class FusedTrainer(Fp8Policy):
         """Start a weight's gradient bucket: reduce-scatter (sharded optimizer) or all-reduce (the
         replicated update, and record steps); the GEMMs behind it get the comm CU budget."""
         self._cus = self._cus_comm
-        if self.zero is not None:
+        if self._sharded(seg):
             return self.zero.all_reduce(seg.offset) if self._zero_ar else self.zero.reduce_scatter(seg.offset)
         return self.ctx.all_reduce_async(self._w_grad(seg))
+
+    def _sharded(self, seg) -> bool:
+        return self.zero is not None and seg.offset in self.zero.shards
 
     def _dw_update(self, st: Stage, x_in, g) -> None:
         """dW GEMM + the weight's optimizer update in one launch (fuse_opt). The update writes the

@@ -50,6 +50,7 @@ class Shard:
 class ZeroShards:
     def __init__(self, ctx, dense_segments, shadow_parities: int, device: torch.device):
         self.ctx = ctx
+        ctx.open_side_comm()  # all-gathers + statistics on a communicator of their own
         self.world = ctx.shard_world
         self.rank = ctx.shard_rank
         self.shards: dict[int, Shard] = {}
@@ -94,19 +95,23 @@ class ZeroShards:
         """Record steps: the whole summed gradient on every rank."""
         return self.ctx.all_reduce_async(self.shards[off].g_full)
 
-    def update(self, opt, off: int, grads: torch.Tensor, l2: float, scale: float, parity: int, source: str = "rs"):
+    def update(self, opt, off: int, grads: torch.Tensor, l2: float, scale: float, parity: int, source: str = "rs",
+               side: bool = True):
         """This rank's slice update into shadow set ``parity``, then the all-gather of that set
-        (in place). Returns the all-gather's handle (the reader waits for it)."""
+        (in place). Returns the all-gather's handle (the reader waits for it). ``side``: on the
+        second communicator (updates on the side stream); the step-end update on the compute
+        stream gathers on the bucket communicator, behind that step's last reduce-scatters, where
+        no side-stream update can hold it."""
         sh = self.shards[off]
         if sh.cnt > 0:
             opt.step_group(("z", off, source), grads, l2, scale, parity)
         full = sh.sh_full[parity]
-        return self.ctx.all_gather_async(full[sh.lo:sh.lo + sh.s], full)
+        return self.ctx.all_gather_async(full[sh.lo:sh.lo + sh.s], full, side=side)
 
     def all_reduce_stats(self, stats: torch.Tensor) -> None:
         """Sum the per-weight statistics partials over the ranks (stream-ordered on the current
         stream; exact fp64)."""
-        self.ctx.wait_one(self.ctx.all_reduce_async(stats, exact=True))
+        self.ctx.wait_one(self.ctx.side_all_reduce_async(stats))
 
     def gather_state(self, flat: torch.Tensor, *moments: torch.Tensor | None) -> None:
         """All-gather every weight's fp32 master (and Adam moments) from the slice owners, so

@@ -46,6 +46,12 @@ class DataParallelContext:
     # smaller (csrc/gemm_sk.hip) instead of its one-round tiled grid, whose workgroups on the held
     # CUs would otherwise form a whole second round (profiles/r5_comm_pressure.txt).
     comm_cus: int = 0
+    # second communicator (process group / native RCCL comm) for the sharded optimizer's all-gathers
+    # and statistics sums: ONE communicator runs its collectives in issue order, and an all-gather
+    # waits for its weight's update on the side stream — on the bucket communicator it would hold
+    # every later reduce-scatter (the first layer's, on the step boundary) behind that update
+    ag_group: object = None
+    ag_native: object = None
 
     @property
     def enabled(self) -> bool:
@@ -99,23 +105,47 @@ class DataParallelContext:
         work = dist.reduce_scatter_tensor(shard, full, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         return (work, None, None)
 
-    def all_gather_async(self, shard: torch.Tensor, full: torch.Tensor):
+    def open_side_comm(self) -> None:
+        """Bring up the second communicator (collective: every rank calls it at the same point —
+        the fused trainer's constructor when it shards the optimizer)."""
+        if not self.enabled or self.ag_group is not None or self.ag_native is not None:
+            return
+        if isinstance(self.native, _ProxyComm):
+            self.ag_native = _ProxyComm()
+        elif self.native is not None:
+            self.ag_native = _NativeComm(self.rank, self.world_size)
+        elif dist.is_initialized():
+            self.ag_group = dist.new_group(list(range(self.world_size)))
+
+    def all_gather_async(self, shard: torch.Tensor, full: torch.Tensor, side: bool = False):
         """Start an all-gather of every rank's ``shard`` into ``full`` (rank r's at
-        ``[r*n, (r+1)*n)``); ``shard`` may be this rank's slice of ``full`` (in place)."""
+        ``[r*n, (r+1)*n)``); ``shard`` may be this rank's slice of ``full`` (in place).
+        ``side``: on the second communicator (:meth:`open_side_comm`) when there is one."""
         if not self.enabled:
             return None
-        if self.native is not None:
-            return (_Ticket(self.native.handle, torch.ops.pz.rccl_all_gather(self.native.handle, shard, full)),
-                    None, None)
+        native = self.ag_native if side and self.ag_native is not None else self.native
+        group = self.ag_group if side and self.ag_group is not None else self.group
+        if native is not None:
+            return (_Ticket(native.handle, torch.ops.pz.rccl_all_gather(native.handle, shard, full)), None, None)
         if full.is_cuda and self.backend == "gloo":
             # (gloo on device tensors: zeros elsewhere + one exact sum all-reduce)
             n = shard.numel()
             tmp = torch.zeros_like(full)
             tmp[self.rank * n:(self.rank + 1) * n].copy_(shard)
-            work = dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+            work = dist.all_reduce(tmp, op=dist.ReduceOp.SUM, group=group, async_op=True)
             return (work, tmp, full)
-        work = dist.all_gather_into_tensor(full, shard, group=self.group, async_op=True)
+        work = dist.all_gather_into_tensor(full, shard, group=group, async_op=True)
         return (work, None, None)
+
+    def side_all_reduce_async(self, t: torch.Tensor):
+        """Exact SUM all-reduce on the second communicator (the sharded statistics)."""
+        if not self.enabled:
+            return None
+        if self.ag_native is not None:
+            return (_Ticket(self.ag_native.handle, torch.ops.pz.rccl_all_reduce(self.ag_native.handle, t)), None, None)
+        if self.ag_group is not None:
+            return (dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.ag_group, async_op=True), None, None)
+        return self.all_reduce_async(t, exact=True)
 
     def all_reduce_(self, t: torch.Tensor) -> None:
         """Blocking exact SUM all-reduce in place (stream-ordered under RCCL): the synchronised
@@ -329,11 +359,13 @@ def set_context(ctx: DataParallelContext | None) -> None:
 
 def shutdown() -> None:
     global _CONTEXT
-    if _CONTEXT is not None and _CONTEXT.native is not None:
+    if _CONTEXT is not None and (_CONTEXT.native is not None or _CONTEXT.ag_native is not None):
         if torch.cuda.is_available():
             torch.cuda.synchronize()
-        _CONTEXT.native.close()
-        _CONTEXT.native = None
+        for comm in (_CONTEXT.ag_native, _CONTEXT.native):
+            if comm is not None:
+                comm.close()
+        _CONTEXT.native = _CONTEXT.ag_native = None
     if dist.is_available() and dist.is_initialized():
         dist.destroy_process_group()
     _CONTEXT = None

@@ -517,3 +517,32 @@ def test_bf16_training_is_bit_reproducible():
         flats.append((model._param_store.flat.clone(), [v["exp_avg"].clone() for v in st.values()]))
     assert torch.equal(flats[0][0], flats[1][0])
     assert all(torch.equal(a, b) for a, b in zip(flats[0][1], flats[1][1]))
+
+
+def test_training_with_record_steps_is_bit_reproducible():
+    """PZ_DETERMINISTIC across a batch-size change and a RECORD step (the stats epochs: unfused
+    epilogues, per-layer outputs kept, bias gradients from pz::colsum's ordered fold instead of
+    float atomics): two runs give bit-identical weights and Adam moments; the costs (float-atomic
+    loss slots) agree to rounding."""
+    sizes = [1024, 2048, 2048, 512]
+    algos = ["relu", "relu", "softmax"]
+    n, steps = 8192, 5
+    g = torch.Generator().manual_seed(6)
+    inputs = torch.randn(n, sizes[0], generator=g)
+    labels = torch.randint(0, sizes[-1], (n,), generator=g)
+    outs = []
+    for _ in range(2):
+        torch.manual_seed(0)
+        model = NeuralNetworkModel("bnd", sizes, "xavier", "random", algos, "adam", dtype="bfloat16", device="cuda")
+        tr = FusedTrainer(model)
+        tr.load_tensors(inputs, labels, seed=4)
+        tr.begin(steps)
+        for e in range(steps):
+            tr.step(e, 1e-3, 4096 if e != 3 else 2048, 0.2, 1e-3, want_ratios=True, record=e == 2)
+        costs = [c for _, c, _, _ in tr.drain()]
+        st = model.optimizer.state_dict()["state"]
+        outs.append((model._param_store.flat.clone(), [v["exp_avg"].clone() for v in st.values()], costs))
+        tr.close()
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert all(torch.equal(a, b) for a, b in zip(outs[0][1], outs[1][1]))
+    assert all(abs(a - b) <= 1e-12 * abs(b) for a, b in zip(outs[0][2], outs[1][2]))

@@ -795,3 +795,20 @@ def test_write_through_epilogue_stores_are_bit_identical(tmp_path):
             torch.testing.assert_close(outs[0][k].float(), outs[1][k].float(), rtol=2 ** -7, atol=1e-2)
         else:
             assert torch.equal(outs[0][k], outs[1][k]), k
+
+
+def test_colsum_is_deterministic_and_accumulates(native_lib):
+    """pz::colsum (record-step bias gradients): out += column sums, against fp64, and two runs
+    bit-identical — per-block partial rows folded in block order, no float atomics."""
+    for dt, odt in ((torch.bfloat16, torch.float32), (torch.float32, torch.float32), (torch.float64, torch.float64)):
+        x = torch.randn(3001, 700, device=DEV).to(dt)
+        base = torch.randn(700, device=DEV, dtype=odt)
+        outs = []
+        for _ in range(2):
+            out = base.clone()
+            native_lib.colsum(x, out)
+            outs.append(out)
+        assert torch.equal(outs[0], outs[1])
+        ref = base.double() + x.double().sum(0)
+        tol = 1e-9 if odt == torch.float64 else 1e-3
+        assert (outs[0].double() - ref).abs().max().item() < tol * math.sqrt(3001)

@@ -12,6 +12,11 @@ ms/step, interleaved over rounds (same box):
                 150 GB/s (the default schedule: full-grid tiled GEMMs)
   proxy_w<W>_sk the same with PZ_COMM_BUDGET=W: the backward GEMMs behind a bucket on the
                 persistent stream-K engine with 256 - W CUs (parallel/dist.py comm_cus)
+  zero_*        the same with the sharded optimizer (PZ_ZERO=1, engine/zero.py; zeroall_*: PZ_ZERO_SCOPE=all,
+                the first layer sharded too): reduce-scatter +
+                all-gather per weight (torch: real 1-rank RCCL calls, whole-weight slices; proxy:
+                the modelled 8-rank world as its rank 0 — 1/8 of every weight updated, the proxy
+                holding its workgroups for a ring reduce-scatter and a ring all-gather)
 
     python tools/comm_pressure.py [--rounds 2] [--steps 60] [--wgs 16,32]
 """
@@ -26,6 +31,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def run(env_extra, steps, warmup):
     env = dict(os.environ, **env_extra)
+    if env_extra.get("PZ_FORCE_COMM") == "1":  # a file rendezvous: no TCP port to race for
+        import tempfile
+        env["PZ_RENDEZVOUS_FILE"] = os.path.join(tempfile.mkdtemp(prefix="pz_rdv_"), "store")
     out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", str(steps), "--warmup",
                           str(warmup)], env=env, capture_output=True, text=True, timeout=300)
     if out.returncode != 0:
@@ -41,6 +49,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--wgs", default="16,32")
     ap.add_argument("--gbps", default="150")
+    ap.add_argument("--cases", default="", help="comma-separated subset of the case names")
     a = ap.parse_args()
     forced = {"PZ_FORCE_COMM": "1"}
     cases = {"none": {}, "torch": dict(forced, PZ_COMM="torch"), "native": dict(forced, PZ_COMM="native"),
@@ -49,6 +58,16 @@ def main():
         proxy = dict(forced, PZ_COMM="proxy", PZ_COMM_PROXY_WGS=str(w), PZ_COMM_PROXY_GBPS=a.gbps)
         cases[f"proxy_w{w}"] = proxy
         cases[f"proxy_w{w}_sk"] = dict(proxy, PZ_COMM_BUDGET=str(w))
+        cases[f"zero_proxy_w{w}"] = dict(proxy, PZ_ZERO="1")
+        cases[f"zeroall_proxy_w{w}"] = dict(proxy, PZ_ZERO="1", PZ_ZERO_SCOPE="all")
+    cases["zero_torch"] = dict(forced, PZ_COMM="torch", PZ_ZERO="1")
+    cases["zero_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1")
+    cases["zeroall_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1", PZ_ZERO_SCOPE="all")
+    for c in (x for x in a.cases.split(",") if x):
+        if c not in cases:
+            raise SystemExit(f"unknown case {c}: {sorted(cases)}")
+    if a.cases:
+        cases = {k: v for k, v in cases.items() if k in a.cases.split(",") or k == "none"}
     res = {name: [] for name in cases}
     for r in range(a.rounds):
         for name, env in cases.items():
