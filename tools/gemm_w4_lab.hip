@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1)))
   PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
   const int tiles_m = p.M / BM, tiles_n = p.N / BN;
   int tm, tn, tile_id, slice;
-  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
   const int m0 = tm * BM, n0 = tn * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -300,7 +300,7 @@ __global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1)))
   PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
   const int tiles_m = p.M / BM, tiles_n = p.N / BN;
   int tm, tn, tile_id, slice;
-  tile_coords(tiles_m * tiles_n, tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
   const int m0 = tm * BM, n0 = tn * BN;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int wm = wave >> 1, wn = wave & 1;
@@ -413,6 +413,343 @@ hipError_t launch32(const GemmArgs& p, hipStream_t s) {
   hipLaunchKernelGGL(kern32, dim3((p.M / BM) * (p.N / BN)), dim3(NT), 2 * SLOT, s, p);
   return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------------------------
+// kdma<B0>: the schedule of hipBLASLt's gfx950 dX kernel (Custom_Cijk_Alik_Bljk_..._MT256x256x64,
+// disassembled in round 6: profiles/r6_hipblaslt_kernels.txt) in HIP. 4 waves, 128x128 wave tiles
+// (8x8 16x16x32 accumulators = 256 AGPRs), TWO LDS buffers of one 64-deep tile each, every
+// operand k-half its own [256][32] slot (swz_kc<32>), filled by LDS-DMA. Fragments of BOTH
+// k-halves of tile t are in registers before its second k-half's MFMAs start (sets S0 / S1), so
+// buffer t&1 is free for tile t+2's DMAs half-way through iteration t — a prefetch distance of
+// about one iteration with two buffers:
+//   [B0: barrier, B0 = true]  phase 1: MFMAs S0 rows 0-3  + reads of S1        (+ k-half-0 DMAs)
+//   B1: lgkmcnt(0) + barrier  phase 2: MFMAs S0 rows 4-7  + DMAs of tile t+2
+//                             phase 3: MFMAs S1 rows 0-3  + DMAs of tile t+2
+//   B2: vmcnt(tile t+1 landed) + barrier   phase 4: MFMAs S1 rows 4-7 + reads of S0 (tile t+1)
+// B0 = true: a barrier at the top of the iteration certifies every wave's tile-t S0 reads done,
+// so the k-half-0 slots take their DMAs already in phase 1 (16 DMAs over 96 MFMAs, not 64).
+constexpr int HS = BM * 32 * 2;       // one operand k-half slot: 16 KiB
+constexpr int TB = 4 * HS;            // one tile buffer: A kh0, A kh1, B kh0, B kh1 = 64 KiB
+
+// D4: DMA pieces issued in phase 4 (the rest, 16 - D4, spread over phases 2-3); the loop body is
+// branch-free — past the last tile the DMAs re-load tile nk-1 into the free buffer and the reads
+// re-read the other buffer (harmless) — and every per-piece source offset is a precomputed scalar
+template <int D4>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) kdma(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+  const int tiles_m = p.M / BM, tiles_n = p.N / BN;
+  int tm, tn, tile_id, slice;
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const i32x4_t rs_a = buf_rsrc(p.A), rs_b = buf_rsrc(p.B);
+  const int prow = lane >> 2;
+  const int pch = (lane & 3) ^ swz_kc<32>(prow);
+  const uint32_t va = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.lda) + pch * 8) * 2u;
+  const uint32_t vb = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.ldb) + pch * 8) * 2u;
+  const uint32_t lds0 = lds_addr(smem);
+  // per piece d: wave-uniform source byte offset at k = 0 and LDS destination in buffer 0
+  uint32_t sbase[16], dbase[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const int sl = d >> 2, i = d & 3;
+    const bool isb = sl >= 2;
+    const uint32_t rbase = static_cast<uint32_t>((wave * 4 + i) * 16);
+    const uint32_t ld = static_cast<uint32_t>(isb ? p.ldb : p.lda);
+    sbase[d] = __builtin_amdgcn_readfirstlane(((static_cast<uint32_t>(isb ? n0 : m0) + rbase) * ld + (sl & 1) * 32) * 2u);
+    dbase[d] = __builtin_amdgcn_readfirstlane(lds0 + static_cast<uint32_t>(sl * HS) + rbase * 64u);
+  }
+  const int nk = p.K / BK;
+  auto dma = [&](int kt, int d) __attribute__((always_inline)) {
+    kt = kt < nk ? kt : nk - 1;
+    blds16<0>(d >= 8 ? rs_b : rs_a, d >= 8 ? vb : va, sbase[d] + static_cast<uint32_t>(kt) * (BK * 2),
+              dbase[d] + static_cast<uint32_t>((kt & 1) * TB));
+  };
+  auto frag = [&](int buf, int kh, int f) __attribute__((always_inline)) -> i16x8_t {
+    const PZ_LDS char* base = smem + buf * TB + (f < 8 ? 2 + kh : kh) * HS;
+    const int row = (f < 8 ? wn : wm) * 128 + (f & 7) * 16 + (lane & 15);
+    return frag_kc<32>(base, row, lane >> 4);
+  };
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const i16x8_t (&F)[16], int i, int j) __attribute__((always_inline)) {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, F[j]),
+                                                        __builtin_bit_cast(bf16x8_t, F[8 + i]), acc[i][j], 0, 0, 0);
+  };
+  i16x8_t S0[16], S1[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(0, d);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(1, d);
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int f = 0; f < 16; ++f) S0[f] = frag(0, 0, f);
+  constexpr int D23 = 16 - D4;  // pieces over phases 2-3 (64 MFMAs)
+  for (int t = 0; t < nk; ++t) {
+    const int buf = t & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 1: S0 rows 0-3 (32 MFMAs), the 16 S1 reads (1 per 2 MFMAs)
+    static_for<16>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      mm(S0, g >> 2, 2 * (g & 3));
+      mm(S0, g >> 2, 2 * (g & 3) + 1);
+      S1[g] = frag(buf, 1, g);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // phases 2-3: S0 rows 4-7, S1 rows 0-3 (64 MFMAs) + D23 DMA pieces of tile t+2 into buffer buf
+    static_for<64>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (c < 32) mm(S0, 4 + (c >> 3), c & 7);
+      else mm(S1, (c - 32) >> 3, c & 7);
+      constexpr int every = 64 / (D23 > 0 ? D23 : 1);
+      if constexpr (D23 > 0 && c % every == every - 1 && c / every < D23) {
+        dma(t + 2, c / every);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+    // tile t+1 landed (the D23 pieces of tile t+2 just issued stay in flight)
+    wait_vm<D23>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 4: S1 rows 4-7 (32 MFMAs) + the 16 S0 reads of tile t+1 (+ D4 DMA pieces)
+    static_for<16>([&](auto gc) {
+      constexpr int g = decltype(gc)::value;
+      mm(S1, 4 + (g >> 2), 2 * (g & 3));
+      mm(S1, 4 + (g >> 2), 2 * (g & 3) + 1);
+      S0[g] = frag(buf ^ 1, 0, g);
+      constexpr int every4 = 16 / (D4 > 0 ? D4 : 1);
+      if constexpr (D4 > 0 && g % every4 == every4 - 1 && g / every4 < D4) dma(t + 2, D23 + g / every4);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  }
+  wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+  uint16_t* C = static_cast<uint16_t*>(p.C);
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int m = m0 + wm * 128 + i * 16 + (lane & 15), n = n0 + wn * 128 + j * 16 + 4 * (lane >> 4);
+      float v[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha, acc[i][j][3] * p.alpha};
+      store4<uint16_t>(C + static_cast<int64_t>(m) * p.ldc + n, v);
+    }
+}
+
+template <int D4>
+hipError_t launch_dma(const GemmArgs& p, hipStream_t s) {
+  static bool set = false;
+  if (!set) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kdma<D4>), hipFuncAttributeMaxDynamicSharedMemorySize, 2 * TB));
+    set = true;
+  }
+  if (p.M % BM || p.N % BN || p.K % BK || p.K < BK) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(kdma<D4>, dim3((p.M / BM) * (p.N / BN)), dim3(NT), 2 * TB, s, p);
+  return hipGetLastError();
+}
+
+// kdmap<D4>: kdma made persistent — min(tiles, CUs) workgroups, workgroup r owns tiles r, r+G, ...
+// and runs ONE k pipeline over all of them (global k step g = tile_i * nk + kt): the DMAs of the
+// next tile's first two k steps go out during the current tile's last two, so only the epilogue
+// (64 stores straight from the accumulators) separates two tiles — no prologue, no relaunch
+// MODE (diagnostics): 0 = the GEMM, 1 = every tile reads tile (0, 0)'s operands (L2-resident loads),
+// 2 = no DMAs at all (MFMA + LDS-read issue only; results are garbage); 3 = the GEMM with full
+// 64-deep rows per slot ([256][64], swz_kc<64>: one DMA = 8 rows x 128 B, whole cache lines,
+// instead of 16 rows x 64 B half-lines of the [256][32] k-half slots); diagnostics of the full
+// layout: 4 = no swizzle at all (bank-conflicted reads), 5 = nt loads, 6 = natural-order global
+// addresses with swizzled reads (timing only: the data lands permuted)
+template <int D4, int MODE = 0>
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(1, 1))) kdmap(const GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+  const int tiles_m = p.M / BM, tiles_n = p.N / BN, tiles = tiles_m * tiles_n;
+  const int G = gridDim.x;
+  const int r = xcd_remap(blockIdx.x, G);
+  const int T = (tiles - r + G - 1) / G;  // this workgroup's tile count (>= 1: G <= tiles)
+  const int nk = p.K / BK;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const i32x4_t rs_a = buf_rsrc(p.A), rs_b = buf_rsrc(p.B);
+  constexpr bool FULL = MODE >= 3, NOSWZ = MODE == 4, GNAT = MODE == 4 || MODE == 6;
+  constexpr int POL = MODE == 5 ? 1 : 0;
+  constexpr int RPD = FULL ? 8 : 16, CPR = FULL ? 8 : 4;  // rows per DMA, 16-B chunks per slot row
+  const int prow = lane / CPR;
+  // the chunk swizzle of row r (absolute in the slot) — for FULL it differs between even and odd
+  // 8-row pieces ((r >> 1) & 4), hence two lane offsets per operand
+  const int pch0 = (lane % CPR) ^ (GNAT ? 0 : FULL ? swz_kc<64>(prow) : swz_kc<32>(prow));
+  const int pch1 = (lane % CPR) ^ (GNAT ? 0 : FULL ? swz_kc<64>(prow + 8) : swz_kc<32>(prow));
+  const uint32_t va0 = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.lda) + pch0 * 8) * 2u;
+  const uint32_t vb0 = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.ldb) + pch0 * 8) * 2u;
+  const uint32_t va1 = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.lda) + pch1 * 8) * 2u;
+  const uint32_t vb1 = (static_cast<uint32_t>(prow) * static_cast<uint32_t>(p.ldb) + pch1 * 8) * 2u;
+  const uint32_t lds0 = lds_addr(smem);
+  uint32_t pofs[16], dbase[16];  // per piece: source byte offset within a tile at k = 0, LDS slot
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    if constexpr (FULL) {
+      const int op = d >> 3, i = d & 7;
+      const uint32_t rbase = static_cast<uint32_t>((wave * 8 + i) * RPD);
+      const uint32_t ld = static_cast<uint32_t>(op ? p.ldb : p.lda);
+      pofs[d] = __builtin_amdgcn_readfirstlane(rbase * ld * 2u);
+      dbase[d] = __builtin_amdgcn_readfirstlane(lds0 + static_cast<uint32_t>(op * (TB / 2)) + rbase * 128u);
+    } else {
+      const int sl = d >> 2, i = d & 3;
+      const uint32_t rbase = static_cast<uint32_t>((wave * 4 + i) * RPD);
+      const uint32_t ld = static_cast<uint32_t>(sl >= 2 ? p.ldb : p.lda);
+      pofs[d] = __builtin_amdgcn_readfirstlane((rbase * ld + (sl & 1) * 32) * 2u);
+      dbase[d] = __builtin_amdgcn_readfirstlane(lds0 + static_cast<uint32_t>(sl * HS) + rbase * 64u);
+    }
+  }
+  auto origin = [&](int i, int& m0, int& n0) __attribute__((always_inline)) {
+    int tm, tn, tile_id, slice;
+    tile_coords(r + i * G, tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+  // DMA cursor (k step dk of tile di; stays on the last step once there — re-loads are harmless)
+  int dk = 0, di = 0;
+  uint32_t abase, bbase;
+  auto set_bases = [&]() __attribute__((always_inline)) {
+    int m0, n0;
+    origin(di, m0, n0);
+    if constexpr (MODE == 1) m0 = n0 = 0;
+    abase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m0) * static_cast<uint32_t>(p.lda) * 2u);
+    bbase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n0) * static_cast<uint32_t>(p.ldb) * 2u);
+  };
+  set_bases();
+  auto dma = [&](int g, int d) __attribute__((always_inline)) {
+    if constexpr (MODE == 2) return;
+    const bool odd = FULL && (d & 1);
+    blds16<POL>(d >= 8 ? rs_b : rs_a, d >= 8 ? (odd ? vb1 : vb0) : (odd ? va1 : va0),
+              (d >= 8 ? bbase : abase) + pofs[d] + static_cast<uint32_t>(dk) * (BK * 2),
+              dbase[d] + static_cast<uint32_t>((g & 1) * TB));
+  };
+  auto advance = [&]() __attribute__((always_inline)) {
+    if (dk + 1 < nk) {
+      ++dk;
+    } else if (di + 1 < T) {
+      dk = 0;
+      ++di;
+      set_bases();
+    }
+  };
+  auto frag = [&](int buf, int kh, int f) __attribute__((always_inline)) -> i16x8_t {
+    const int row = (f < 8 ? wn : wm) * 128 + (f & 7) * 16 + (lane & 15);
+    if constexpr (NOSWZ)
+      return *reinterpret_cast<const PZ_LDS i16x8_t*>(smem + buf * TB + (f < 8 ? TB / 2 : 0) + row * 128 +
+                                                      (kh * 4 + (lane >> 4)) * 16);
+    if constexpr (FULL) return frag_kc<64>(smem + buf * TB + (f < 8 ? TB / 2 : 0), row, kh * 4 + (lane >> 4));
+    const PZ_LDS char* base = smem + buf * TB + (f < 8 ? 2 + kh : kh) * HS;
+    return frag_kc<32>(base, row, lane >> 4);
+  };
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const i16x8_t (&F)[16], int i, int j) __attribute__((always_inline)) {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, F[j]),
+                                                        __builtin_bit_cast(bf16x8_t, F[8 + i]), acc[i][j], 0, 0, 0);
+  };
+  i16x8_t S0[16], S1[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(0, d);
+  advance();
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(1, d);
+  advance();
+  wait_vm<16>();
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int f = 0; f < 16; ++f) S0[f] = frag(0, 0, f);
+  constexpr int D23 = 16 - D4;
+  uint16_t* C = static_cast<uint16_t*>(p.C);
+  int g = 0;  // global k step: buffer parity
+  for (int ci = 0; ci < T; ++ci) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < nk; ++kt, ++g) {
+      const int buf = g & 1;
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<16>([&](auto gc) {
+        constexpr int q = decltype(gc)::value;
+        mm(S0, q >> 2, 2 * (q & 3));
+        mm(S0, q >> 2, 2 * (q & 3) + 1);
+        S1[q] = frag(buf, 1, q);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<64>([&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if constexpr (c < 32) mm(S0, 4 + (c >> 3), c & 7);
+        else mm(S1, (c - 32) >> 3, c & 7);
+        constexpr int every = 64 / (D23 > 0 ? D23 : 1);
+        if constexpr (D23 > 0 && c % every == every - 1 && c / every < D23) {
+          dma(g, c / every);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      });
+      wait_vm<D23>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      static_for<16>([&](auto gc) {
+        constexpr int q = decltype(gc)::value;
+        mm(S1, 4 + (q >> 2), 2 * (q & 3));
+        mm(S1, 4 + (q >> 2), 2 * (q & 3) + 1);
+        S0[q] = frag(buf ^ 1, 0, q);
+        constexpr int every4 = 16 / (D4 > 0 ? D4 : 1);
+        if constexpr (D4 > 0 && q % every4 == every4 - 1 && q / every4 < D4) dma(g, D23 + q / every4);
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      advance();
+    }
+    // tile ci complete: store it straight from the accumulators
+    int m0, n0;
+    origin(ci, m0, n0);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int m = m0 + wm * 128 + i * 16 + (lane & 15), n = n0 + wn * 128 + j * 16 + 4 * (lane >> 4);
+        float v[4] = {acc[i][j][0] * p.alpha, acc[i][j][1] * p.alpha, acc[i][j][2] * p.alpha,
+                      acc[i][j][3] * p.alpha};
+        store4<uint16_t>(C + static_cast<int64_t>(m) * p.ldc + n, v);
+      }
+  }
+  wait_vm<0>();  // no LDS-DMA may outlive the workgroup
+}
+
+template <int D4, int MODE = 0>
+hipError_t launch_dmap(const GemmArgs& p, hipStream_t s) {
+  static bool set = false;
+  static int cus = 0;
+  if (!set) {
+    CK(hipFuncSetAttribute(reinterpret_cast<const void*>(kdmap<D4, MODE>), hipFuncAttributeMaxDynamicSharedMemorySize, 2 * TB));
+    int dev = 0;
+    CK(hipGetDevice(&dev));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    set = true;
+  }
+  if (p.M % BM || p.N % BN || p.K % BK || p.K < BK) return hipErrorInvalidValue;
+  const int tiles = (p.M / BM) * (p.N / BN);
+  hipLaunchKernelGGL((kdmap<D4, MODE>), dim3(std::min(tiles, cus)), dim3(NT), 2 * TB, s, p);
+  return hipGetLastError();
+}
 }  // namespace w4
 
 
@@ -441,7 +778,12 @@ int main(int argc, char** argv) {
   std::vector<Case> cases = {{"dX_L2", 8192, 4096, 4096}, {"dX_L3", 8192, 4096, 1024}};
   struct V { const char* name; LaunchFn fn; };
   std::vector<V> vs = {{"lib_var30", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
-                       {"w4_early", w4::launch<5>}, {"w4_32x32", w4::launch32}};
+                       {"w4_dma0", w4::launch_dma<0>}, {"w4_dma4", w4::launch_dma<4>},
+                       {"w4_dma8", w4::launch_dma<8>},
+                       {"w4_dmap4", w4::launch_dmap<4>}, {"w4_dmap8", w4::launch_dmap<8>},
+                       {"dmap8_hot", w4::launch_dmap<8, 1>}, {"dmap8_nodma", w4::launch_dmap<8, 2>},
+                       {"dmap4_full", w4::launch_dmap<4, 3>}, {"dmap8_full", w4::launch_dmap<8, 3>},
+                       {"dmap4_noswz", w4::launch_dmap<4, 4>}, {"dmap4_gnat", w4::launch_dmap<4, 6>}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (const Case& c : cases) {

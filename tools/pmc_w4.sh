@@ -14,7 +14,7 @@ from collections import defaultdict
 acc = defaultdict(lambda: defaultdict(float)); n = defaultdict(set)
 for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"]; k = "lib_var30" if "gemm_mfma" in k else ("w4<%s>" % k.split("ILi")[1][0] if "w44kern" in k else None)
+        k = r["Kernel_Name"]; k = ("lib_var30" if "gemm_mfma" in k else k.split("::")[1].split("(")[0] if k.startswith("void w4::") else None)
         if k is None: continue
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"]); n[k].add(r["Dispatch_Id"])
 for k, c in sorted(acc.items()):
