@@ -690,6 +690,8 @@ gemm_mfma_kernel(const GemmArgs p) {
   gemm_body<BM, BN, WM, WN, A_KC, B_KC, OutT, AuxT, VAR, EK>(p, xcd_remap(blockIdx.x, gridDim.x));
 }
 
+#include "gemm_w4.h"  // VAR 40: the dX layout on 4-wave workgroups (hipBLASLt's schedule)
+
 // Two independent GEMMs of one layout / epilogue kind in ONE launch (gemm_pair): the first nwg0
 // remapped workgroup ids run GEMM 0, the rest GEMM 1 — e.g. the two skinny weight-gradient GEMMs
 // of a 3-layer MLP (64 tiles each at batch 8192) that alone would each need a 4-way split-K to
@@ -755,6 +757,15 @@ bool use_bk64(const GemmArgs& p, bool buf) {
   return buf && full && p.K % 64 == 0 && (p.K / 64) % split == 0;
 }
 
+// VAR 40 for the dX layout (gemm_w4.h); PZ_GEMM_W4=0 keeps those GEMMs on VAR 30 (A/B)
+bool w4_default() {
+  static const bool on = [] {
+    const char* e = getenv("PZ_GEMM_W4");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
 // which specialised epilogue (gemm_epilogue.h: EK_*) covers these arguments
 int epi_kind(const GemmArgs& p) {
   if (p.out_dtype != DT_BF16 || p.accumulate) return EK_ANY;
@@ -817,6 +828,11 @@ hipError_t launch_tiles(const GemmArgs& p, hipStream_t s) {
     if (bk64) return launch_bk64_256<OutT, AuxT, 30>(p, s);
     if (buf) return launch_layout<256, 256, 2, 4, OutT, AuxT, 6>(p, s);
     return launch_layout<256, 256, 2, 4, OutT, AuxT>(p, s);
+  }
+  if constexpr (std::is_same<OutT, uint16_t>::value) {
+    const int ek = epi_kind(p);
+    if (w4_default() && w4_eligible(p, ek))
+      return ek == EK_BWD_MASK ? launch_w4<EK_BWD_MASK>(p, s) : launch_w4<EK_STORE>(p, s);
   }
   // buffer-addressed LDS-DMA (VAR 6; +2..12% on the step's shapes, tools/gemm_lab)
   if (tiles(256, 256) >= kFill) {

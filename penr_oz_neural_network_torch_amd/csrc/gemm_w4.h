@@ -1,0 +1,170 @@
+// VAR 40 — the dX GEMM (both operands K-contiguous) on 4-wave workgroups: the schedule of
+// hipBLASLt's gfx950 dX kernel (Custom_Cijk_Alik_Bljk_..._MT256x256x64, disassembled in round 6:
+// profiles/r6_hipblaslt_kernels.txt), written for this library's LDS-DMA and epilogues.
+// Included by gemm_mfma.hip inside namespace pz::(anonymous).
+//
+//   * 256 x 256 tiles, 4 waves (one per SIMD), 128 x 128 per wave: 8 x 8 16x16x32 accumulators
+//     = 256 AGPRs, mfma(B, A) so the Lay16 epilogue layout applies (gemm_epilogue.h).
+//   * TWO 64-KiB LDS buffers, one 64-deep K step each ([256][64] A then [256][64] B, 128-B rows,
+//     swz_kc<64>), filled by buffer_load ... lds: one DMA = 8 rows x 128 B (whole cache lines).
+//   * Fragments of BOTH k-halves of step t are in registers before its second half's MFMAs (sets
+//     S0 / S1), so buffer t&1 is free for step t+2's DMAs from the middle of iteration t on:
+//       phase 1: MFMAs S0 rows 0-3 + the 16 S1 reads (step t)       B1: lgkmcnt(0) + barrier
+//       phase 2-3: MFMAs S0 rows 4-7, S1 rows 0-3 + 12 DMAs (step t+2)
+//       B2: vmcnt(12) (step t+1 landed) + barrier
+//       phase 4: MFMAs S1 rows 4-7 + the 16 S0 reads (step t+1) + 4 DMAs (step t+2)
+//     The last two iterations are compile-time copies without DMAs (no wasted loads, no per-DMA
+//     branches: a per-piece guard inside the unrolled phases cost 11% in the lab).
+//   * The 128 KiB of LDS then hold the epilogue's tile image (epilogue_lds: bias-free backward
+//     kinds EK_BWD_MASK / EK_STORE, column sums, e5m2 copy — the library's own epilogue code).
+// tools/gemm_w4_lab.hip (same box, plain store): dX [8192,4096] K=4096 1436 vs 1387 TF/s (VAR 30),
+// K=1024 1095 vs 1040; the diagnostics there put the remaining gap to hipBLASLt (1569) in the
+// DMA issue itself (no-DMA build 1690 TF/s; L2-resident operands: no change).
+namespace w4 {
+constexpr int kW4M = 256, kW4N = 256, kW4K = 64, kW4T = 256;
+constexpr int kTB = kW4M * kW4K * 2 * 2;  // one K-step buffer: A + B, 64 KiB
+constexpr int kD4 = 4;                  // DMA pieces issued in phase 4 (the other 12 in phases 2-3)
+constexpr int kD23 = 16 - kD4;
+}  // namespace w4
+
+template <int EK>
+__global__ void __launch_bounds__(w4::kW4T) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_w4_kernel(const GemmArgs p) {
+  using namespace w4;
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+  const int tiles_m = p.M / kW4M, tiles_n = p.N / kW4N;
+  int tm, tn, tile_id, slice;
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+  const int m0 = tm * kW4M, n0 = tn * kW4N;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const i32x4_t rs_a = buf_rsrc(p.A), rs_b = buf_rsrc(p.B);
+  // DMA lanes: row lane/8 of an 8-row piece, 16-B chunk lane%8; the chunk swizzle of slot row r is
+  // (r >> 1) & 7, which for the piece's base row (a multiple of 8) differs between even and odd
+  // pieces by 4 — hence two lane offsets per operand
+  const int prow = lane >> 3;
+  const int pch0 = (lane & 7) ^ swz_kc<64>(prow), pch1 = (lane & 7) ^ swz_kc<64>(prow + 8);
+  const uint32_t lda = static_cast<uint32_t>(p.lda), ldb = static_cast<uint32_t>(p.ldb);
+  const uint32_t va0 = (prow * lda + pch0 * 8) * 2u, va1 = (prow * lda + pch1 * 8) * 2u;
+  const uint32_t vb0 = (prow * ldb + pch0 * 8) * 2u, vb1 = (prow * ldb + pch1 * 8) * 2u;
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t abase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m0) * lda * 2u);
+  const uint32_t bbase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n0) * ldb * 2u);
+  // piece d (16 per wave and K step): operand d / 8, rows (wave * 8 + d % 8) * 8 .. + 8
+  uint32_t soff[16], dst[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const int op = d >> 3;
+    const uint32_t rbase = static_cast<uint32_t>((wave * 8 + (d & 7)) * 8);
+    soff[d] = __builtin_amdgcn_readfirstlane((op ? bbase : abase) + rbase * (op ? ldb : lda) * 2u);
+    dst[d] = __builtin_amdgcn_readfirstlane(lds0 + static_cast<uint32_t>(op * (kTB / 2)) + rbase * 128u);
+  }
+  auto dma = [&](int kt, int d) __attribute__((always_inline)) {
+    const bool odd = d & 1;
+    blds16<0>(d >= 8 ? rs_b : rs_a, d >= 8 ? (odd ? vb1 : vb0) : (odd ? va1 : va0),
+              soff[d] + static_cast<uint32_t>(kt) * (kW4K * 2), dst[d] + static_cast<uint32_t>((kt & 1) * kTB));
+  };
+  // fragment f of k-half kh: f < 8 -> B (output columns), else A (output rows)
+  auto frag = [&](int buf, int kh, int f) __attribute__((always_inline)) -> i16x8_t {
+    const int row = (f < 8 ? wn : wm) * 128 + (f & 7) * 16 + (lane & 15);
+    return frag_kc<64>(smem + buf * kTB + (f < 8 ? kTB / 2 : 0), row, kh * 4 + (lane >> 4));
+  };
+  f32x4_t acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
+  auto mm = [&](const i16x8_t (&F)[16], int i, int j) __attribute__((always_inline)) {
+    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8_t, F[j]),
+                                                        __builtin_bit_cast(bf16x8_t, F[8 + i]), acc[i][j], 0, 0, 0);
+  };
+  i16x8_t S0[16], S1[16];
+  const int nk = p.K / kW4K;  // >= 2 (w4_eligible)
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(0, d);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(1, d);
+  wait_vm<16>();
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < 16; ++f) S0[f] = frag(0, 0, f);
+
+  // one K step; DMA: step kt+2 goes out (kt + 2 < nk); NEXT: step kt+1's S0 is read in phase 4
+  auto step = [&](int kt, auto dmac, auto nextc) __attribute__((always_inline)) {
+    constexpr bool DMA = decltype(dmac)::value, NEXT = decltype(nextc)::value;
+    const int buf = kt & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<16>([&](auto gc) {
+      constexpr int q = decltype(gc)::value;
+      mm(S0, q >> 2, 2 * (q & 3));
+      mm(S0, q >> 2, 2 * (q & 3) + 1);
+      S1[q] = frag(buf, 1, q);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // every wave has both k-halves of step kt: buffer buf is free
+    __builtin_amdgcn_sched_barrier(0);
+    static_for<64>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (c < 32) mm(S0, 4 + (c >> 3), c & 7);
+      else mm(S1, (c - 32) >> 3, c & 7);
+      constexpr int every = 64 / kD23;
+      if constexpr (DMA && c % every == every - 1 && c / every < kD23) {
+        dma(kt + 2, c / every);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+    if constexpr (NEXT) {
+      if constexpr (DMA) wait_vm<kD23>();  // step kt+1 landed; step kt+2's pieces stay in flight
+      else wait_vm<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    static_for<16>([&](auto gc) {
+      constexpr int q = decltype(gc)::value;
+      mm(S1, 4 + (q >> 2), 2 * (q & 3));
+      mm(S1, 4 + (q >> 2), 2 * (q & 3) + 1);
+      if constexpr (NEXT) S0[q] = frag(buf ^ 1, 0, q);
+      constexpr int every4 = 16 / kD4;
+      if constexpr (DMA && q % every4 == every4 - 1) dma(kt + 2, kD23 + q / every4);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  int kt = 0;
+  for (; kt < nk - 2; ++kt) step(kt, T_{}, T_{});
+  step(kt, F_{}, T_{});
+  step(kt + 1, F_{}, F_{});
+  PZ_STAMP(3);
+  // (epilogue_lds opens with a barrier: every wave is done with the operand buffers)
+  epilogue_lds<kW4M, kW4N, 2, 2, Lay16<8, 8>, false, EK>(p, acc, smem, m0, n0, wm, wn, lane, p.alpha);
+}
+
+// dX-layout bf16 GEMMs VAR 40 takes: whole 256 x 256 tiles that fill the CUs, >= 2 K steps, no
+// split-K, buffer-addressable operands, a backward-mask or plain-store epilogue
+inline bool w4_eligible(const GemmArgs& p, int ek) {
+  if (!p.a_kc || !p.b_kc || p.in_dtype != DT_BF16 || p.out_dtype != DT_BF16 || p.accumulate) return false;
+  if (p.split_k > 1 || p.M % 256 || p.N % 256 || p.K % 64 || p.K < 128) return false;
+  if (ek != EK_BWD_MASK && ek != EK_STORE) return false;
+  if ((p.M / 256) * (p.N / 256) < 240) return false;
+  constexpr int64_t kLim = int64_t(1) << 32;
+  return static_cast<int64_t>(p.M) * p.lda * 2 < kLim && static_cast<int64_t>(p.N) * p.ldb * 2 < kLim;
+}
+
+template <int EK>
+hipError_t launch_w4(const GemmArgs& p, hipStream_t s) {
+  auto kern = gemm_w4_kernel<EK>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       2 * w4::kTB);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((p.M / w4::kW4M) * (p.N / w4::kW4N)), dim3(w4::kW4T), 2 * w4::kTB, s, p);
+  return hipGetLastError();
+}

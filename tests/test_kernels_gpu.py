@@ -174,6 +174,29 @@ def test_gemm_relu_bitmask_forward_and_backward(native_lib, M, N, K):
     assert (out_bit.double() - ref).abs().max().item() < 0.02 * ref.abs().max().item()
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 128), (4096, 4096, 320), (8192, 4096, 1024)])
+def test_gemm_w4_dx_engine(native_lib, M, N, K):
+    """VAR 40 (csrc/gemm_w4.h: 4-wave LDS-DMA kernel for the dX layout, whole 256-tiles that fill
+    the CUs): plain store and the ReLU-bitmask backward epilogue with column sums == fp64 torch, at
+    the minimum two K steps, an odd step count and the mlp4 dX_L3 shape."""
+    p, seed = 0.2, (7, 9)
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    gz = torch.randn(M, K, generator=g).to(DEV, torch.bfloat16)
+    wt = torch.randn(N, K, generator=g).to(DEV, torch.bfloat16)
+    ref = gz.double() @ wt.double().t()
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    PF.gemm(gz, True, wt, True, out)
+    assert (out.double() - ref).abs().max().item() < 1e-3 * math.sqrt(K) + 0.01 * ref.abs().max().item()
+    yb = torch.randn(M, N, generator=g).to(DEV) > 0
+    mask = PF.relu_mask_pack(yb)
+    epi = PF.epi_spec(act=PF.ACT_RELU, drop_pre=1, drop_post=2, p=p, seed=seed)
+    cs = torch.zeros(N, device=DEV)
+    PF.gemm(gz, True, wt, True, out, colsum=cs, mode=PF.EPI_BWD, epi=epi, mask=mask)
+    refb = ref * yb.double() / (1 - p) ** 2
+    assert (out.double() - refb).abs().max().item() < 0.01 * refb.abs().max().item()
+    assert (cs.double() - out.double().sum(0)).abs().max().item() < 2e-3 * out.double().abs().sum(0).max().item()
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 256, 128), (8192, 8192, 1024), (300, 264, 192)])
 def test_gemm_fp8_e5m2_backward(native_lib, M, N, K):
     """Backward dX of the fp8 policy: e5m2 gradient x e4m3 weight (v_mfma_scale_f32_32x32x64_f8f6f4
