@@ -376,6 +376,9 @@ class FusedTrainer(Fp8Policy):
             self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
         # the side-stream updates of all layers but the first are queued together behind the last
         # of their gradients (one event instead of one per layer; mlp4 1.311-1.320 vs 1.321-1.326 ms)
+        # (measured again in r6, not kept: the bf16 policy's side update queued right behind its dW
+        # GEMM instead of behind the layer's dX — dX_L2 stretched 194 -> 286 us by the update beside
+        # it, the boundary shrank 96 -> 48 us: mlp4 1.141 vs 1.099 ms, profiles/r6_ab_update_early.txt)
         self._flush_key = gemm_w[1] if len(gemm_w) > 1 else None
         self._side_pending: list = []
 
