@@ -321,6 +321,16 @@ class FusedTrainer(Fp8Policy):
         # PZ_OPT_OVERLAP=0: every update on the compute stream, after the backward.
         self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
         self.opt_stream = torch.cuda.Stream(device=self.dev) if self.overlap else None
+        # One process: the steps run on a priority -1 stream of the trainer's own, so the compute
+        # stream's workgroups dispatch ahead of the side stream's updates when both have work
+        # queued — the step-end first-layer update 68 -> 50 us beside the side stream's L2 update,
+        # mlp4 1.0894 vs 1.0947 ms (3 of 3 interleaved rounds, profiles/r6_ab_main_prio.txt).
+        # Not under data parallelism: collectives issued from the caller's stream (_SaveAgreement)
+        # and the trainer's must stay on one stream per communicator. PZ_MAIN_PRIO=0: off.
+        self._main_stream = (torch.cuda.Stream(device=self.dev, priority=-1)
+                             if self.overlap and not self.ctx.enabled and os.environ.get("PZ_MAIN_PRIO", "1") != "0"
+                             else None)
+        self._main_joined = False
         # (measured, not kept: the next batch's gather on the side stream during the step, double-
         # buffered; the step-end update on a high-priority stream — each saved its 12-20 us on the
         # boundary and paid it back in cross-stream event latency, profiles/r6_ab_boundary.txt)
@@ -701,6 +711,17 @@ class FusedTrainer(Fp8Policy):
                      and want_ratios == (epoch % plan["every"] == 0) and lr == plan["lrs"][epoch]
                      and (not self.opt.adam or self.opt.step_count == plan["t0"] + epoch))
         gkey = (self.parity, batch, sample_size, float(dropout), float(l2))
+        if self._main_stream is not None:
+            if not self._main_joined:  # the caller's queued work (inputs, parameters) first
+                self._main_stream.wait_stream(torch.cuda.current_stream(self.dev))
+                self._main_joined = True
+            with torch.cuda.stream(self._main_stream):
+                self._step_on(gkey, graphable, epoch, lr, batch, dropout, l2, row, record, indices)
+        else:
+            self._step_on(gkey, graphable, epoch, lr, batch, dropout, l2, row, record, indices)
+        self._ctr_epoch = epoch + 1
+
+    def _step_on(self, gkey, graphable, epoch, lr, batch, dropout, l2, row, record, indices) -> None:
         if graphable and gkey in self._warm:
             self._replay(gkey, epoch, lr, batch, dropout, l2, row)
         else:
@@ -708,7 +729,6 @@ class FusedTrainer(Fp8Policy):
             self._pending.append((epoch, row, self._last_event))
             if graphable:
                 self._warm.add(gkey)
-        self._ctr_epoch = epoch + 1
 
     def _replay(self, gkey, epoch: int, lr: float, batch: int, dropout: float, l2: float, row) -> None:
         main = torch.cuda.current_stream(self.dev)
@@ -1326,6 +1346,7 @@ class FusedTrainer(Fp8Policy):
         if not self._pending:
             return []
         torch.cuda.synchronize(self.dev)
+        self._main_joined = False  # (device-synchronised: the next step re-joins the caller's stream)
         costs = self.costs.cpu().tolist()
         ratios = self.ratios.cpu().view(-1, max(1, self.opt.nslots)).tolist()
         out = []
