@@ -76,12 +76,13 @@ class FusedOptimizer:
         # epoch's lr / bias corrections from the table instead of the baked-in scalars
         self.graph_tables = None
 
-    def define_groups(self, keys: list[int], rest_stats: bool = True) -> None:
+    def define_groups(self, keys: list[int], rest_stats: bool = True, replicated=()) -> None:
         """Split the update into launches: one per listed segment offset (a dense weight whose
         gradient bucket is ready early in the backward) plus one for every other segment. Each
         launch is the same fused kernel over its own packed segment table. ``rest_stats=False``:
-        the rest group adds nothing to the per-weight statistics (sharded optimizer, ranks > 0:
-        rank 0's replicated copy counts once in the all-reduced sums)."""
+        the rest group and the listed ``replicated`` keys add nothing to the per-weight statistics
+        (sharded optimizer, ranks > 0: rank 0's replicated copy counts once in the all-reduced
+        sums)."""
         dev = self.store.device
         by_off = {s.offset: s for s in self.store.segments}
         rest = sorted((s for s in self.store.segments if s.offset not in set(keys)), key=lambda s: s.offset)
@@ -94,7 +95,7 @@ class FusedOptimizer:
                 starts.append(acc)
                 acc += b
             block_seg = torch.tensor(starts, dtype=torch.int64, device=dev)
-            stats = rest_stats or key != "rest"
+            stats = rest_stats or (key != "rest" and key not in replicated)
             for parity in range(len(self.shadow_sets)):
                 self.groups[(key, parity)] = (self._pack(segs, parity, stats), block_seg, len(segs), acc)
 

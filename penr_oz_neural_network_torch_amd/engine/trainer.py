@@ -200,10 +200,13 @@ class FusedTrainer(Fp8Policy):
         # with bf16 gradient buckets and the overlapped update only (fp8 keeps replicated updates:
         # its e4m3 copies and weight amax are written by the update itself). PZ_ZERO=1 forces it
         # (e.g. a forced 1-rank RCCL group, or the one-GPU collective proxy's modelled world).
-        # PZ_ZERO_SCOPE: "side" (default) shards the weights updated on the side stream while the
-        # backward runs and keeps the step-end (first-layer) update replicated — its all-reduce +
-        # update stays the boundary's one collective hop instead of reduce-scatter -> slice update ->
-        # all-gather; "all" shards every dense weight.
+        # PZ_ZERO_SCOPE: "mid" (default) shards the weights whose gradient is complete while the
+        # backward still runs (not the first layer, not its paired partner): their reduce-scatter ->
+        # slice update -> all-gather chain overlaps the rest of the backward, while the two updates
+        # that cross the step boundary stay one all-reduce hop each. "side" also shards the paired
+        # partner, "all" every dense weight. Modelled 8-rank step (tools/comm_pressure.py, 16-WG
+        # collective proxy, 3 interleaved rounds): mid +22.5%, replicated +26.4%, side +28.1%
+        # (profiles/r6_comm_pressure.txt).
         zmode = os.environ.get("PZ_ZERO", "auto")
         self.zero: ZeroShards | None = None
         if ((zmode == "1" or (zmode == "auto" and self.ctx.world_size > 1)) and self.ctx.enabled
@@ -211,7 +214,13 @@ class FusedTrainer(Fp8Policy):
                 and os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
                 and os.environ.get("PZ_GRAD_COMM_DTYPE", "bf16").lower() in ("bf16", "bfloat16")):
             dense = [st.seg_w for st in self.stages if st.kind == "gemm"]
-            sharded = dense if os.environ.get("PZ_ZERO_SCOPE", "side") == "all" else dense[1:]
+            scope = os.environ.get("PZ_ZERO_SCOPE", "mid")
+            sharded = dense if scope == "all" else dense[1:]
+            if scope == "mid":  # not the paired partner either: its update also crosses the boundary
+                cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
+                if cands and os.environ.get("PZ_DW_PAIR", "1") == "1" and self.stages[0].kind == "gemm":
+                    partner = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).seg_w
+                    sharded = [sg for sg in sharded if sg is not partner]
             if sharded:
                 self.zero = ZeroShards(self.ctx, sharded, len(self.shadow_sets), self.dev)
         self._zero_ar = False  # record step: all-reduced dense gradients (the record needs them whole)
@@ -320,6 +329,10 @@ class FusedTrainer(Fp8Policy):
         # the backward runs; the bandwidth-bound update hides behind the MFMA-bound GEMMs.
         # PZ_OPT_OVERLAP=0: every update on the compute stream, after the backward.
         self.overlap = os.environ.get("PZ_OPT_OVERLAP", "1") != "0"
+        # (measured, not kept: the side stream at priority -1 under data parallelism, so the sharded
+        # slice updates between a reduce-scatter and its all-gather dispatch ahead of the GEMMs —
+        # every compute-stream kernel stretched, modelled 8-rank step +92 vs +29%,
+        # profiles/r6_comm_pressure.txt)
         self.opt_stream = torch.cuda.Stream(device=self.dev) if self.overlap else None
         # One process: the steps run on a priority -1 stream of the trainer's own, so the compute
         # stream's workgroups dispatch ahead of the side stream's updates when both have work
@@ -379,8 +392,9 @@ class FusedTrainer(Fp8Policy):
         if self.zero is not None:
             # the sharded weights by slices; the rest group (the replicated first layer under the
             # default scope, and the small parameters) reports its statistics from rank 0 only
-            self.opt.define_groups([o for o in gemm_w if o in self.zero.shards or o in gemm_w[1:]],
-                                   rest_stats=self.zero.rank == 0)
+            keys = [o for o in gemm_w if o in self.zero.shards or o in gemm_w[1:]]
+            self._zero_repl = [o for o in keys if o not in self.zero.shards]  # replicated side-stream weights
+            self.opt.define_groups(keys, rest_stats=self.zero.rank == 0, replicated=set(self._zero_repl))
             self.zero.define_groups(self.opt)
         else:
             self.opt.define_groups(gemm_w if self.fuse_opt else gemm_w[1:])
@@ -928,7 +942,8 @@ class FusedTrainer(Fp8Policy):
             self.opt.begin_step(lr)
             gathers = [self.zero.update(self.opt, off, self.grads, l2, 1.0, 1 - self.parity, source="ar")
                        for off in self.zero.shards]
-            self.opt.step_group("rest", self.grads, l2, 1.0, 1 - self.parity)
+            for off in self._zero_repl + ["rest"]:
+                self.opt.step_group(off, self.grads, l2, 1.0, 1 - self.parity)
             for h in gathers:
                 self.ctx.wait_one(h)
             self.zero.all_reduce_stats(self.opt.stats[self.opt.cur])

@@ -51,10 +51,18 @@ def _bn_stats(model):
             for l in model.layers if l.algo == "batchnorm"]
 
 
+def _zero_env(zero, on="auto"):
+    """zero: "auto" / "1" (the default scope: weights complete mid-backward), "side" (+ the paired
+    partner), "all" (every dense weight), "0" (replicated)"""
+    os.environ.pop("PZ_ZERO_SCOPE", None)
+    os.environ["PZ_ZERO"] = on if zero in ("side", "all") else zero
+    if zero in ("side", "all"):
+        os.environ["PZ_ZERO_SCOPE"] = zero
+
+
 def _rank_main(rank, world, port, optimizer, comm, out_path, bn=False, zero="auto"):
-    # zero: "auto" (sharded side-stream weights, the default), "all" (every dense weight), "0" (replicated)
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), PZ_GRAD_COMM_DTYPE=comm,
-                      PZ_ZERO="auto" if zero == "all" else zero, PZ_ZERO_SCOPE="all" if zero == "all" else "side")
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), PZ_GRAD_COMM_DTYPE=comm)
+    _zero_env(zero)
     torch.set_num_threads(2)
     # file rendezvous (port = the store path): no TCP port picked ahead of the spawned ranks
     dist.init_process_group("gloo", init_method=f"file://{port}", rank=rank, world_size=world)
@@ -96,7 +104,8 @@ TOL = {  # (comm, world): (cost rel, adam mean |dp|, adam frac |dp| > 1e-3, sgd 
     (2, "stochastic", "bf16", False, "auto"), (2, "adam", "fp32", True, "auto"), (2, "adam", "bf16", True, "auto"),
     (2, "adam", "bf16", False, "0"), (3, "adam", "bf16", False, "auto"), (3, "stochastic", "bf16", False, "auto"),
     (3, "adam", "bf16", False, "all"), (8, "adam", "bf16", False, "auto"), (8, "adam", "bf16", False, "0"),
-    (8, "adam", "bf16", False, "all"), (8, "stochastic", "fp32", False, "auto"),
+    (8, "adam", "bf16", False, "all"), (2, "adam", "bf16", False, "side"), (8, "adam", "bf16", False, "side"),
+    (8, "stochastic", "fp32", False, "auto"),
     (8, "stochastic", "bf16", False, "auto")])
 def test_multi_rank_step_equals_single_rank(tmp_path, monkeypatch, world, optimizer, comm, bn, zero):
     """A W-rank data-parallel fused step == one rank on the concatenated batch (W ranks share the
@@ -159,8 +168,8 @@ def _forced_main(rank, comm, out_path, impl="native", zero="auto"):
     all-reduce (PZ_ZERO=1: reduce-scatter + slice update + all-gather) on its comm stream, waited
     for by the optimizer's stream."""
     os.environ.update(PZ_FORCE_COMM="1", PZ_GRAD_COMM_DTYPE=comm, PZ_COMM=impl, MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(_free_port()), PZ_ZERO="1" if zero == "all" else zero,
-                      PZ_ZERO_SCOPE="all" if zero == "all" else "side")
+                      MASTER_PORT=str(_free_port()))
+    _zero_env(zero, on="1")
     if impl == "proxy":  # (the proxy's 16 workgroups, and the GEMMs behind a bucket on 240 CUs)
         os.environ.update(PZ_COMM_PROXY_WGS="16", PZ_COMM_BUDGET="16")
     os.environ.pop("WORLD_SIZE", None)
@@ -175,7 +184,7 @@ def _forced_main(rank, comm, out_path, impl="native", zero="auto"):
     model = _build("adam", "bf16")
     tr = FusedTrainer(model, ctx)
     assert bool(tr.grads16) == (comm == "bf16")
-    assert (tr.zero is not None) == (zero in ("1", "all")), zero
+    assert (tr.zero is not None) == (zero in ("1", "side", "all")), zero
     if tr.zero is not None:  # one rank: one whole slice (the proxy shards for the world it models, as rank 0)
         assert tr.zero.world == (8 if impl == "proxy" else 1) and tr.zero.rank == 0
     # PZ_COMM_BUDGET: the backward GEMMs behind a bucket run on the persistent engine with the CUs
@@ -197,12 +206,13 @@ def _forced_main(rank, comm, out_path, impl="native", zero="auto"):
 @pytest.mark.parametrize("comm,impl,zero", [("fp32", "native", "auto"), ("bf16", "native", "auto"),
                                             ("fp32", "torch", "auto"), ("fp32", "proxy", "auto"),
                                             ("bf16", "native", "1"), ("bf16", "torch", "1"), ("bf16", "proxy", "1"),
-                                            ("bf16", "native", "all"), ("bf16", "proxy", "all")])
+                                            ("bf16", "native", "side"), ("bf16", "native", "all"),
+                                            ("bf16", "proxy", "all")])
 def test_forced_rccl_world1_matches_no_comm(tmp_path, monkeypatch, comm, impl, zero):
     out = str(tmp_path / "forced.pt")
     mp.start_processes(_forced_main, args=(comm, out, impl, zero), nprocs=1, start_method="spawn")
     got = torch.load(out, weights_only=True)
-    if impl == "proxy" and zero in ("1", "all"):
+    if impl == "proxy" and zero in ("1", "side", "all"):
         # the proxy runs the sharded step of its modelled world as rank 0 (1/8 of every weight is
         # updated): a timing model, whose numbers need only be finite
         assert all(math.isfinite(c) for c in got["costs"]) and torch.isfinite(got["flat"]).all()

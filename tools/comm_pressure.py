@@ -12,8 +12,9 @@ ms/step, interleaved over rounds (same box):
                 150 GB/s (the default schedule: full-grid tiled GEMMs)
   proxy_w<W>_sk the same with PZ_COMM_BUDGET=W: the backward GEMMs behind a bucket on the
                 persistent stream-K engine with 256 - W CUs (parallel/dist.py comm_cus)
-  zero_*        the same with the sharded optimizer (PZ_ZERO=1, engine/zero.py; zeroall_*: PZ_ZERO_SCOPE=all,
-                the first layer sharded too): reduce-scatter +
+  zero_*        the same with the sharded optimizer (PZ_ZERO=1, engine/zero.py, default scope "mid":
+                the weights complete mid-backward; zeroside_*: PZ_ZERO_SCOPE=side, + the paired
+                partner; zeroall_*: PZ_ZERO_SCOPE=all, the first layer too): reduce-scatter +
                 all-gather per weight (torch: real 1-rank RCCL calls, whole-weight slices; proxy:
                 the modelled 8-rank world as its rank 0 — 1/8 of every weight updated, the proxy
                 holding its workgroups for a ring reduce-scatter and a ring all-gather)
@@ -60,9 +61,11 @@ def main():
         cases[f"proxy_w{w}_sk"] = dict(proxy, PZ_COMM_BUDGET=str(w))
         cases[f"zero_proxy_w{w}"] = dict(proxy, PZ_ZERO="1")
         cases[f"zeroall_proxy_w{w}"] = dict(proxy, PZ_ZERO="1", PZ_ZERO_SCOPE="all")
+        cases[f"zeroside_proxy_w{w}"] = dict(proxy, PZ_ZERO="1", PZ_ZERO_SCOPE="side")
     cases["zero_torch"] = dict(forced, PZ_COMM="torch", PZ_ZERO="1")
     cases["zero_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1")
     cases["zeroall_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1", PZ_ZERO_SCOPE="all")
+    cases["zeroside_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1", PZ_ZERO_SCOPE="side")
     for c in (x for x in a.cases.split(",") if x):
         if c not in cases:
             raise SystemExit(f"unknown case {c}: {sorted(cases)}")
