@@ -20,17 +20,21 @@
 // tools/gemm_w4_lab.hip (same box, plain store): dX [8192,4096] K=4096 1436 vs 1387 TF/s (VAR 30),
 // K=1024 1095 vs 1040; the diagnostics there put the remaining gap to hipBLASLt (1569) in the
 // DMA issue itself (no-DMA build 1690 TF/s; L2-resident operands: no change).
-namespace w4 {
+namespace w4cfg {
 constexpr int kW4M = 256, kW4N = 256, kW4K = 64, kW4T = 256;
 constexpr int kTB = kW4M * kW4K * 2 * 2;  // one K-step buffer: A + B, 64 KiB
 constexpr int kD4 = 4;                  // DMA pieces issued in phase 4 (the other 12 in phases 2-3)
 constexpr int kD23 = 16 - kD4;
-}  // namespace w4
+}  // namespace w4cfg
 
-template <int EK>
-__global__ void __launch_bounds__(w4::kW4T) __attribute__((amdgpu_waves_per_eu(1, 1)))
+// B_KC = false (VAR 41, instantiated by tools/gemm_w4_lab.hip only): B M/N-contiguous ([K][N], the
+// forward's weights): its K-step slot is [64 k][256 n] (512-B rows, swz_mn), one DMA = 2 k-rows,
+// fragments by transposing ds_read_b64_tr_b16 reads (frag_mn). Measured, not dispatched: fwd_L2
+// 1,278 vs 1,286 TF/s (VAR 30), fwd_L1 926 vs 944, same box (profiles/r6_gemm_w4.txt)
+template <int EK, bool B_KC = true>
+__global__ void __launch_bounds__(w4cfg::kW4T) __attribute__((amdgpu_waves_per_eu(1, 1)))
 gemm_w4_kernel(const GemmArgs p) {
-  using namespace w4;
+  using namespace w4cfg;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
   const int tiles_m = p.M / kW4M, tiles_n = p.N / kW4N;
@@ -47,26 +51,52 @@ gemm_w4_kernel(const GemmArgs p) {
   const int pch0 = (lane & 7) ^ swz_kc<64>(prow), pch1 = (lane & 7) ^ swz_kc<64>(prow + 8);
   const uint32_t lda = static_cast<uint32_t>(p.lda), ldb = static_cast<uint32_t>(p.ldb);
   const uint32_t va0 = (prow * lda + pch0 * 8) * 2u, va1 = (prow * lda + pch1 * 8) * 2u;
-  const uint32_t vb0 = (prow * ldb + pch0 * 8) * 2u, vb1 = (prow * ldb + pch1 * 8) * 2u;
+  // B lane offsets: K-contiguous as A; M/N-contiguous: k-row lane / 32 of a 2-row piece, 16-B column
+  // chunk lane % 32 XOR swz_mn(k-row), whose bits 0-1 and 3 vary with the piece (4 classes)
+  uint32_t vb[4];
+  if constexpr (B_KC) {
+    vb[0] = vb[2] = (prow * ldb + pch0 * 8) * 2u;
+    vb[1] = vb[3] = (prow * ldb + pch1 * 8) * 2u;
+  } else {
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int kr = 2 * ((c & 1) + 4 * (c >> 1)) + (lane >> 5);  // a k-row of piece i = (c & 1) + 4 (c >> 1)
+      vb[c] = ((lane >> 5) * ldb + (((lane & 31) ^ swz_mn(kr)) * 8)) * 2u;
+    }
+  }
   const uint32_t lds0 = lds_addr(smem);
   const uint32_t abase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m0) * lda * 2u);
-  const uint32_t bbase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n0) * ldb * 2u);
-  // piece d (16 per wave and K step): operand d / 8, rows (wave * 8 + d % 8) * 8 .. + 8
+  const uint32_t bbase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n0) * (B_KC ? ldb : 1u) * 2u);
+  // K-step advance of a piece's source: 64 elements of a K-contiguous row, 64 rows of an
+  // M/N-contiguous operand
+  const uint32_t bstep = __builtin_amdgcn_readfirstlane(B_KC ? kW4K * 2u : kW4K * ldb * 2u);
+  // piece d (16 per wave and K step): operand d / 8, 1 KiB at (wave * 8 + d % 8) KiB of the slot
+  // (K-contiguous: rows 8 (wave * 8 + d % 8) .. + 8; M/N-contiguous B: k-rows 2 (wave * 8 + d % 8) .. + 2)
   uint32_t soff[16], dst[16];
 #pragma unroll
   for (int d = 0; d < 16; ++d) {
     const int op = d >> 3;
-    const uint32_t rbase = static_cast<uint32_t>((wave * 8 + (d & 7)) * 8);
-    soff[d] = __builtin_amdgcn_readfirstlane((op ? bbase : abase) + rbase * (op ? ldb : lda) * 2u);
-    dst[d] = __builtin_amdgcn_readfirstlane(lds0 + static_cast<uint32_t>(op * (kTB / 2)) + rbase * 128u);
+    const uint32_t piece = static_cast<uint32_t>(wave * 8 + (d & 7));
+    if (op == 0 || B_KC)
+      soff[d] = __builtin_amdgcn_readfirstlane((op ? bbase : abase) + piece * 8u * (op ? ldb : lda) * 2u);
+    else
+      soff[d] = __builtin_amdgcn_readfirstlane(bbase + piece * 2u * ldb * 2u);
+    dst[d] = __builtin_amdgcn_readfirstlane(lds0 + static_cast<uint32_t>(op * (kTB / 2)) + piece * 1024u);
   }
   auto dma = [&](int kt, int d) __attribute__((always_inline)) {
-    const bool odd = d & 1;
-    blds16<0>(d >= 8 ? rs_b : rs_a, d >= 8 ? (odd ? vb1 : vb0) : (odd ? va1 : va0),
-              soff[d] + static_cast<uint32_t>(kt) * (kW4K * 2), dst[d] + static_cast<uint32_t>((kt & 1) * kTB));
+    const int i = d & 7;
+    if (d < 8)
+      blds16<0>(rs_a, (i & 1) ? va1 : va0, soff[d] + static_cast<uint32_t>(kt) * (kW4K * 2),
+                dst[d] + static_cast<uint32_t>((kt & 1) * kTB));
+    else
+      blds16<0>(rs_b, vb[(i & 1) + 2 * (i >> 2)], soff[d] + static_cast<uint32_t>(kt) * bstep,
+                dst[d] + static_cast<uint32_t>((kt & 1) * kTB));
   };
   // fragment f of k-half kh: f < 8 -> B (output columns), else A (output rows)
   auto frag = [&](int buf, int kh, int f) __attribute__((always_inline)) -> i16x8_t {
+    if constexpr (!B_KC) {
+      if (f < 8) return frag_mn<kW4N>(smem + buf * kTB + kTB / 2, wn * 128 + f * 16, 8 * (lane >> 4) + 32 * kh, lane);
+    }
     const int row = (f < 8 ? wn : wm) * 128 + (f & 7) * 16 + (lane & 15);
     return frag_kc<64>(smem + buf * kTB + (f < 8 ? kTB / 2 : 0), row, kh * 4 + (lane >> 4));
   };
@@ -155,16 +185,16 @@ inline bool w4_eligible(const GemmArgs& p, int ek) {
   return static_cast<int64_t>(p.M) * p.lda * 2 < kLim && static_cast<int64_t>(p.N) * p.ldb * 2 < kLim;
 }
 
-template <int EK>
+template <int EK, bool B_KC = true>
 hipError_t launch_w4(const GemmArgs& p, hipStream_t s) {
-  auto kern = gemm_w4_kernel<EK>;
+  auto kern = gemm_w4_kernel<EK, B_KC>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       2 * w4::kTB);
+                                       2 * w4cfg::kTB);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  hipLaunchKernelGGL(kern, dim3((p.M / w4::kW4M) * (p.N / w4::kW4N)), dim3(w4::kW4T), 2 * w4::kTB, s, p);
+  hipLaunchKernelGGL(kern, dim3((p.M / w4cfg::kW4M) * (p.N / w4cfg::kW4N)), dim3(w4cfg::kW4T), 2 * w4cfg::kTB, s, p);
   return hipGetLastError();
 }

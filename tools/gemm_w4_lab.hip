@@ -762,31 +762,34 @@ __global__ void fill_bf16(uint16_t* p, int64_t n, uint32_t seed) {
 }
 
 __global__ void ref_rows(const uint16_t* A, const uint16_t* B, float* R, int N, int K, int64_t lda, int64_t ldb,
-                         int stride) {
+                         int stride, int b_kc) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t m = static_cast<int64_t>(blockIdx.y) * stride;
   if (n >= N) return;
   float acc = 0.f;
-  for (int k = 0; k < K; ++k) acc += bf2f(A[m * lda + k]) * bf2f(B[static_cast<int64_t>(n) * ldb + k]);
+  for (int k = 0; k < K; ++k)
+    acc += bf2f(A[m * lda + k]) * bf2f(b_kc ? B[static_cast<int64_t>(n) * ldb + k] : B[static_cast<int64_t>(k) * ldb + n]);
   R[static_cast<int64_t>(blockIdx.y) * N + n] = acc;
 }
 
 typedef hipError_t (*LaunchFn)(const GemmArgs&, hipStream_t);
 
 int main(int argc, char** argv) {
-  struct Case { const char* name; int M, N, K; };
-  std::vector<Case> cases = {{"dX_L2", 8192, 4096, 4096}, {"dX_L3", 8192, 4096, 1024}};
   struct V { const char* name; LaunchFn fn; };
-  std::vector<V> vs = {{"lib_var30", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
-                       {"w4_dma0", w4::launch_dma<0>}, {"w4_dma4", w4::launch_dma<4>},
-                       {"w4_dma8", w4::launch_dma<8>},
-                       {"w4_dmap4", w4::launch_dmap<4>}, {"w4_dmap8", w4::launch_dmap<8>},
-                       {"dmap8_hot", w4::launch_dmap<8, 1>}, {"dmap8_nodma", w4::launch_dmap<8, 2>},
-                       {"dmap4_full", w4::launch_dmap<4, 3>}, {"dmap8_full", w4::launch_dmap<8, 3>},
-                       {"dmap4_noswz", w4::launch_dmap<4, 4>}, {"dmap4_gnat", w4::launch_dmap<4, 6>}};
+  struct Case { const char* name; int M, N, K; bool b_kc; std::vector<V> vs; };
+  // dX_*: B [N][K] (K-contiguous); fwd_*: B [K][N] (N-contiguous, the forward's weights). Earlier
+  // variants (w4::launch_dma<D4>, launch_dmap<D4, MODE> diagnostics) stay instantiable here.
+  const std::vector<V> dx = {{"lib_var30", launch_cfg<256, 256, 2, 4, true, true, uint16_t, uint16_t, 30>},
+                             {"var40", launch_w4<EK_STORE, true>}, {"dmap4_full", w4::launch_dmap<4, 3>},
+                             {"dmap8_nodma", w4::launch_dmap<8, 2>}};
+  const std::vector<V> fw = {{"lib_var30", launch_cfg<256, 256, 2, 4, true, false, uint16_t, uint16_t, 30>},
+                             {"var41", launch_w4<EK_STORE, false>}};
+  std::vector<Case> cases = {{"dX_L2", 8192, 4096, 4096, true, dx}, {"dX_L3", 8192, 4096, 1024, true, dx},
+                             {"fwd_L2", 8192, 4096, 4096, false, fw}, {"fwd_L1", 8192, 4096, 1024, false, fw}};
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (const Case& c : cases) {
+    const std::vector<V>& vs = c.vs;
     const int64_t na = int64_t(c.M) * c.K, nb = int64_t(c.N) * c.K, nc = int64_t(c.M) * c.N;
     uint16_t *A, *B, *C;
     float* R;
@@ -797,16 +800,17 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&R, int64_t(nref) * c.N * 4));
     hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, A, na, 12345u);
     hipLaunchKernelGGL(fill_bf16, dim3(4096), dim3(256), 0, st, B, nb, 777u);
+    const int64_t ldb = c.b_kc ? c.K : c.N;
     hipLaunchKernelGGL(ref_rows, dim3((c.N + 255) / 256, nref), dim3(256), 0, st, A, B, R, c.N, c.K, int64_t(c.K),
-                       int64_t(c.K), stride);
+                       ldb, stride, int(c.b_kc));
     std::vector<float> ref(size_t(nref) * c.N);
     CK(hipMemcpyAsync(ref.data(), R, ref.size() * 4, hipMemcpyDeviceToHost, st));
     CK(hipStreamSynchronize(st));
     GemmArgs p{};
     p.A = A; p.B = B; p.C = C;
     p.M = c.M; p.N = c.N; p.K = c.K;
-    p.lda = c.K; p.ldb = c.K; p.ldc = c.N;
-    p.a_kc = 1; p.b_kc = 1;
+    p.lda = c.K; p.ldb = ldb; p.ldc = c.N;
+    p.a_kc = 1; p.b_kc = c.b_kc;
     p.in_dtype = DT_BF16; p.out_dtype = DT_BF16;
     p.alpha = 1.f; p.epi_mode = EPI_STORE; p.idx_ld = c.N; p.split_k = 1;
     const double flop = 2.0 * c.M * c.N * c.K;
