@@ -341,6 +341,8 @@ def main(argv=None) -> int:
     elapsed = ctx.all_reduce_scalar_max(elapsed)
 
     costs = [c for _, c, _, _ in trainer.drain()]
+    if os.environ.get("PZ_BENCH_SERIES") == "1" and rank == 0:  # per-step GPU periods (the trainer's events)
+        log("step periods (ms): " + " ".join(f"{trainer.step_ms[e]:.3f}" for e in sorted(trainer.step_ms)))
     _emit(args, cfg, world, elapsed, costs, batch, ctx, trainer)
     from penr_oz_neural_network_torch_amd.parallel import shutdown
     shutdown()  # the native RCCL communicator, then the process group
