@@ -216,11 +216,9 @@ class FusedTrainer(Fp8Policy):
             dense = [st.seg_w for st in self.stages if st.kind == "gemm"]
             scope = os.environ.get("PZ_ZERO_SCOPE", "mid")
             sharded = dense if scope == "all" else dense[1:]
-            if scope == "mid":  # not the paired partner either: its update also crosses the boundary
-                cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
-                if cands and os.environ.get("PZ_DW_PAIR", "1") == "1" and self.stages[0].kind == "gemm":
-                    partner = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).seg_w
-                    sharded = [sg for sg in sharded if sg is not partner]
+            partner = self._pair_partner()
+            if scope == "mid" and partner is not None:  # its update also crosses the boundary
+                sharded = [sg for sg in sharded if sg is not partner.seg_w]
             if sharded:
                 self.zero = ZeroShards(self.ctx, sharded, len(self.shadow_sets), self.dev)
         self._zero_ar = False  # record step: all-reduced dense gradients (the record needs them whole)
@@ -382,12 +380,8 @@ class FusedTrainer(Fp8Policy):
         # the backward (mlp4: 8 MB of bf16, ~14 MB of ring traffic per GPU at 8 ranks, ~50 us on
         # xGMI) while the pair saves ~60 us of GEMM time against two split-4 launches
         # (profiles/r5_step_timeline_dpnone.txt: 91 + 101 us vs 130 us paired).
-        self._pair_idx = None
-        if (os.environ.get("PZ_DW_PAIR", "1") == "1" and not self.fuse_opt
-                and self.overlap and self.stages[0].kind == "gemm"):
-            cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
-            if cands:
-                self._pair_idx = min(cands, key=lambda st: (st.seg_w.numel, -st.index)).index
+        partner = self._pair_partner() if not self.fuse_opt and self.overlap else None
+        self._pair_idx = partner.index if partner is not None else None
         self._early_keys = set() if self.fuse_opt else set(gemm_w[1:])
         if self.zero is not None:
             # the sharded weights by slices; the rest group (the replicated first layer under the
@@ -452,6 +446,14 @@ class FusedTrainer(Fp8Policy):
     # ------------------------------------------------------------------------------------
     # data
     # ------------------------------------------------------------------------------------
+    def _pair_partner(self) -> Stage | None:
+        """The GEMM stage whose dW launch is deferred and paired with the first layer's: the later
+        stage with the fewest weight elements (PZ_DW_PAIR=0: none)."""
+        if os.environ.get("PZ_DW_PAIR", "1") != "1" or self.stages[0].kind != "gemm":
+            return None
+        cands = [st for st in self.stages if st.kind == "gemm" and st.index > 0]
+        return min(cands, key=lambda st: (st.seg_w.numel, -st.index)) if cands else None
+
     def load_data(self, data) -> None:
         """Training pairs (python lists) -> device tensors, once per ``train()`` call."""
         inputs = [inp for inp, _ in data]
