@@ -913,6 +913,9 @@ class FusedTrainer(Fp8Policy):
             # side updates not flushed by their last layer (the paired partner's) join the side
             # stream behind the SAME event: one record on this stream fewer (~7 us of idle; the
             # side stream is still busy with the earlier layers' updates when it comes)
+            # (measured, not kept: the partner's update on this stream behind the first layer's
+            # instead of beside the next fwd_L1 — mlp4 1.097-1.102 vs 1.092-1.094 ms, fp8 mlp8192
+            # 0.561-0.567 vs 0.536-0.539, profiles/r6_ab_partner_main.txt)
             if pending:
                 self._opt_async(pending, ready=rest_ev)
             self._ov = None
