@@ -757,7 +757,8 @@ bool use_bk64(const GemmArgs& p, bool buf) {
   return buf && full && p.K % 64 == 0 && (p.K / 64) % split == 0;
 }
 
-// VAR 40 for the dX layout (gemm_w4.h); PZ_GEMM_W4=0 keeps those GEMMs on VAR 30 (A/B)
+// VAR 40 / 42 for the bf16 / fp8 dX layout (gemm_w4.h); PZ_GEMM_W4=0 keeps those GEMMs on VAR 30 /
+// VAR 9, 17 (A/B)
 bool w4_default() {
   static const bool on = [] {
     const char* e = getenv("PZ_GEMM_W4");
@@ -867,6 +868,12 @@ hipError_t launch_fp8(const GemmArgs& p, hipStream_t s) {
                           // plain store)
     return launch_cfg<256, 256, 2, 4, false, false, uint16_t, uint16_t, 14, EK_STORE>(p, s);
   int ek = epi_kind(p);
+  // VAR 43: the fp8 forward on the 4-wave LDS-DMA schedule, plain stores at K >= 2048 (at K = 1,024 it
+  // ties VAR 16). With the fused stage epilogues the 32x32 accumulator layout's 128-column wave rows
+  // (16 four-column groups per lane: values, column sums, bias) spill 66-213 VGPRs — the fused fp8 dX
+  // (VAR 42, tools/gemm_w4f8_lab.hip) ran 144 vs 106 us in the mlp8192 step (profiles/r6_gemm_w4.txt) —
+  // so the trainer's fused fp8 GEMMs stay on VAR 9 / 15-17
+  if (w4_default() && ek == EK_STORE && p.K >= 2048 && w4f8_fwd_eligible(p, ek)) return launch_w4f8<EK_STORE, false>(p, s);
   if (f8_two_wg(p)) {
     if (p.a_kc && !p.b_kc) {
       if (ek == EK_RELU) return launch_cfg<256, 128, 2, 2, true, false, uint16_t, uint16_t, 16, EK_RELU>(p, s);

@@ -27,7 +27,7 @@ constexpr int kD4 = 4;                  // DMA pieces issued in phase 4 (the oth
 constexpr int kD23 = 16 - kD4;
 }  // namespace w4cfg
 
-// B_KC = false (VAR 41, instantiated by tools/gemm_w4_lab.hip only): B M/N-contiguous ([K][N], the
+// B_KC = false (instantiated by tools/gemm_w4_lab.hip only): B M/N-contiguous ([K][N], the
 // forward's weights): its K-step slot is [64 k][256 n] (512-B rows, swz_mn), one DMA = 2 k-rows,
 // fragments by transposing ds_read_b64_tr_b16 reads (frag_mn). Measured, not dispatched: fwd_L2
 // 1,278 vs 1,286 TF/s (VAR 30), fwd_L1 926 vs 944, same box (profiles/r6_gemm_w4.txt)
@@ -188,6 +188,195 @@ inline bool w4_eligible(const GemmArgs& p, int ek) {
 template <int EK, bool B_KC = true>
 hipError_t launch_w4(const GemmArgs& p, hipStream_t s) {
   auto kern = gemm_w4_kernel<EK, B_KC>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       2 * w4cfg::kTB);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kern, dim3((p.M / w4cfg::kW4M) * (p.N / w4cfg::kW4N)), dim3(w4cfg::kW4T), 2 * w4cfg::kTB, s, p);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------------
+// VAR 42 / 43 — the same schedule for the fp8 policy's dX / forward GEMMs. Lab (tools/gemm_w4f8_lab.hip,
+// plain store, same box, TF/s median): dX [8192,8192] K=1024 1,584 vs 1,341 (VAR 17), [8192,4096]
+// K=4096 2,479 vs 1,743; forward [8192,4096] K=4096 2,464 vs 2,262 (VAR 15), [8192,8192] K=1024
+// 1,602 vs 1,598 (VAR 16). VAR 42 = the dX GEMM (e5m2 dZ x e4m3 W, both K-contiguous) on
+// v_mfma_scale_f32_32x32x64_f8f6f4 (unit E8M0 block scales; the per-tensor dequant scales go into
+// the epilogue's alpha). A 128-byte K step of fp8 is the bf16 kernel's slot geometry ([256][128 B],
+// swz_kc<64>, the same DMA pieces); each 64-byte k-half is ONE 32x32x64 MFMA per 32x32 tile:
+// 4 x 4 tiles per wave (f32x16 accumulators = 256 AGPRs), 16 MFMAs per k-half of 64 cycles each —
+// the bf16 kernel's 64 x 16 cycles — so the phases, DMA spread and barriers carry over unchanged.
+// B_KC = false (VAR 43): the fp8 forward X8 (e4m3, K-contiguous) x W8 (e4m3 [in, out], N-contiguous):
+// B's K-step slot is [128 k][256 B] (one DMA = 4 k-rows, swz_mn8<256>), read per 64-k half with the
+// transposing ds_read_b64_tr_b8 (frag_mn8) — the same natural-layout weight copy VAR 15 / 16 read
+template <int EK, bool B_KC = true>
+__global__ void __launch_bounds__(w4cfg::kW4T) __attribute__((amdgpu_waves_per_eu(1, 1)))
+gemm_w4f8_kernel(const GemmArgs p) {
+  using namespace w4cfg;
+  constexpr int kStep = 128;  // K bytes (= fp8 elements) per K step
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  PZ_LDS char* smem = (PZ_LDS char*)(smem_raw);
+  const int tiles_m = p.M / kW4M, tiles_n = p.N / kW4N;
+  int tm, tn, tile_id, slice;
+  tile_coords(xcd_remap(blockIdx.x, gridDim.x), tiles_m, tiles_n, 1, tm, tn, tile_id, slice);
+  const int m0 = tm * kW4M, n0 = tn * kW4N;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int wm = wave >> 1, wn = wave & 1;
+  const i32x4_t rs_a = buf_rsrc(p.A), rs_b = buf_rsrc(p.B);
+  const int prow = lane >> 3;
+  const int pch0 = (lane & 7) ^ swz_kc<64>(prow), pch1 = (lane & 7) ^ swz_kc<64>(prow + 8);
+  const uint32_t lda = static_cast<uint32_t>(p.lda), ldb = static_cast<uint32_t>(p.ldb);  // bytes
+  const uint32_t va0 = prow * lda + pch0 * 16, va1 = prow * lda + pch1 * 16;
+  // B lane offsets: K-contiguous as A; N-contiguous: k-row lane / 16 of a 4-row piece, 16-B chunk
+  // lane % 16 XOR ((k-row & 7) << 1), whose k-row bits vary with the piece's parity
+  uint32_t vb0, vb1;
+  if constexpr (B_KC) {
+    vb0 = prow * ldb + pch0 * 16;
+    vb1 = prow * ldb + pch1 * 16;
+  } else {
+    const int kq = lane >> 4;
+    vb0 = kq * ldb + ((lane & 15) ^ (((0 + kq) & 7) << 1)) * 16;
+    vb1 = kq * ldb + ((lane & 15) ^ (((4 + kq) & 7) << 1)) * 16;
+  }
+  const uint32_t lds0 = lds_addr(smem);
+  const uint32_t abase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(m0) * lda);
+  const uint32_t bbase = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(n0) * (B_KC ? ldb : 1u));
+  const uint32_t bstep = __builtin_amdgcn_readfirstlane(B_KC ? static_cast<uint32_t>(kStep) : kStep * ldb);
+  uint32_t soff[16], dst[16];
+#pragma unroll
+  for (int d = 0; d < 16; ++d) {
+    const int op = d >> 3;
+    const uint32_t piece = static_cast<uint32_t>(wave * 8 + (d & 7));
+    if (op == 0 || B_KC)
+      soff[d] = __builtin_amdgcn_readfirstlane((op ? bbase : abase) + piece * 8u * (op ? ldb : lda));
+    else
+      soff[d] = __builtin_amdgcn_readfirstlane(bbase + piece * 4u * ldb);
+    dst[d] = __builtin_amdgcn_readfirstlane(lds0 + static_cast<uint32_t>(op * (kTB / 2)) + piece * 1024u);
+  }
+  auto dma = [&](int kt, int d) __attribute__((always_inline)) {
+    const bool odd = d & 1;
+    if (d < 8)
+      blds16<0>(rs_a, odd ? va1 : va0, soff[d] + static_cast<uint32_t>(kt) * kStep,
+                dst[d] + static_cast<uint32_t>((kt & 1) * kTB));
+    else
+      blds16<0>(rs_b, odd ? vb1 : vb0, soff[d] + static_cast<uint32_t>(kt) * bstep,
+                dst[d] + static_cast<uint32_t>((kt & 1) * kTB));
+  };
+  // fragment f of k-half kh: f < 4 -> B (32 output columns each), else A (32 output rows); lane l
+  // holds row l & 31, k bytes [32 (l >> 5), +32) of the half = 16-B chunks 4 kh + 2 (l >> 5) + {0, 1}
+  auto frag = [&](int buf, int kh, int f) __attribute__((always_inline)) -> i32x8_t {
+    const PZ_LDS char* t = smem + buf * kTB + (f < 4 ? kTB / 2 : 0);
+    if constexpr (!B_KC) {  // the half's [64 k][256 B] image, transposing 8-bit reads
+      if (f < 4) return frag_mn8<kW4N>(t + kh * 64 * kW4N, wn * 128 + f * 32, lane);
+    }
+    const int row = (f < 4 ? wn : wm) * 128 + (f & 3) * 32 + (lane & 31);
+    const int c = 4 * kh + 2 * (lane >> 5);
+    return cat_frag(frag_kc<64>(t, row, c), frag_kc<64>(t, row, c + 1));
+  };
+  f32x16_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x16_t{};
+  auto mm = [&](const i32x8_t (&F)[8], int i, int j) __attribute__((always_inline)) {
+    // issued as mfma(B, A): cbsz = B's format (e4m3 = 0), blgp = A's (e5m2 = 1 in the backward,
+    // e4m3 = 0 in the forward); E8M0 127 = 1.0
+    acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(F[j], F[4 + i], acc[i][j], 0, B_KC ? 1 : 0, 0, 127,
+                                                                 0, 127);
+  };
+  i32x8_t S0[8], S1[8];
+  const int nk = p.K / kStep;  // >= 2 (w4f8_eligible)
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(0, d);
+#pragma unroll
+  for (int d = 0; d < 16; ++d) dma(1, d);
+  wait_vm<16>();
+  __syncthreads();
+#pragma unroll
+  for (int f = 0; f < 8; ++f) S0[f] = frag(0, 0, f);
+
+  auto step = [&](int kt, auto dmac, auto nextc) __attribute__((always_inline)) {
+    constexpr bool DMA = decltype(dmac)::value, NEXT = decltype(nextc)::value;
+    const int buf = kt & 1;
+    __builtin_amdgcn_sched_barrier(0);
+    // phase 1: S0 rows 0-1 (8 MFMAs) + the 8 S1 reads (step kt, second k-half)
+    static_for<8>([&](auto gc) {
+      constexpr int q = decltype(gc)::value;
+      mm(S0, q >> 2, q & 3);
+      S1[q] = frag(buf, 1, q);
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // every wave has both k-halves of step kt: buffer buf is free
+    __builtin_amdgcn_sched_barrier(0);
+    // phases 2-3: S0 rows 2-3, S1 rows 0-1 (16 MFMAs) + 12 DMAs of step kt+2
+    static_for<16>([&](auto cc) {
+      constexpr int c = decltype(cc)::value;
+      if constexpr (c < 8) mm(S0, 2 + (c >> 2), c & 3);
+      else mm(S1, (c - 8) >> 2, c & 3);
+      if constexpr (DMA && c < kD23) {
+        dma(kt + 2, c);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+    if constexpr (NEXT) {
+      if constexpr (DMA) wait_vm<kD23>();
+      else wait_vm<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // phase 4: S1 rows 2-3 (8 MFMAs) + the 8 S0 reads of step kt+1 + 4 DMAs
+    static_for<8>([&](auto gc) {
+      constexpr int q = decltype(gc)::value;
+      mm(S1, 2 + (q >> 2), q & 3);
+      if constexpr (NEXT) S0[q] = frag(buf ^ 1, 0, q);
+      if constexpr (DMA && (q & 1)) dma(kt + 2, kD23 + (q >> 1));
+      __builtin_amdgcn_sched_barrier(0);
+    });
+  };
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  int kt = 0;
+  for (; kt < nk - 2; ++kt) step(kt, T_{}, T_{});
+  step(kt, F_{}, T_{});
+  step(kt + 1, F_{}, F_{});
+  const float alpha = p.alpha * (p.scale_a != nullptr ? *p.scale_a : 1.f) * (p.scale_b != nullptr ? *p.scale_b : 1.f);
+  epilogue_lds<kW4M, kW4N, 2, 2, Lay32<4, 4>, !B_KC, EK>(p, acc, smem, m0, n0, wm, wn, lane, alpha);
+}
+
+// the fp8 policy's dX GEMMs VAR 42 takes (e5m2 x e4m3, both K-contiguous): whole 256 x 256 tiles
+// that fill the CUs, >= 2 K steps of 128 bytes, no split-K, buffer-addressable operands
+inline bool w4f8_eligible(const GemmArgs& p, int ek) {
+  if (!p.a_kc || !p.b_kc || p.in_dtype != DT_FP8 || p.a_fmt != 1 || p.b_fmt != 0 || p.out_dtype != DT_BF16 ||
+      p.accumulate)
+    return false;
+  if (p.split_k > 1 || p.M % 256 || p.N % 256 || p.K % 128 || p.K < 256) return false;
+  if (ek != EK_BWD_MASK && ek != EK_ANY && ek != EK_STORE) return false;
+  if ((p.M / 256) * (p.N / 256) < 240) return false;
+  constexpr int64_t kLim = int64_t(1) << 32;
+  return static_cast<int64_t>(p.M) * p.lda < kLim && static_cast<int64_t>(p.N) * p.ldb < kLim;
+}
+
+// the fp8 forward GEMMs VAR 43 takes (e4m3 x e4m3 [in, out] weights): same shape conditions
+inline bool w4f8_fwd_eligible(const GemmArgs& p, int ek) {
+  if (!p.a_kc || p.b_kc || p.in_dtype != DT_FP8 || p.a_fmt != 0 || p.b_fmt != 0 || p.out_dtype != DT_BF16 ||
+      p.accumulate || p.epi_mode == EPI_BWD)
+    return false;
+  if (p.split_k > 1 || p.M % 256 || p.N % 256 || p.K % 128 || p.K < 256) return false;
+  if (!ek_fixed(ek) && ek != EK_RELU && ek != EK_STORE) return false;
+  if ((p.M / 256) * (p.N / 256) < 240) return false;
+  constexpr int64_t kLim = int64_t(1) << 32;
+  return static_cast<int64_t>(p.M) * p.lda < kLim && static_cast<int64_t>(p.K) * p.ldb < kLim;
+}
+
+template <int EK, bool B_KC = true>
+hipError_t launch_w4f8(const GemmArgs& p, hipStream_t s) {
+  auto kern = gemm_w4f8_kernel<EK, B_KC>;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kern), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -340,6 +340,21 @@ def test_gemm_fp8_forward_natural_weights(native_lib, M, N, K):
     assert abs(amax.item() - amaxt.item()) <= 2 ** -7 * amaxt.item()
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 2048), (8192, 4096, 4096)])
+def test_gemm_w4_fp8_forward_plain(native_lib, M, N, K):
+    """VAR 43 (csrc/gemm_w4.h, plain stores, K >= 2048): e4m3 activations x the [in, out] e4m3 weights
+    == fp64 torch on the same fp8 values with the per-tensor scales applied."""
+    g = torch.Generator(device="cpu").manual_seed(K)
+    sa, sb = torch.tensor([0.25], device=DEV), torch.tensor([1.0 / 32], device=DEV)
+    x4 = (torch.randn(M, K, generator=g) * 4).to(DEV).to(torch.float8_e4m3fn)
+    w4n = (torch.randn(K, N, generator=g) * 2).to(DEV).to(torch.float8_e4m3fn)  # [in, out]
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    assert PF.gemm_path(x4, True, w4n, False, out) == "mfma"
+    PF.gemm(x4, True, w4n, False, out, scale_a=sa, scale_b=sb)
+    ref = (x4.double() @ w4n.double()) * (0.25 / 32)
+    assert (out.double() - ref).abs().max().item() < 0.01 * ref.abs().max().item()
+
+
 @pytest.mark.parametrize("M,N,K", [(512, 768, 1024), (8192, 8192, 1024)])
 def test_gemm_fp8_backward_store_c_false(native_lib, M, N, K):
     """e5m2 x e4m3 dX GEMM with store_c=False: only the e5m2 dZ copy, its amax and the bias-gradient
