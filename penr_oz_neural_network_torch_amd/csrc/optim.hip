@@ -393,6 +393,8 @@ hipError_t optimizer_step(const OptArgs& a, hipStream_t s) {
     else hipLaunchKernelGGL((optimizer_kernel<false, double, 1>), dim3(grid), dim3(kThreads), 0, s, a);
   } else {
     // non-temporal state streams (r4 A/B: mlp4 1.1081 -> 1.1023 ms)
+    // (measured r6, not kept: 2 / 4 preloaded vector groups for the one-round launches — step-end
+    // first layer, head weight — mlp4 1.101-1.112 vs 1.088-1.094 ms, profiles/r6_ab_opt_pre_small.txt)
     if (a.adam) hipLaunchKernelGGL((optimizer_kernel<true, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((optimizer_kernel<false, float, 1, true>), dim3(grid), dim3(kThreads), 0, s, a);
   }

@@ -1,14 +1,9 @@
 #!/bin/bash
-# round-6 session: per-kernel HBM traffic of the mlp4 step (two rocprofv3 --pmc passes, kernel trace only)
+# round-6 session: preload depth of the one-round optimizer launches (PZ_OPT_PRE_SMALL) A/B, mlp4
 set -e
-repo=$(pwd)
-out=$repo/gpurun_out/pmc_step
+out=gpurun_out/r6d13
 mkdir -p $out
-cd /tmp && export TMPDIR=/tmp
-timeout -s KILL 200 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$out/f" -o run --output-format csv \
-  -- python3 "$repo/bench.py" --steps 6 --warmup 3 > "$out/f.log" 2>&1
-timeout -s KILL 200 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$out/w" -o run --output-format csv \
-  -- python3 "$repo/bench.py" --steps 6 --warmup 3 > "$out/w.log" 2>&1
-cd "$repo"
-python3 tools/pmc_step_summary.py gpurun_out/pmc_step > gpurun_out/pmc_step/summary.txt 2>&1 || true
-head -30 gpurun_out/pmc_step/summary.txt
+PZ_OPT_PRE_SMALL=4 timeout -k 10 240 python -u -m pytest tests/test_engine_gpu.py -q --timeout 120 --timeout-method thread -k "reproducible or bench_shape" > $out/tests.txt 2>&1 || { tail -30 $out/tests.txt; exit 1; }
+tail -1 $out/tests.txt
+ROUNDS=3 ARGS="--steps 100 --warmup 20" timeout -k 10 900 tools/ab_bench.sh "base=" "pre2=PZ_OPT_PRE_SMALL=2" "pre4=PZ_OPT_PRE_SMALL=4" > $out/ab.txt 2>&1
+cat $out/ab.txt
