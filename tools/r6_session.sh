@@ -1,13 +1,7 @@
 #!/bin/bash
-# round-6 session: 8-rank gloo rehearsal of the driver's DP bench command (all ranks on the one GPU; host
-# collectives, so the time is meaningless — the check is that the 8-rank sharded-optimizer path runs and
-# reports one JSON line), then the forced 1-rank RCCL bench with the sharded optimizer
+# round-6 session: the round's two step-level defaults against their switches, 5 interleaved rounds, mlp4
 set -e
-out=gpurun_out/r6d14
+out=gpurun_out/r6d15
 mkdir -p $out
-PZ_DIST_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 \
-  --master-port 29541 bench.py --gpus 8 --steps 3 --warmup 1 > $out/bench_gloo8.txt 2>&1 || { tail -30 $out/bench_gloo8.txt; exit 1; }
-grep '"metric"' $out/bench_gloo8.txt | cut -c1-160
-grep -o '"optimizer_sharding": "[a-z0-9]*"\|"parallelism": "[a-z0-9]*"\|"n_gpus": [0-9]*' $out/bench_gloo8.txt
-PZ_FORCE_COMM=1 PZ_ZERO=1 MASTER_ADDR=127.0.0.1 MASTER_PORT=29542 timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $out/bench_forced_zero.txt 2>&1 || { tail -30 $out/bench_forced_zero.txt; exit 1; }
-grep -o '"ms_per_step": [0-9.]*\|"optimizer_sharding": "[a-z0-9]*"' $out/bench_forced_zero.txt
+ROUNDS=5 ARGS="--steps 100 --warmup 20" timeout -k 10 1000 tools/ab_bench.sh "r6=" "no_var40=PZ_GEMM_W4=0" "no_prio=PZ_MAIN_PRIO=0" "r5_like=PZ_GEMM_W4=0,PZ_MAIN_PRIO=0" > $out/ab.txt 2>&1
+cat $out/ab.txt
