@@ -63,6 +63,7 @@ def main():
         cases[f"zeroall_proxy_w{w}"] = dict(proxy, PZ_ZERO="1", PZ_ZERO_SCOPE="all")
         cases[f"zeroside_proxy_w{w}"] = dict(proxy, PZ_ZERO="1", PZ_ZERO_SCOPE="side")
     cases["zero_torch"] = dict(forced, PZ_COMM="torch", PZ_ZERO="1")
+    cases["zero_native"] = dict(forced, PZ_COMM="native", PZ_ZERO="1")
     cases["zero_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1")
     cases["zeroall_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1", PZ_ZERO_SCOPE="all")
     cases["zeroside_dpnone"] = dict(cases["dpnone"], PZ_ZERO="1", PZ_ZERO_SCOPE="side")

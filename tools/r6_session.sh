@@ -1,7 +1,8 @@
 #!/bin/bash
-# round-6 session: the round's two step-level defaults against their switches, 5 interleaved rounds, mlp4
+# round-6 session: world-1 cost of the real RCCL paths (ProcessGroupNCCL vs the native communicator), replicated and
+# sharded optimizer, and the modelled 8-rank step, final r6 tree
 set -e
-out=gpurun_out/r6d15
+out=gpurun_out/r6d16
 mkdir -p $out
-ROUNDS=5 ARGS="--steps 100 --warmup 20" timeout -k 10 1000 tools/ab_bench.sh "r6=" "no_var40=PZ_GEMM_W4=0" "no_prio=PZ_MAIN_PRIO=0" "r5_like=PZ_GEMM_W4=0,PZ_MAIN_PRIO=0" > $out/ab.txt 2>&1
-cat $out/ab.txt
+timeout -k 10 1100 python tools/comm_pressure.py --rounds 2 --steps 60 --wgs 16 --cases torch,native,zero_torch,zero_native,dpnone,zero_dpnone,proxy_w16,zero_proxy_w16 > $out/comm_pressure.txt 2>&1
+tail -9 $out/comm_pressure.txt
