@@ -1,8 +1,9 @@
 #!/bin/bash
-# round-6 session: world-1 cost of the real RCCL paths (ProcessGroupNCCL vs the native communicator), replicated and
-# sharded optimizer, and the modelled 8-rank step, final r6 tree
+# round-6 session: cost of deterministic reductions on the final tree (mlp4), priority stream on fp8 mlp8192
 set -e
-out=gpurun_out/r6d16
+out=gpurun_out/r6d17
 mkdir -p $out
-timeout -k 10 1100 python tools/comm_pressure.py --rounds 2 --steps 60 --wgs 16 --cases torch,native,zero_torch,zero_native,dpnone,zero_dpnone,proxy_w16,zero_proxy_w16 > $out/comm_pressure.txt 2>&1
-tail -9 $out/comm_pressure.txt
+ROUNDS=3 ARGS="--steps 100 --warmup 20" timeout -k 10 900 tools/ab_bench.sh "det=" "nondet=PZ_DETERMINISTIC=0" > $out/ab_det.txt 2>&1
+cat $out/ab_det.txt
+ROUNDS=3 ARGS="--config mlp8192 --steps 100 --warmup 20" timeout -k 10 900 tools/ab_bench.sh "prio=" "noprio=PZ_MAIN_PRIO=0" > $out/ab_fp8_prio.txt 2>&1
+cat $out/ab_fp8_prio.txt
